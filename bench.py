@@ -1,0 +1,302 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: env steps/s (whole node) + achieved HBM GB/s on a batch of 1,048,576 4x4 boards
+per GPU (configs[2]'s batch; the per-GPU shard of configs[4]).
+
+One "step" = one launch of the fused HIP env step (g2048_step) over the whole per-GPU board batch: slide/merge
+(LDS row table) + numpy-PCG64 spawn + reward (fp64) + done/truncation + auto-reset + action mask + log2 obs.
+Inputs are synthetic and resident in HBM before timing: random-state boards (each cell empty w.p. 6/16, else an
+exponent uniform in 1..12, seed 0x2048), actions uniform over 0..3 (seed 1; invalid no-change moves included),
+per-lane seeds seed0 + global lane for auto-reset.  Weak scaling: every GPU owns B boards (lanes
+[rank*B, (rank+1)*B)), no collective on the data path.
+
+    python bench.py [--gpus N --steps K --warmup W --boards B --rng pcg64|philox --obs log2|onehot|raw|none]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  Extras: `roofline` of the step kernel (algorithmic bytes / HIP-event kernel time vs
+8 TB/s; `traffic` = HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes when rocprofv3 is present),
+`cpu_baseline` (the C oracle's env step on host cores, a bounded sample), and `policy_rollout` (env steps/s with
+the [256,256] ReLU policy MLP + on-device sampling in the loop, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env steps/sec (whole node) + achieved HBM GB/s, batch=1M 4x4 boards"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# Algorithmic bytes one g2048_step moves per board in steady state (no reset), by mode.  Reads / writes:
+#   board 8/8, action 1/-, status 1/-, step_count 4/4, max_tile 1/1, score 4/4, reward -/4, flags -/1, mask -/4
+#   PCG64: rng_state 16/16, rng_inc 16/-, rng_buf 8/8          Philox: lane seed 8/-
+#   obs: log2/raw -/64, onehot -/1088
+CORE_R, CORE_W = 8 + 1 + 1 + 4 + 1 + 4, 8 + 4 + 1 + 4 + 4 + 1 + 4
+RNG_BYTES = {"pcg64": (40, 24), "philox": (8, 0)}
+OBS_BYTES = {"none": 0, "raw": 64, "log2": 64, "onehot": 1088}
+
+
+def bytes_per_step(rng: str, obs: str) -> tuple[int, int]:
+    r = CORE_R + RNG_BYTES[rng][0]
+    w = CORE_W + RNG_BYTES[rng][1] + OBS_BYTES[obs]
+    return r, w
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--boards", type=int, default=1 << 20, help="boards per GPU")
+    ap.add_argument("--rng", default="pcg64", choices=["pcg64", "philox"])
+    ap.add_argument("--obs", default="log2", choices=["log2", "onehot", "raw", "none"])
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default="auto", choices=["auto", "off"])
+    ap.add_argument("--no-policy", action="store_true")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------------------------- inputs
+def synthetic_boards(torch, B: int, lane_offset: int, device, seed: int = 0x2048):
+    """Random-state boards: cell empty w.p. 6/16, else exponent uniform over 1..12.
+    A counter hash of (global lane, cell) so shards of an N-GPU run are slices of the 1-GPU global batch."""
+    M = 0x7FFFFFFFFFFFFFFF
+    idx = (torch.arange(B * 16, dtype=torch.int64, device=device) + lane_offset * 16) ^ seed
+    h = idx * -0x61C8864680B583EB - 0x61C8864680B583EB  # splitmix64 (0x9E3779B97F4A7C15 as int64), wraps
+    h = (h ^ ((h >> 30) & (M >> 29))) * -0x40A7B892E31B1A47
+    h = (h ^ ((h >> 27) & (M >> 26))) * -0x6B2FB644ECCEEE15
+    h = h ^ ((h >> 31) & (M >> 30))
+    u = h & 0xFFFF
+    exps = torch.where((u & 15) < 6, torch.zeros_like(u), 1 + ((u >> 4) % 12)).view(B, 16)
+    shifts = torch.arange(0, 64, 4, dtype=torch.int64, device=device)
+    return (exps << shifts).sum(dim=1)
+
+
+def make_env(torch, args, B, lane_offset, device):
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+    from rl2048_amd import _lib as L
+
+    cfg = Game2048EnvConfig(obs_mode="log2" if args.obs == "none" else args.obs, obs_log2_scale=0.0625,
+                            reward_mode="log2", base_reward_scale=0.5, max_steps=1024)
+    env = VecGame2048Env(B, cfg, device=device, rng=args.rng, auto_reset=True,
+                         reset_stride=B * max(args.gpus, 1), lane_offset=lane_offset)
+    if args.obs == "none":
+        env._out.obs = None
+    env.seed.copy_(torch.arange(B, dtype=torch.int64, device=device) + (1_000_003 + lane_offset))
+    if env.rng_mode == L.RNG_PCG64:
+        L.check(L.lib().g2048_seed_pcg64(L.ptr(env.seed), L.ptr(env.rng_state), L.ptr(env.rng_inc),
+                                         L.ptr(env.rng_buf), B, L.stream_handle(device)))
+    env.board.copy_(synthetic_boards(torch, B, lane_offset, device))
+    env.status.fill_(L.S_ACTIVE)
+    env.max_tile.fill_(2)
+    return env
+
+
+# ---------------------------------------------------------------------------------------------- PMC traffic
+def pmc_traffic(args) -> dict | None:
+    """Run this benchmark twice under rocprofv3 (separate FETCH_SIZE and WRITE_SIZE passes, kernel-trace only,
+    per MI355X_MICROARCH.md 'HBM') and return HBM bytes per step-kernel launch.  FETCH_SIZE is doubled: on
+    gfx950 it reports half the bytes of coalesced streaming reads."""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None
+    vals = {}
+    base = os.path.join(ROOT, "gpurun_out", "pmc") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        out = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir=base)
+        cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "pmc", "--", sys.executable,
+               os.path.abspath(__file__), "--pmc-child", "--steps", "10", "--warmup", "3", "--boards",
+               str(args.boards), "--rng", args.rng, "--obs", args.obs]
+        try:
+            subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        except Exception:  # noqa: BLE001 -- traffic is optional; report null on any profiler failure
+            return None
+        rows = []
+        for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+            import csv
+
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if "step_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                        rows.append(float(row["Counter_Value"]))
+        if not rows:
+            return None
+        vals[counter] = sum(rows[1:] if len(rows) > 1 else rows) / max(len(rows) - 1, 1)
+    fetch_b = vals["FETCH_SIZE"] * 1024.0 * 2.0
+    write_b = vals["WRITE_SIZE"] * 1024.0
+    return {"fetch_bytes": fetch_b, "write_bytes": write_b, "bytes": fetch_b + write_b}
+
+
+# ---------------------------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(args, seconds: float) -> dict:
+    from oracle import oracle as O
+
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = max(1, min(cores, 16))
+    os.environ["OMP_NUM_THREADS"] = str(cores)
+    cfg = dict(obs_mode="log2" if args.obs == "none" else args.obs, obs_log2_scale=0.0625, reward_mode="log2",
+               base_reward_scale=0.5, max_steps=1024)
+    boards = 64 * cores
+    t0 = time.perf_counter()
+    steps, _ = O.bench_env_steps(boards, 32, **cfg)
+    dt = time.perf_counter() - t0
+    rounds = max(32, int(32 * seconds / max(dt, 1e-6)))
+    t0 = time.perf_counter()
+    steps, _ = O.bench_env_steps(boards, rounds, **cfg)
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env steps/s", "cores": cores, "kind": "port",
+            "sample": f"C oracle (oracle/g2048_oracle.c, literal restatement of src/game2048.py + src/env.py step, "
+                      f"{args.obs} obs + action mask, numpy-PCG64 spawn) {boards} boards x {rounds} steps = "
+                      f"{steps} env steps in {dt:.1f} s, OpenMP over boards"}
+
+
+# ---------------------------------------------------------------------------------------------- policy loop
+def policy_rollout_rate(torch, B: int, device, steps: int = 20, warmup: int = 5) -> dict:
+    """Env steps/s with the runner-default policy in the loop: MLP [256,256] ReLU HeNormal (fp32, hipBLASLt) on
+    log2 obs -> fused masked-softmax + numpy-PCG64 choice kernel -> fused env step (auto-reset)."""
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+    from rl2048_amd import _lib as L
+    from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
+    from rl2048_amd.mlp import MLPConfig
+
+    cfg = Game2048EnvConfig(obs_mode="log2", obs_log2_scale=0.0625, reward_mode="log2", base_reward_scale=0.5)
+    agent = ReinforceAgent(cfg, MLPConfig(hidden_sizes=[256, 256], activation="ReLU", init_distribution="HeNormal"),
+                           ReinforceAgentConfig(), device=device)
+    env = VecGame2048Env(B, cfg, device=device, auto_reset=True)
+    env.reset(seed=7)
+    lib = L.lib()
+    st = torch.empty(2 * B, dtype=torch.int64, device=device)
+    inc = torch.empty(2 * B, dtype=torch.int64, device=device)
+    buf = torch.empty(B, dtype=torch.int64, device=device)
+    seeds = torch.arange(B, dtype=torch.int64, device=device) + 99
+    stream = L.stream_handle(device)
+    L.check(lib.g2048_seed_pcg64(L.ptr(seeds), L.ptr(st), L.ptr(inc), L.ptr(buf), B, stream))
+    acts = torch.empty(B, dtype=torch.uint8, device=device)
+
+    def one():
+        logits = agent._policy_logits(env.obs)
+        L.check(lib.g2048_sample(L.ptr(logits), L.ptr(env.mask), None, 0, 0, L.ptr(st), L.ptr(inc), L.ptr(buf), 0,
+                                 None, None, None, L.ptr(acts), B, stream))
+        env.step_into(acts)
+
+    with torch.no_grad():
+        for _ in range(warmup):
+            one()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    return {"value": steps * B / dt, "unit": "env steps/s", "boards": B, "steps": steps,
+            "ms_per_step": dt / steps * 1e3, "model": "MLP 16-256-256-4 ReLU fp32 (runner.py defaults)"}
+
+
+# ---------------------------------------------------------------------------------------------- main
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        args.gpus = world
+    # profiler passes and the CPU baseline run before this process touches the GPU
+    traffic = None
+    if rank == 0 and world == 1 and not args.pmc_child and args.traffic == "auto":
+        traffic = pmc_traffic(args)
+    cpu = None
+    if rank == 0 and world == 1 and not args.pmc_child and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, args.cpu_baseline_seconds)
+
+    import torch
+    import torch.distributed as dist
+
+    import rl2048_amd  # noqa: F401
+
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    B = args.boards
+    env = make_env(torch, args, B, rank * B, device)
+    K, W = args.steps, args.warmup
+    g = torch.Generator(device=device)
+    g.manual_seed(1 + rank)
+    actions = torch.randint(0, 4, (K + W, B), dtype=torch.uint8, device=device, generator=g)
+    for k in range(W):
+        env.step_into(actions[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev[k][0].record()
+        env.step_into(actions[W + k])
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / K
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    if args.pmc_child:
+        return
+    policy = None
+    if rank == 0 and world == 1 and not args.no_policy:
+        try:
+            del actions
+            torch.cuda.empty_cache()
+            policy = policy_rollout_rate(torch, B, device)
+        except Exception as e:  # noqa: BLE001 -- an extra, never the headline
+            policy = {"error": repr(e)}
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank != 0:
+        return
+    rb, wb = bytes_per_step(args.rng, args.obs)
+    alg_bytes = (rb + wb) * B
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    total_steps = K * B * world
+    line = {
+        "metric": METRIC, "value": total_steps / elapsed, "unit": "env steps/s", "n_gpus": world, "steps": K,
+        "warmup": W, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": f"g2048_step over {B:,} random-state boards per GPU (configs[2] batch): "
+                               f"slide/merge + {args.rng} spawn + fp64 reward + done/trunc + auto-reset + mask + "
+                               f"{args.obs} obs, uniform random actions incl. invalid",
+                   "boards_per_gpu": B, "global_boards": B * world, "rng": args.rng, "obs": args.obs,
+                   "parallelism": f"dp{world} (board shards, no data-path collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic["bytes"] if traffic else None,
+                     "algorithmic_bytes_per_launch": alg_bytes, "bytes_per_board_step": rb + wb,
+                     "kernel_ms": kern_ms, "kernel": "step_kernel (g2048_step)"},
+        "cpu_baseline": cpu,
+    }
+    if traffic:
+        line["roofline"]["traffic_detail"] = traffic
+    if policy is not None:
+        line["policy_rollout"] = policy
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

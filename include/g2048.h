@@ -1,0 +1,174 @@
+/*
+ * g2048.h -- C ABI of libg2048.so, the MI355X (gfx950) HIP implementation of the 2048 hot path of
+ * pqpeqr/RL-2048-with-Reinforce-and-Actor-Critic.
+ *
+ * The reference is pure Python/NumPy and exposes no FFI; its boundary for this path is its Python API.  Each
+ * entry point below replaces the reference interface cited next to it, batched over n boards ("lanes").
+ * The Python host layer (rl-2048-with-reinforce-and-actor-critic_amd/) binds these with ctypes and mirrors
+ * the reference's classes and error behaviour on top (INTEGRATION.md shows the binding).
+ *
+ * Conventions (all entry points):
+ *   - Every pointer argument that names a buffer is a DEVICE pointer owned by the caller (torch tensors in
+ *     practice).  The library never allocates caller buffers; it owns only its row lookup table.
+ *   - Calls are asynchronous and ordered on `stream` (a hipStream_t; NULL = the default stream).  Nothing
+ *     synchronises the host.  Calls on different streams are independent (reentrant).
+ *   - Return value: G2048_OK or an error code; g2048_last_error() gives a thread-local message.  Bad
+ *     arguments are rejected before any launch (the Python layer turns them into ValueError /
+ *     AssertionError exactly where the reference raises).  Per-lane conditions (invalid action, tile
+ *     overflow) never abort: they are reported in the per-lane flags.
+ *   - Board encoding ("bitboard"): one uint64 per board, nibble (r*4+c) holds log2(tile) (0 = empty).
+ *     A tile of 2**15 merging with another 2**15 (the reference's int64 board would hold 65536) saturates
+ *     at 2**15 and raises G2048_F_OVERFLOW; rewards/score still use the true merged value.
+ *   - Actions: 0 up, 1 right, 2 down, 3 left (src/game2048.py:9).
+ */
+#ifndef G2048_H
+#define G2048_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define G2048_ABI_VERSION 1
+
+/* status codes */
+#define G2048_OK 0
+#define G2048_EINVAL 1   /* bad argument (null required buffer, bad mode, n < 0) */
+#define G2048_EHIP 2     /* HIP runtime error (message in g2048_last_error) */
+#define G2048_ENOINIT 3  /* g2048_init() not called for the current device */
+
+/* observation encodings: Game2048EnvConfig.obs_mode (src/env.py:23, :131-150) */
+#define G2048_OBS_NONE (-1)
+#define G2048_OBS_RAW 0
+#define G2048_OBS_LOG2 1
+#define G2048_OBS_ONEHOT 2     /* 17 channels per cell, index (r*4+c)*17 + log2(tile) */
+
+/* spawn / policy random streams */
+#define G2048_RNG_PCG64 0      /* numpy default_rng(seed) bit-exact (parity mode) */
+#define G2048_RNG_PHILOX 1     /* Philox4x32-10, counter = (lane seed, step, tag): throughput mode */
+
+/* per-lane step flags (uint8) */
+#define G2048_F_CHANGED 0x01     /* Game2048.step is_changed */
+#define G2048_F_TERMINATED 0x02  /* is_done -> Game2048Env.step terminated */
+#define G2048_F_TRUNCATED 0x04   /* step_count >= max_steps and not terminated */
+#define G2048_F_INVALID 0x08     /* Game2048Env.step info["invalid_action"] = not changed and not done */
+#define G2048_F_OVERFLOW 0x10    /* a 2**15 + 2**15 merge saturated (see encoding note) */
+#define G2048_F_RESET 0x20       /* lane finished and was auto-reset in this call */
+#define G2048_F_INACTIVE 0x40    /* lane was already finished (no auto-reset): nothing happened */
+#define G2048_F_BADACTION 0x80   /* action outside 0..3: lane untouched (reference raises) */
+
+/* lane status bits (g2048_lanes.status) */
+#define G2048_S_ACTIVE 0x01
+
+/* Game2048EnvConfig (src/env.py:19-40).  size is fixed at 4. */
+typedef struct g2048_env_cfg {
+    int32_t obs_mode;              /* G2048_OBS_* */
+    int32_t reward_mode;           /* 0 "sum", 1 "log2" */
+    int32_t bonus_mode;            /* 0 "off", 1 "raw", 2 "log2" */
+    int32_t use_action_mask;       /* bool */
+    float obs_log2_scale;
+    int32_t _pad0;
+    double base_reward_scale;
+    double empty_tile_reward;
+    double merge_reward;
+    double bonus_scale;
+    double step_reward;
+    double endgame_penalty;
+    double invalid_action_penalty;
+    int64_t max_steps;             /* < 0 means None */
+} g2048_env_cfg;
+
+/* Per-lane environment state, structure-of-arrays, each array of length n (rng_* of length 2n). */
+typedef struct g2048_lanes {
+    uint64_t* board;       /* Game2048.board as a bitboard */
+    uint32_t* step_count;  /* Game2048Env._step_count (== Game2048.step_count) */
+    uint32_t* score;       /* Game2048.score */
+    uint8_t* max_tile;     /* log2(Game2048Env.max_tile_seen) */
+    uint8_t* status;       /* G2048_S_* */
+    uint64_t* seed;        /* seed of the lane's current episode (Game2048.reset(seed)) */
+    uint64_t* rng_state;   /* PCG64 128-bit state, (lo, hi) per lane            [PCG64 mode only] */
+    uint64_t* rng_inc;     /* PCG64 128-bit increment, (lo, hi) per lane        [PCG64 mode only] */
+    uint64_t* rng_buf;     /* PCG64 next_uint32 buffer: has_uint32 << 32 | uinteger [PCG64 mode only] */
+} g2048_lanes;
+
+/* Outputs of one step.  reward and flags are required; the others may be NULL. */
+typedef struct g2048_step_out {
+    float* reward;         /* [n] Game2048Env._compute_reward (computed in fp64, stored fp32) */
+    uint8_t* flags;        /* [n] G2048_F_* */
+    int8_t* mask;          /* [n*4] obs["action_mask"] of the resulting board (src/env.py:154-156) */
+    float* obs;            /* [n*16] or [n*272] obs["board"] of the resulting board, cfg.obs_mode */
+    uint32_t* merged;      /* [n] merged tiles of this step in the reference's list order, as nibbles
+                              (log2(v) - 1), first merge in the lowest nibble, 0-terminated (<= 8) */
+    uint64_t* prev_board;  /* [n] the board before the step (trajectory record) */
+} g2048_step_out;
+
+/* ---------------------------------------------------------------------------------------------------- */
+
+int g2048_abi_version(void);
+const char* g2048_last_error(void);
+
+/* Build the 65,536-entry row table (move-left of every 4-nibble line) in the memory of `device`.
+ * Idempotent and thread-safe.  Replaces the per-row Python loop of Game2048._row_move_left
+ * (src/game2048.py:120-137). */
+int g2048_init(int device);
+
+/* Seed PCG64 streams exactly like np.random.default_rng(seed[i]) (numpy SeedSequence -> PCG64).
+ * Replaces Game2048._set_seed (src/game2048.py:102-106) and default_rng(policy_seed)
+ * (src/reinforce_agent.py:211).  rng_state / rng_inc: [2n] (lo, hi); rng_buf: [n]. */
+int g2048_seed_pcg64(const uint64_t* seeds, uint64_t* rng_state, uint64_t* rng_inc, uint64_t* rng_buf,
+                     int64_t n, void* stream);
+
+/* Reset lanes: Game2048Env.reset(seed=...) (src/env.py:174-194) -> Game2048.reset (src/game2048.py:26-34).
+ * seeds: [n] or NULL (NULL keeps lanes->seed); reset_mask: [n] (nonzero = reset this lane) or NULL (all).
+ * mask_out [n*4] / obs_out (cfg->obs_mode) may be NULL. */
+int g2048_reset(const g2048_lanes* lanes, const uint64_t* seeds, const uint8_t* reset_mask,
+                const g2048_env_cfg* cfg, int rng_mode, uint64_t philox_key, int8_t* mask_out, float* obs_out,
+                int64_t n, void* stream);
+
+/* One environment step of every lane: Game2048Env.step(action) (src/env.py:264-302) with
+ * Game2048.step (src/game2048.py:40-70) and the reward of _compute_reward (src/env.py:197-261).
+ * actions: [n] uint8.  auto_reset != 0: a lane that terminates or truncates is reset in the same call with
+ * seed += reset_stride (flag G2048_F_RESET; obs/mask then describe the new episode).  auto_reset == 0: the
+ * lane is marked inactive and later calls leave it untouched (G2048_F_INACTIVE). */
+int g2048_step(const g2048_lanes* lanes, const uint8_t* actions, const g2048_env_cfg* cfg,
+               const g2048_step_out* out, int rng_mode, uint64_t philox_key, int auto_reset,
+               uint64_t reset_stride, int64_t n, void* stream);
+
+/* Observation + action mask of a board array (src/env.py:131-159 with src/MLP.py:22-43 flattening and
+ * Game2048.get_action_mask src/game2048.py:95-99).  obs may be NULL (mask only), mask may be NULL. */
+int g2048_obs(const uint64_t* boards, int obs_mode, float obs_log2_scale, float* obs, int8_t* mask, int64_t n,
+              void* stream);
+
+/* Pre-spawn move only: Game2048._move (src/game2048.py:158-165) for KATs.  out_board [n]; merged [n] as
+ * in g2048_step_out; flags [n] gets G2048_F_CHANGED / G2048_F_OVERFLOW / G2048_F_BADACTION. */
+int g2048_move(const uint64_t* boards, const uint8_t* actions, uint64_t* out_board, uint32_t* merged,
+               uint8_t* flags, int64_t n, void* stream);
+
+/* Policy head: logits_to_probs (src/MLP.py:139-156) + action choice of ReinforceAgent.select_action
+ * (src/reinforce_agent.py:178-190).  logits [n*4] fp32, mask [n*4] int8 (NULL = no mask).
+ * greedy != 0: argmax(probs * mask).  Otherwise rng_mode PCG64: Generator.choice(4, p=probs) on the lane's
+ * stream (rng_* as in g2048_seed_pcg64); PHILOX: inverse-CDF on a Philox draw keyed (philox_key, lane_seed[i],
+ * counter[i]).  active: [n] (NULL = all); inactive lanes are left untouched.  probs_out [n*4] may be NULL. */
+int g2048_sample(const float* logits, const int8_t* mask, const uint8_t* active, int greedy, int rng_mode,
+                 uint64_t* rng_state, uint64_t* rng_inc, uint64_t* rng_buf, uint64_t philox_key,
+                 const uint64_t* lane_seed, const uint32_t* counter, float* probs_out, uint8_t* actions,
+                 int64_t n, void* stream);
+
+/* Discounted returns per episode (ReinforceAgent.compute_returns src/reinforce_agent.py:255-273):
+ * rewards / returns are time-major [T, n] fp32 (lane i's episode occupies rows 0..lengths[i]-1); the scan is
+ * accumulated in fp64 like the reference's Python float and stored as fp32. */
+int g2048_returns(const float* rewards, const int32_t* lengths, double gamma, float* returns, int64_t T,
+                  int64_t n, void* stream);
+
+/* The 8 dihedral symmetries of Game2048Env.get_symmetries (src/env.py:317-398) on bitboards:
+ * boards [n] -> out_boards [8n] (symmetry-major: out[k*n + i]); actions [n] -> out_actions [8n] (NULL ok);
+ * masks are recomputed from the transformed boards by g2048_obs. */
+int g2048_symmetries(const uint64_t* boards, const uint8_t* actions, uint64_t* out_boards, uint8_t* out_actions,
+                     int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* G2048_H */

@@ -219,7 +219,7 @@ def make_env_cfg(**kw) -> EnvCfg:
     for k in ("obs_log2_scale", "base_reward_scale", "empty_tile_reward", "merge_reward", "bonus_scale",
               "step_reward", "endgame_penalty", "invalid_action_penalty"):
         setattr(c, k, float(d[k]))
-    c.max_steps = 0 if d["max_steps"] is None else int(d["max_steps"])
+    c.max_steps = -1 if d["max_steps"] is None else max(int(d["max_steps"]), 0)
     return c
 
 

@@ -1,0 +1,141 @@
+"""ctypes binding of libg2048.so (include/g2048.h) -- the only way this package reaches the GPU.
+
+There is no fallback: if the library is missing, or no HIP device is present, every entry point raises.
+torch is imported before the library is opened so that the library's libamdhip64 dependency resolves to the
+HIP runtime torch already loaded (same SONAME), i.e. one HIP context shared with torch's allocator/streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+import torch
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_ROOT = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "libg2048.so")
+SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
+INCLUDE = os.path.join(REPO_ROOT, "include")
+ABI_VERSION = 1
+
+# include/g2048.h constants
+OBS_NONE, OBS_RAW, OBS_LOG2, OBS_ONEHOT = -1, 0, 1, 2
+RNG_PCG64, RNG_PHILOX = 0, 1
+F_CHANGED, F_TERMINATED, F_TRUNCATED, F_INVALID = 0x01, 0x02, 0x04, 0x08
+F_OVERFLOW, F_RESET, F_INACTIVE, F_BADACTION = 0x10, 0x20, 0x40, 0x80
+S_ACTIVE = 0x01
+G2048_OK, G2048_EINVAL, G2048_EHIP, G2048_ENOINIT = 0, 1, 2, 3
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libg2048.so for gfx950 in-tree (hipcc cross-compiles; no GPU needed)."""
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-I" + INCLUDE,
+           "-I" + os.path.dirname(SRC), "-o", LIB_PATH, SRC]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
+    if verbose:
+        print(" ".join(cmd))
+    return LIB_PATH
+
+
+class EnvCfg(ctypes.Structure):
+    _fields_ = [("obs_mode", ctypes.c_int32), ("reward_mode", ctypes.c_int32), ("bonus_mode", ctypes.c_int32),
+                ("use_action_mask", ctypes.c_int32), ("obs_log2_scale", ctypes.c_float), ("_pad0", ctypes.c_int32),
+                ("base_reward_scale", ctypes.c_double), ("empty_tile_reward", ctypes.c_double),
+                ("merge_reward", ctypes.c_double), ("bonus_scale", ctypes.c_double), ("step_reward", ctypes.c_double),
+                ("endgame_penalty", ctypes.c_double), ("invalid_action_penalty", ctypes.c_double),
+                ("max_steps", ctypes.c_int64)]
+
+
+class Lanes(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in
+                ("board", "step_count", "score", "max_tile", "status", "seed", "rng_state", "rng_inc", "rng_buf")]
+
+
+class StepOut(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in ("reward", "flags", "mask", "obs", "merged", "prev_board")]
+
+
+_lib = None
+_lock = threading.Lock()
+_inited_devices: set[int] = set()
+
+
+def _declare(L):
+    vp, i64, u64, i32, d, f = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_float
+    P = ctypes.POINTER
+    L.g2048_abi_version.restype = ctypes.c_int
+    L.g2048_last_error.restype = ctypes.c_char_p
+    L.g2048_init.argtypes = [i32]
+    L.g2048_seed_pcg64.argtypes = [vp, vp, vp, vp, i64, vp]
+    L.g2048_reset.argtypes = [P(Lanes), vp, vp, P(EnvCfg), i32, u64, vp, vp, i64, vp]
+    L.g2048_step.argtypes = [P(Lanes), vp, P(EnvCfg), P(StepOut), i32, u64, i32, u64, i64, vp]
+    L.g2048_obs.argtypes = [vp, i32, f, vp, vp, i64, vp]
+    L.g2048_move.argtypes = [vp, vp, vp, vp, vp, i64, vp]
+    L.g2048_sample.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp, u64, vp, vp, vp, vp, i64, vp]
+    L.g2048_returns.argtypes = [vp, vp, d, vp, i64, i64, vp]
+    L.g2048_symmetries.argtypes = [vp, vp, vp, vp, i64, vp]
+    for name in ("g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step", "g2048_obs", "g2048_move",
+                 "g2048_sample", "g2048_returns", "g2048_symmetries"):
+        getattr(L, name).restype = ctypes.c_int
+
+
+EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g2048_seed_pcg64", "g2048_reset",
+                    "g2048_step", "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries")
+
+
+def lib():
+    """Open libg2048.so (no device work).  Raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+            L = ctypes.CDLL(LIB_PATH)
+            _declare(L)
+            v = L.g2048_abi_version()
+            if v != ABI_VERSION:
+                raise RuntimeError(f"libg2048.so ABI {v} != expected {ABI_VERSION}; rebuild")
+            _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc == G2048_OK:
+        return
+    msg = lib().g2048_last_error().decode(errors="replace")
+    if rc == G2048_EINVAL:
+        raise ValueError(msg)
+    raise RuntimeError(f"libg2048 error {rc}: {msg}")
+
+
+def ensure_device(device: torch.device) -> None:
+    """g2048_init for `device` (builds the row table there).  Fails loudly without a HIP device."""
+    if device.type != "cuda":
+        raise RuntimeError(f"the 2048 hot path runs on a HIP device only (got {device}); there is no CPU fallback")
+    if not torch.cuda.is_available():
+        raise RuntimeError("no HIP device visible: the 2048 hot path has no CPU fallback")
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx in _inited_devices:
+        return
+    with _lock:
+        if idx not in _inited_devices:
+            check(lib().g2048_init(idx))
+            _inited_devices.add(idx)
+
+
+def stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("buffers passed to libg2048 must be contiguous")
+    return t.data_ptr()

@@ -1,0 +1,629 @@
+"""ReinforceAgent (src/reinforce_agent.py) on the MI355X path.
+
+Two faces over one implementation:
+
+* the reference's API, unchanged in names / arguments / results -- ``select_action``, ``run_episode``,
+  ``compute_returns``, ``update_batch(trajectories: list[dict])``, ``load_model`` / ``save_model``,
+  ``clip_grads_global_norm``;
+* the batched hot path -- ``rollout_batch(env_seeds, policy_seeds)`` plays every episode of a batch in its own
+  device lane (VecGame2048Env + the fused masked-softmax/choice kernel) and records a time-major device
+  trajectory buffer; ``update_from_batch(batch)`` applies exactly the update of ``update_batch`` to it.
+
+The update is the reference's per-timestep manual backprop (src/reinforce_agent.py:502-555, :639-678) restated
+as batched autograd over all valid steps: the actor's logit gradient is A_t * (onehot(a_t) - pi(.|s_t)) scaled by
+rank_w / (T_i * n) and back-propagated through the MLP (identical to summing the reference's per-step outer
+products); the critic's is the (MSE or Huber) TD gradient with the same weights.  Gradient clipping, SGD ascent /
+descent and Adam follow :558-582, :719-770, :835-861.
+
+Data parallel: when torch.distributed is initialised each rank holds a shard of the batch's episodes; rank
+weights all-gather the episode totals, the batch baselines all-reduce three scalars, and the actor+critic
+gradients travel in ONE fused all-reduce (RCCL over xGMI on MI355X) before clipping, so every rank applies the
+update of the concatenated batch.
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+from dataclasses import dataclass
+from typing import Any, Callable, Literal
+
+import numpy as np
+import torch
+from . import _lib as L
+from . import dp
+from .config import Game2048EnvConfig, obs_width
+from .mlp import (MLPConfig, encode_observation, forward_logits, init_model_params, load_model_params,
+                  logits_to_probs, save_model_params)
+from .vec_env import VecGame2048Env
+
+BaselineMode = Literal["off", "each", "batch", "batch_norm"]
+OptimizerType = Literal["sgd", "adam"]
+CriticLossType = Literal["mse", "huber"]
+
+_OBS_CODE = {"raw": L.OBS_RAW, "log2": L.OBS_LOG2, "onehot": L.OBS_ONEHOT}
+
+
+@dataclass
+class ReinforceAgentConfig:
+    gamma: float = 1
+    learning_rate: float = 1e-3
+    baseline_mode: BaselineMode = "off"
+    model_seed: int = 0
+    reward_rank_weights: list[float] | None = None
+    optimizer: OptimizerType = "sgd"
+    adam_beta1: float = 0.9
+    adam_beta2: float = 0.999
+    augmentation: bool = False
+    use_critic: bool = False
+    critic_learning_rate: float = 1e-3
+    max_grad_norm: float = 1.0
+    critic_loss_type: CriticLossType = "mse"
+    huber_delta: float = 1.0
+
+
+@dataclass
+class TrajectoryBatch:
+    """Device trajectory buffer of one batch of episodes, time-major: row t, column = episode (lane).
+    boards[t, i] is the board BEFORE action actions[t, i]; rewards[t, i] its reward; valid iff t < lengths[i]."""
+    boards: torch.Tensor       # [T, n] int64 bitboards
+    actions: torch.Tensor      # [T, n] uint8
+    rewards: torch.Tensor      # [T, n] float32
+    flags: torch.Tensor        # [T, n] uint8 (G2048_F_*)
+    lengths: torch.Tensor      # [n] int32
+    total_reward: torch.Tensor  # [n] float64
+    max_tile: torch.Tensor     # [n] int64 (Game2048Env.max_tile_seen at the end of the episode)
+    final_boards: torch.Tensor  # [n] int64
+    probs: torch.Tensor | None = None  # [T, n, 4] policy probabilities used for each draw (record_probs=True)
+
+    @property
+    def n(self) -> int:
+        return int(self.lengths.numel())
+
+    @property
+    def T(self) -> int:
+        return int(self.boards.shape[0])
+
+
+def _render_values(vals: np.ndarray) -> str:
+    from .env import _render
+
+    return _render(vals.tolist())
+
+
+def _board_values(b: int) -> np.ndarray:
+    e = np.array([(b >> (4 * i)) & 15 for i in range(16)], dtype=np.int64).reshape(4, 4)
+    return np.where(e > 0, np.left_shift(np.int64(1), e), 0).astype(np.int64)
+
+
+class _Steps:
+    """The valid steps of a batch in time-major order plus how to build their MLP inputs.
+
+    Feature source is either bitboards (batched path: obs / mask built on the fly by g2048_obs, symmetries by
+    g2048_symmetries) or host-provided features (drop-in update_batch on reference trajectories)."""
+
+    def __init__(self, agent: "ReinforceAgent", lengths: torch.Tensor, actions: torch.Tensor, rewards: torch.Tensor,
+                 boards: torch.Tensor | None = None, X: torch.Tensor | None = None, M: torch.Tensor | None = None):
+        dev = agent.device
+        self.agent = agent
+        self.T, self.n = rewards.shape
+        self.lengths = lengths.to(dev, torch.int64)
+        t_idx = torch.arange(self.T, device=dev).unsqueeze(1)
+        valid = t_idx < self.lengths.unsqueeze(0)                     # [T, n]
+        self.vidx = valid.reshape(-1).nonzero().squeeze(1)             # flat t*n + lane, time-major
+        self.lane = self.vidx % self.n
+        self.t = self.vidx // self.n
+        self.has_next = (self.t + 1) < self.lengths[self.lane]
+        self.actions = actions.reshape(-1)[self.vidx].to(torch.int64)
+        self.rewards = rewards.reshape(-1)[self.vidx].to(torch.float32)
+        self.rewards_tm = rewards
+        self.boards = boards
+        self.X = X
+        self.M = M
+        self.N = int(self.vidx.numel())
+
+    # ---------------------------------------------------------------- features of flat time-major indices
+    def _board_obs(self, flat: torch.Tensor, k: int):
+        b = self.boards.reshape(-1)[flat].contiguous()
+        if k:
+            b = self.agent._symmetry_boards(b, k)
+        return self.agent._obs_from_boards(b)
+
+    def features(self, sel: torch.Tensor, k: int = 0, nxt: bool = False):
+        """(x [m, D] f32, mask [m, 4] int8) of the valid steps `sel` (indices into vidx), symmetry k, or of
+        their successor step (nxt=True)."""
+        flat = self.vidx[sel] + (self.n if nxt else 0)
+        if self.boards is not None:
+            return self._board_obs(flat, k)
+        x = self.X.reshape(self.T * self.n, -1)[flat]
+        m = self.M.reshape(self.T * self.n, 4)[flat] if self.M is not None else None
+        if k:
+            x, m = self.agent._symmetry_features(x, m, k)
+        return x, m
+
+    def actions_k(self, sel: torch.Tensor, k: int) -> torch.Tensor:
+        a = self.actions[sel]
+        if k == 0:
+            return a
+        if k >= 4:
+            a = torch.where(a == 1, 3, torch.where(a == 3, 1, a))
+        return (a - (k & 3)) % 4
+
+
+class ReinforceAgent:
+    def __init__(self, env, mlp_config: MLPConfig, agent_config: ReinforceAgentConfig | None = None,
+                 initial_params_path: str | None = None, device=None, chunk_steps: int = 1 << 18):
+        """env: a Game2048Env (drop-in, src/reinforce_agent.py:51-105) or a Game2048EnvConfig."""
+        if isinstance(env, Game2048EnvConfig):
+            self.env = None
+            self.env_config = env
+        else:
+            self.env = env
+            self.env_config = env.config
+        self.mlp_config = mlp_config
+        self.agent_config = agent_config or ReinforceAgentConfig()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        L.ensure_device(self.device)
+        self.rng = np.random.default_rng(self.agent_config.model_seed)
+        self._logger = logging.getLogger(__name__ + ".ReinforceAgent")
+        if not self._logger.handlers:
+            self._logger.addHandler(logging.NullHandler())
+        if self.env is not None:
+            self.env.reset(seed=0)       # the reference probes input_dim this way (src/reinforce_agent.py:70)
+        self.input_dim = obs_width(self.env_config.obs_mode)
+        self.n_actions = 4
+        if initial_params_path is None:
+            self.params = init_model_params(self.input_dim, self.mlp_config.hidden_sizes, self.n_actions, self.rng,
+                                            self.mlp_config.init_distribution, self.mlp_config.last_init_normal,
+                                            device=self.device)
+        else:
+            self.params = load_model_params(initial_params_path, device=self.device)
+        self._init_adam(self.params, prefix="actor")
+        self._adam_t = 0
+        self.critic_params = None
+        if self.agent_config.use_critic:
+            self.critic_params = init_model_params(self.input_dim, self.mlp_config.hidden_sizes, 1, self.rng,
+                                                   self.mlp_config.init_distribution,
+                                                   self.mlp_config.last_init_normal, device=self.device)
+            self._init_adam(self.critic_params, prefix="critic")
+            self._adam_t_c = 0
+        self.chunk_steps = int(chunk_steps)
+        self._vec_cache: dict = {}
+        self._lib = L.lib()
+        self.last_stats: dict = {}
+
+    # ============================================================================================ model I/O
+    def load_model(self, file_path: str = "params.npz") -> None:
+        """src/reinforce_agent.py:108-116"""
+        self.params = load_model_params(file_path, device=self.device)
+        self.mlp_config.hidden_sizes = [int(W.shape[1]) for W in self.params["W"][:-1]]
+        self._logger.info(f"Model parameters loaded from {file_path}")
+
+    def save_model(self, file_path: str = "params.npz") -> None:
+        """src/reinforce_agent.py:119-123"""
+        save_model_params(self.params, file_path)
+
+    # ============================================================================================ helpers
+    @property
+    def _stream(self) -> int:
+        return L.stream_handle(self.device)
+
+    def _obs_from_boards(self, boards: torch.Tensor):
+        m = boards.numel()
+        x = torch.empty(m, self.input_dim, dtype=torch.float32, device=self.device)
+        mk = torch.empty(m, 4, dtype=torch.int8, device=self.device)
+        L.check(self._lib.g2048_obs(L.ptr(boards), _OBS_CODE[self.env_config.obs_mode],
+                                    float(self.env_config.obs_log2_scale), L.ptr(x), L.ptr(mk), m, self._stream))
+        return x, mk
+
+    def _symmetry_boards(self, boards: torch.Tensor, k: int) -> torch.Tensor:
+        m = boards.numel()
+        out = torch.empty(8 * m, dtype=torch.int64, device=self.device)
+        L.check(self._lib.g2048_symmetries(L.ptr(boards), None, L.ptr(out), None, m, self._stream))
+        return out[k * m:(k + 1) * m]
+
+    def _symmetry_features(self, x: torch.Tensor, m: torch.Tensor | None, k: int):
+        """get_symmetries (src/env.py:317-398) on host-provided features: board [.,4,4(,17)] and mask."""
+        onehot = x.shape[1] == 272
+        b = x.view(-1, 4, 4, 17) if onehot else x.view(-1, 4, 4)
+        if k >= 4:
+            b = torch.flip(b, dims=[2])
+            if m is not None:
+                m = m[:, [0, 3, 2, 1]]
+        for _ in range(k & 3):
+            b = torch.rot90(b, k=1, dims=(1, 2))
+            if m is not None:
+                m = torch.roll(m, shifts=-1, dims=1)
+        return b.reshape(x.shape[0], -1).contiguous(), m
+
+    def _vec_env(self, n: int, rng: str) -> VecGame2048Env:
+        key = (n, rng)
+        if key not in self._vec_cache:
+            self._vec_cache.clear()
+            self._vec_cache[key] = VecGame2048Env(n, self.env_config, device=self.device, rng=rng)
+        return self._vec_cache[key]
+
+    def _policy_logits(self, x: torch.Tensor) -> torch.Tensor:
+        return forward_logits(self.params, x, self.mlp_config.activation, keep_cache=False)[0]
+
+    # ============================================================================================ acting
+    def select_action(self, obs, rng: np.random.Generator, action_fn: Callable | None = None,
+                      use_greedy: bool = False):
+        """src/reinforce_agent.py:126-192 for one observation (numpy obs from Game2048Env).  The forward runs on
+        the device; the draw uses the caller's numpy Generator exactly like the reference."""
+        x, action_mask = encode_observation(obs)
+        xt = torch.as_tensor(np.asarray(x, dtype=np.float32), device=self.device).unsqueeze(0)
+        logits, acts, pres = forward_logits(self.params, xt, self.mlp_config.activation)
+        mk = None if action_mask is None else torch.as_tensor(np.asarray(action_mask), device=self.device).unsqueeze(0)
+        probs = logits_to_probs(logits, mk)[0].cpu().numpy()
+        action = None
+        if action_fn is not None:
+            try:
+                candidate = int(action_fn(self.env.state if self.env is not None else None, action_mask))
+            except Exception as e:  # noqa: BLE001 (same fallback as the reference)
+                self._logger.exception(f"action_fn raised an exception: {e}. Falling back to policy.")
+            else:
+                if not (0 <= candidate < len(probs)):
+                    self._logger.warning(f"action_fn returned out-of-range action {candidate}, falling back to policy.")
+                elif action_mask is not None and not bool(action_mask[candidate]):
+                    self._logger.warning(f"action_fn returned masked-out action {candidate}, falling back to policy.")
+                else:
+                    action = candidate
+        if action is None:
+            if use_greedy:
+                p = probs * action_mask if action_mask is not None else probs
+                action = int(np.argmax(p))
+            else:
+                action = int(rng.choice(len(probs), p=probs))
+        return action, probs, [a[0] for a in acts], [p[0] for p in pres]
+
+    @torch.no_grad()
+    def rollout_batch(self, env_seeds, policy_seeds, use_greedy: bool = False, rng: str = "pcg64",
+                      check_every: int = 8, record_probs: bool = False) -> TrajectoryBatch:
+        """Play one episode per lane (env.reset(seed=env_seeds[i]), policy stream default_rng(policy_seeds[i]))
+        until every lane terminates or truncates -- the batched equivalent of calling run_episode for each
+        (env_seed, policy_seed) pair (runner.py:587-591).  Everything stays on the device."""
+        n = len(env_seeds)
+        if len(policy_seeds) != n:
+            raise ValueError("env_seeds and policy_seeds must have the same length")
+        env = self._vec_env(n, rng)
+        env.reset(seed=list(env_seeds) if not isinstance(env_seeds, torch.Tensor) else env_seeds)
+        dev = self.device
+        from .vec_env import _as_u64_seeds
+
+        pseeds = _as_u64_seeds(list(policy_seeds) if not isinstance(policy_seeds, torch.Tensor) else policy_seeds,
+                               n, 0, dev)
+        pst = torch.empty(2 * n, dtype=torch.int64, device=dev)
+        pinc = torch.empty(2 * n, dtype=torch.int64, device=dev)
+        pbuf = torch.empty(n, dtype=torch.int64, device=dev)
+        rng_mode = L.RNG_PCG64 if rng == "pcg64" else L.RNG_PHILOX
+        if rng_mode == L.RNG_PCG64:
+            L.check(self._lib.g2048_seed_pcg64(L.ptr(pseeds), L.ptr(pst), L.ptr(pinc), L.ptr(pbuf), n, self._stream))
+        ms = self.env_config.max_steps
+        cap = int(ms) if (ms is not None and ms > 0) else 1024
+        cap = max(cap, 1)
+        boards = torch.empty(cap, n, dtype=torch.int64, device=dev)
+        actions = torch.empty(cap, n, dtype=torch.uint8, device=dev)
+        rewards = torch.empty(cap, n, dtype=torch.float32, device=dev)
+        flags = torch.empty(cap, n, dtype=torch.uint8, device=dev)
+        probs = torch.zeros(cap, n, 4, dtype=torch.float32, device=dev) if record_probs else None
+        t = 0
+        while True:
+            if t == cap:
+                grow = cap
+                boards = torch.cat([boards, torch.empty(grow, n, dtype=torch.int64, device=dev)])
+                actions = torch.cat([actions, torch.empty(grow, n, dtype=torch.uint8, device=dev)])
+                rewards = torch.cat([rewards, torch.empty(grow, n, dtype=torch.float32, device=dev)])
+                flags = torch.cat([flags, torch.empty(grow, n, dtype=torch.uint8, device=dev)])
+                if probs is not None:
+                    probs = torch.cat([probs, torch.zeros(grow, n, 4, dtype=torch.float32, device=dev)])
+                cap += grow
+            logits = self._policy_logits(env.obs)
+            L.check(self._lib.g2048_sample(L.ptr(logits), L.ptr(env.mask), L.ptr(env.status), int(use_greedy),
+                                           rng_mode, L.ptr(pst), L.ptr(pinc), L.ptr(pbuf), env.philox_key ^ 0x5A5A,
+                                           L.ptr(pseeds), L.ptr(env.step_count),
+                                           L.ptr(probs[t]) if probs is not None else None, L.ptr(actions[t]), n,
+                                           self._stream))
+            env.step_into(actions[t], reward=rewards[t], flags=flags[t], prev_board=boards[t])
+            t += 1
+            if t % check_every == 0 and not bool(env.status.any()):
+                break
+        fl = flags[:t]
+        lengths = ((fl & L.F_INACTIVE) == 0).sum(0).to(torch.int32)
+        T = int(lengths.max().item()) if n else 0
+        rw = rewards[:T]
+        valid = torch.arange(T, device=dev).unsqueeze(1) < lengths.unsqueeze(0)
+        total = torch.where(valid, rw.double(), torch.zeros((), dtype=torch.float64, device=dev)).sum(0)
+        return TrajectoryBatch(boards=boards[:T], actions=actions[:T], rewards=torch.where(valid, rw, 0.0),
+                               flags=fl[:T], lengths=lengths, total_reward=total,
+                               max_tile=env.max_tile_seen.clone(), final_boards=env.board.clone(),
+                               probs=probs[:T] if probs is not None else None)
+
+    def trajectories_from_batch(self, batch: TrajectoryBatch, with_states: bool = True) -> list[dict[str, Any]]:
+        """Convert a device batch to the reference's trajectory dicts (src/reinforce_agent.py:240-247)."""
+        n, T = batch.n, batch.T
+        x, mk = self._obs_from_boards(batch.boards.reshape(-1).contiguous())
+        x = x.view(T, n, -1).cpu().numpy()
+        mk = mk.view(T, n, 4).cpu().numpy()
+        boards = batch.boards.cpu().numpy().view(np.uint64)
+        acts = batch.actions.cpu().numpy()
+        rews = batch.rewards.cpu().numpy()
+        lens = batch.lengths.cpu().numpy()
+        tot = batch.total_reward.cpu().numpy()
+        mt = batch.max_tile.cpu().numpy()
+        shape = (4, 4, 17) if self.input_dim == 272 else (4, 4)
+        out = []
+        for i in range(n):
+            Ti = int(lens[i])
+            obs = []
+            for t in range(Ti):
+                board = x[t, i].reshape(shape).copy()
+                obs.append({"board": board, "action_mask": mk[t, i].copy()} if self.env_config.use_action_mask
+                           else board)
+            traj = {"obs": obs, "actions": [int(a) for a in acts[:Ti, i]],
+                    "rewards": [float(r) for r in rews[:Ti, i]], "total_reward": float(tot[i]),
+                    "states": [_render_values(_board_values(int(b))) for b in boards[:Ti, i]] if with_states else [],
+                    "max_tile": int(mt[i])}
+            out.append(traj)
+        return out
+
+    def run_episode(self, env_seed: int, policy_seed: int, action_gen: Callable | None = None,
+                    use_greedy: bool = False) -> dict[str, Any]:
+        """src/reinforce_agent.py:195-252.  Without action_gen the episode runs on the device lane path (same
+        spawn and policy streams as the reference); with action_gen it steps the drop-in env from the host."""
+        if action_gen is None:
+            return self.trajectories_from_batch(self.rollout_batch([env_seed], [policy_seed], use_greedy))[0]
+        from .env import Game2048Env
+
+        env = self.env if self.env is not None else Game2048Env(self.env_config, device=self.device)
+        saved = self.env
+        self.env = env
+        try:
+            obs, _ = env.reset(seed=env_seed)
+            state = env.render(mode="ansi")
+            prng = np.random.default_rng(policy_seed)
+            traj = {"obs": [], "actions": [], "rewards": [], "states": []}
+            total, done = 0.0, False
+            while not done:
+                a, _, _, _ = self.select_action(obs, prng, action_gen, use_greedy=use_greedy)
+                nobs, r, te, tr, _ = env.step(a)
+                traj["obs"].append(obs)
+                traj["actions"].append(a)
+                traj["rewards"].append(float(r))
+                traj["states"].append(state)
+                total += float(r)
+                obs = nobs
+                done = te or tr
+                state = env.render(mode="ansi")
+            traj["total_reward"] = total
+            traj["max_tile"] = env.max_tile_seen
+            return traj
+        finally:
+            self.env = saved
+
+    # ============================================================================================ returns
+    def compute_returns(self, rewards) -> np.ndarray:
+        """src/reinforce_agent.py:255-273 (fp64 scan, fp32 result) on the device."""
+        r = torch.as_tensor(np.asarray(rewards, dtype=np.float32), device=self.device).view(-1, 1).contiguous()
+        T = r.shape[0]
+        out = torch.zeros_like(r)
+        ln = torch.full((1,), T, dtype=torch.int32, device=self.device)
+        L.check(self._lib.g2048_returns(L.ptr(r), L.ptr(ln), float(self.agent_config.gamma), L.ptr(out), T, 1,
+                                        self._stream))
+        return out.view(-1).cpu().numpy()
+
+    def _returns_tm(self, rewards_tm: torch.Tensor, lengths: torch.Tensor) -> torch.Tensor:
+        T, n = rewards_tm.shape
+        out = torch.zeros_like(rewards_tm)
+        ln = lengths.to(torch.int32).contiguous()
+        L.check(self._lib.g2048_returns(L.ptr(rewards_tm.contiguous()), L.ptr(ln), float(self.agent_config.gamma),
+                                        L.ptr(out), T, n, self._stream))
+        return out
+
+    # ============================================================================================ weights & baselines
+    def _compute_episode_rank_weights(self, totals: torch.Tensor) -> torch.Tensor:
+        """src/reinforce_agent.py:681-716 on the global batch (dp.rank_weights)."""
+        return dp.rank_weights(totals, self.agent_config.reward_rank_weights)
+
+    def _advantages(self, values: torch.Tensor, lane: torch.Tensor, n_lanes: int, step_rank_w: torch.Tensor) -> torch.Tensor:
+        """_compute_advantages (src/reinforce_agent.py:276-325) + _compute_weighted_stats (:864-881) over flat
+        steps; 'batch' statistics are global across ranks (one tiny all-reduce)."""
+        mode = self.agent_config.baseline_mode
+        if mode == "off":
+            return values
+        if mode == "each":
+            s = torch.zeros(n_lanes, dtype=torch.float64, device=self.device).index_add_(0, lane, values.double())
+            c = torch.zeros(n_lanes, dtype=torch.float64, device=self.device).index_add_(
+                0, lane, torch.ones_like(values, dtype=torch.float64))
+            mean = (s / c.clamp(min=1)).to(torch.float32)
+            return values - mean[lane]
+        if mode not in ("batch", "batch_norm"):
+            raise ValueError(f"Unknown baseline mode: {mode}")
+        mean, std = dp.weighted_stats(values, step_rank_w)
+        if mode == "batch":
+            return (values - np.float32(mean)).to(torch.float32)
+        std = max(std, 1e-8)
+        return ((values - np.float32(mean)) / np.float32(std)).to(torch.float32)
+
+    # ============================================================================================ optimiser
+    def _init_adam(self, params, prefix="actor"):
+        """src/reinforce_agent.py:811-832"""
+        z = lambda ts: [torch.zeros_like(t) for t in ts]  # noqa: E731
+        if prefix == "actor":
+            self._adam_m_W, self._adam_v_W = z(params["W"]), z(params["W"])
+            self._adam_m_B, self._adam_v_B = z(params["b"]), z(params["b"])
+        else:
+            self._adam_m_W_c, self._adam_v_W_c = z(params["W"]), z(params["W"])
+            self._adam_m_B_c, self._adam_v_B_c = z(params["b"]), z(params["b"])
+
+    def clip_grads_global_norm(self, grad_W_list, grad_b_list):
+        """src/reinforce_agent.py:835-861: fp32 L2 over all W then all b; scale in place if > max_grad_norm."""
+        max_norm = self.agent_config.max_grad_norm
+        sq = torch.zeros((), dtype=torch.float32, device=self.device)
+        for g in list(grad_W_list) + list(grad_b_list):
+            sq = sq + torch.linalg.vector_norm(g.float()) ** 2
+        total = torch.sqrt(sq)
+        tn = float(total)
+        coef = np.float32(max_norm) / np.float32(max(tn, 1e-8))
+        if coef < 1.0:
+            for g in list(grad_W_list) + list(grad_b_list):
+                g.mul_(float(coef))
+        return tn
+
+    def _adam_update(self, grad_W_list, grad_b_list, prefix="actor") -> None:
+        """src/reinforce_agent.py:719-770 (fp32, eps outside the sqrt, separate step counters)."""
+        c = self.agent_config
+        if prefix == "actor":
+            P, mW, vW, mB, vB = self.params, self._adam_m_W, self._adam_v_W, self._adam_m_B, self._adam_v_B
+            self._adam_t += 1
+            t, lr, sign = self._adam_t, c.learning_rate, 1.0
+        else:
+            P, mW, vW, mB, vB = (self.critic_params, self._adam_m_W_c, self._adam_v_W_c, self._adam_m_B_c,
+                                 self._adam_v_B_c)
+            self._adam_t_c += 1
+            t, lr, sign = self._adam_t_c, c.critic_learning_rate, -1.0
+        b1, b2, eps = c.adam_beta1, c.adam_beta2, 1e-8
+        bc1, bc2 = 1.0 - b1 ** t, 1.0 - b2 ** t
+        for key, m, v, G in (("W", mW, vW, grad_W_list), ("b", mB, vB, grad_b_list)):
+            for l in range(len(P[key])):
+                m[l].mul_(b1).add_(G[l] * (1.0 - b1))
+                v[l].mul_(b2).add_((G[l] * G[l]) * (1.0 - b2))
+                P[key][l] = P[key][l] + sign * lr * (m[l] / bc1) / (torch.sqrt(v[l] / bc2) + eps)
+
+    # ============================================================================================ update
+    def update_batch(self, trajectories: list[dict[str, Any]]) -> None:
+        """src/reinforce_agent.py:357-620 on reference-format trajectories (obs as numpy dicts/arrays)."""
+        n = len(trajectories)
+        lens = [len(tr["obs"]) for tr in trajectories]
+        if n == 0:
+            return
+        T = max(lens) if lens else 0
+        D = self.input_dim
+        X = np.zeros((T, n, D), dtype=np.float32)
+        M = np.ones((T, n, 4), dtype=np.int8)
+        A = np.zeros((T, n), dtype=np.uint8)
+        R = np.zeros((T, n), dtype=np.float32)
+        for i, tr in enumerate(trajectories):
+            for t, o in enumerate(tr["obs"]):
+                x, m = encode_observation(o)
+                X[t, i] = x
+                if m is not None:
+                    M[t, i] = m
+            A[:lens[i], i] = tr["actions"]
+            R[:lens[i], i] = tr["rewards"]
+        dev = self.device
+        totals = torch.tensor([float(tr["total_reward"]) for tr in trajectories], dtype=torch.float64, device=dev)
+        steps = _Steps(self, torch.tensor(lens, device=dev), torch.from_numpy(A).to(dev), torch.from_numpy(R).to(dev),
+                       X=torch.from_numpy(X).to(dev), M=torch.from_numpy(M).to(dev))
+        self._update(steps, totals)
+
+    def update_from_batch(self, batch: TrajectoryBatch) -> dict:
+        """update_batch on a device TrajectoryBatch (the hot path: no host round trip)."""
+        steps = _Steps(self, batch.lengths, batch.actions, batch.rewards, boards=batch.boards)
+        return self._update(steps, batch.total_reward)
+
+    def _chunks(self, N: int):
+        for s in range(0, N, self.chunk_steps):
+            yield torch.arange(s, min(N, s + self.chunk_steps), device=self.device)
+
+    def _update(self, steps: _Steps, totals: torch.Tensor) -> dict:
+        c = self.agent_config
+        n_local = steps.n
+        n_global = dp.global_count(n_local, self.device)
+        K = 8 if c.augmentation else 1
+        n_traj = n_global * K
+        rank_w = self._compute_episode_rank_weights(totals)               # [n_local]
+        lane = steps.lane
+        lens_f = steps.lengths.to(torch.float64)
+        step_w = (rank_w[lane].double() / (lens_f[lane] * n_traj)).to(torch.float32)   # rank_w / (T_i * n)
+        stats: dict = {}
+
+        actor_g = [torch.zeros_like(p) for p in self.params["W"] + self.params["b"]]
+        critic_g = None
+        if c.use_critic:
+            critic_g = [torch.zeros_like(p) for p in self.critic_params["W"] + self.critic_params["b"]]
+            deltas = torch.empty(K, steps.N, dtype=torch.float32, device=self.device)
+            cparams = [p.detach().requires_grad_(True) for p in self.critic_params["W"] + self.critic_params["b"]]
+            nW = len(self.critic_params["W"])
+            cp = {"W": cparams[:nW], "b": cparams[nW:]}
+            for k in range(K):
+                for sel in self._chunks(steps.N):
+                    x, _ = steps.features(sel, k)
+                    v = forward_logits(cp, x, self.mlp_config.activation, keep_cache=False)[0].view(-1)
+                    with torch.no_grad():
+                        hn = steps.has_next[sel]
+                        vn = torch.zeros_like(v)
+                        if bool(hn.any()):
+                            xn, _ = steps.features(sel[hn], k, nxt=True)
+                            vn[hn] = forward_logits(self.critic_params, xn, self.mlp_config.activation,
+                                                    keep_cache=False)[0].view(-1)
+                        r = steps.rewards[sel]
+                        tgt = r + (float(c.gamma) * vn) * hn.to(torch.float32)
+                        deltas[k, sel] = tgt - v
+                        diff = v - tgt
+                        if c.critic_loss_type == "mse":
+                            g = diff
+                        elif c.critic_loss_type == "huber":
+                            g = torch.where(diff.abs() <= c.huber_delta, diff,
+                                            float(c.huber_delta) * torch.sign(diff))
+                        else:
+                            raise ValueError(f"Unknown critic loss type: {c.critic_loss_type}")
+                        g = g * step_w[sel]
+                    grads = torch.autograd.grad(v, cparams, grad_outputs=g)
+                    for acc, gr in zip(critic_g, grads):
+                        acc.add_(gr)
+            # advantages from TD errors, over all K x n "episodes"
+            lane_k = (torch.arange(K, device=self.device).unsqueeze(1) * n_local + lane.unsqueeze(0)).reshape(-1)
+            adv = self._advantages(deltas.reshape(-1), lane_k, K * n_local,
+                                   rank_w[lane].repeat(K)).view(K, steps.N)
+        else:
+            G = self._returns_tm(steps.rewards_tm, steps.lengths).reshape(-1)[steps.vidx]
+            adv1 = self._advantages(G, lane, n_local, rank_w[lane])
+            adv = adv1.unsqueeze(0).expand(K, -1)
+        stats["adv_mean"] = float(adv.mean()) if adv.numel() else 0.0
+        stats["adv_std"] = float(adv.std(unbiased=False)) if adv.numel() else 0.0
+
+        aparams = [p.detach().requires_grad_(True) for p in self.params["W"] + self.params["b"]]
+        nW = len(self.params["W"])
+        ap = {"W": aparams[:nW], "b": aparams[nW:]}
+        for k in range(K):
+            for sel in self._chunks(steps.N):
+                x, mk = steps.features(sel, k)
+                logits = forward_logits(ap, x, self.mlp_config.activation, keep_cache=False)[0]
+                with torch.no_grad():
+                    p = logits_to_probs(logits, mk)
+                    onehot = torch.nn.functional.one_hot(steps.actions_k(sel, k), 4).to(torch.float32)
+                    g = (onehot - p) * (adv[k, sel] * step_w[sel]).unsqueeze(1)
+                grads = torch.autograd.grad(logits, aparams, grad_outputs=g)
+                for acc, gr in zip(actor_g, grads):
+                    acc.add_(gr)
+
+        # one fused all-reduce of actor (+ critic) gradients across ranks, before clipping
+        dp.fused_all_reduce_(actor_g + (critic_g or []))
+        self.last_grads = {"actor": [g.clone() for g in actor_g],
+                           "critic": [g.clone() for g in critic_g] if critic_g else None}
+        gW, gb = actor_g[:nW], actor_g[nW:]
+        stats["actor_grad_norm"] = self.clip_grads_global_norm(gW, gb)
+        if c.use_critic:
+            ncW = len(self.critic_params["W"])
+            gWc, gbc = critic_g[:ncW], critic_g[ncW:]
+            stats["critic_grad_norm"] = self.clip_grads_global_norm(gWc, gbc)
+        if c.optimizer == "sgd":
+            for l in range(nW):
+                self.params["W"][l] = self.params["W"][l] + c.learning_rate * gW[l]
+                self.params["b"][l] = self.params["b"][l] + c.learning_rate * gb[l]
+            if c.use_critic:
+                for l in range(ncW):
+                    self.critic_params["W"][l] = self.critic_params["W"][l] - c.critic_learning_rate * gWc[l]
+                    self.critic_params["b"][l] = self.critic_params["b"][l] - c.critic_learning_rate * gbc[l]
+        elif c.optimizer == "adam":
+            self._adam_update(gW, gb)
+            if c.use_critic:
+                self._adam_update(gWc, gbc, prefix="critic")
+        else:
+            raise ValueError(f"Unknown optimizer: {c.optimizer}")
+        if self._logger.isEnabledFor(logging.INFO):
+            self._logger.info(f"Global Grad Norms: Actor: {stats['actor_grad_norm']:.4f}")
+            if c.use_critic:
+                self._logger.info(f"Global Grad Norms: Critic: {stats['critic_grad_norm']:.4f}")
+        self.last_stats = stats
+        return stats

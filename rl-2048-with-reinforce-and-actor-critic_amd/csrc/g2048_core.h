@@ -1,0 +1,408 @@
+// g2048_core.h -- bitboard arithmetic of the 2048 hot path, shared by the gfx950 kernels (g2048.hip) and the
+// CPU unit-test harness (tests/native/core_test.cpp, test-only).  Nothing here allocates or launches.
+//
+// Board ("bitboard"): uint64, nibble i = 4*r + c holds log2(tile) (0 = empty); row r = bits [16r, 16r+16),
+// cell c = nibble c of its row.  A "line" is 4 nibbles in move-left frame order (nibble 0 = destination edge).
+//
+// Every function names the reference semantics it implements (paths relative to the reference repo root).
+#pragma once
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#define G2048_HD __host__ __device__ inline
+#else
+#define G2048_HD static inline  // test-only host build of the same code
+#endif
+
+namespace g2048 {
+
+constexpr uint64_t kNibLsb = 0x1111111111111111ull;
+constexpr uint64_t kHMask = 0x0111011101110111ull;  // cells with c in {0,1,2}: a right-hand neighbour exists
+constexpr uint64_t kVMask = 0x0000111111111111ull;  // cells with r in {0,1,2}: a lower neighbour exists
+
+G2048_HD int popc64(uint64_t x) { return __builtin_popcountll(x); }
+
+// bit 4i set iff nibble i != 0
+G2048_HD uint64_t nz_bits(uint64_t b) {
+    uint64_t x = b | (b >> 1);
+    x |= x >> 2;
+    return x & kNibLsb;
+}
+
+// 4x4 nibble transpose: cell (r,c) <-> (c,r)
+G2048_HD uint64_t transpose(uint64_t x) {
+    uint64_t t = (x ^ (x >> 12)) & 0x0000F0F00000F0F0ull;
+    x ^= t ^ (t << 12);
+    t = (x ^ (x >> 24)) & 0x00000000FF00FF00ull;
+    x ^= t ^ (t << 24);
+    return x;
+}
+
+// reverse the 4 nibbles of every row: cell (r,c) -> (r,3-c)
+G2048_HD uint64_t reverse_rows(uint64_t x) {
+    x = ((x & 0x00FF00FF00FF00FFull) << 8) | ((x >> 8) & 0x00FF00FF00FF00FFull);
+    x = ((x & 0x0F0F0F0F0F0F0F0Full) << 4) | ((x >> 4) & 0x0F0F0F0F0F0F0F0Full);
+    return x;
+}
+
+// reverse the order of the rows: cell (r,c) -> (3-r,c)
+G2048_HD uint64_t reverse_cols(uint64_t x) {
+    x = ((x & 0x00000000FFFFFFFFull) << 32) | (x >> 32);
+    x = ((x & 0x0000FFFF0000FFFFull) << 16) | ((x >> 16) & 0x0000FFFF0000FFFFull);
+    return x;
+}
+
+// Game2048._is_done (src/game2048.py:172-187): no empty cell and no equal horizontal / vertical neighbours.
+G2048_HD bool is_done(uint64_t b) {
+    uint64_t nz = nz_bits(b);
+    if (nz != kNibLsb) return false;
+    uint64_t eqh = ~nz_bits(b ^ (b >> 4)) & kHMask;
+    uint64_t eqv = ~nz_bits(b ^ (b >> 16)) & kVMask;
+    return (eqh | eqv) == 0;
+}
+
+// Game2048.get_action_mask (src/game2048.py:95-99, :233-237): bit a set iff action a changes the board.
+// A line changes under move-left iff an empty cell precedes a tile or two adjacent tiles are equal.
+G2048_HD uint32_t action_mask(uint64_t b) {
+    uint64_t nz = nz_bits(b);
+    uint64_t z = ~nz & kNibLsb;
+    uint64_t eqh = ~nz_bits(b ^ (b >> 4)) & nz & kHMask;
+    uint64_t eqv = ~nz_bits(b ^ (b >> 16)) & nz & kVMask;
+    uint32_t up = ((z & (nz >> 16) & kVMask) | eqv) != 0;
+    uint32_t down = ((nz & (z >> 16) & kVMask) | eqv) != 0;
+    uint32_t left = ((z & (nz >> 4) & kHMask) | eqh) != 0;
+    uint32_t right = ((nz & (z >> 4) & kHMask) | eqh) != 0;
+    return up | (right << 1) | (down << 2) | (left << 3);
+}
+
+G2048_HD uint32_t nibble_sum16(uint32_t x) {
+    x = (x & 0x0F0Fu) + ((x >> 4) & 0x0F0Fu);
+    return (x & 0xFFu) + (x >> 8);
+}
+
+// _row_move_left (src/game2048.py:120-137) on one line: compress, merge equal neighbours once left to right,
+// compress.  A 15+15 merge saturates at 15 (the caller flags it).  Used to build the row table.
+G2048_HD uint32_t line_move_left(uint32_t row) {
+    uint32_t c[4];
+    int n = 0;
+    for (int k = 0; k < 4; k++) {
+        uint32_t e = (row >> (4 * k)) & 15u;
+        if (e) c[n++] = e;
+    }
+    uint32_t out = 0;
+    int w = 0, i = 0;
+    while (i < n) {
+        uint32_t e;
+        if (i + 1 < n && c[i] == c[i + 1]) {
+            e = c[i] + 1;
+            if (e > 15) e = 15;
+            i += 2;
+        } else {
+            e = c[i];
+            i += 1;
+        }
+        out |= e << (4 * w);
+        w++;
+    }
+    return out;
+}
+
+// What the merges of one line were, recovered from the old and new line (no second table needed):
+//   c = tiles(old) - tiles(new) merges; c == 1: merged exponent = sum(old) - sum(new) + 2 (17 => saturated
+//   15+15, true exponent 16); c == 2: old was [a,a,b,b] (all four cells full) -> exponents a+1, b+1 in order.
+struct LineMerges {
+    uint32_t n;       // 0..2
+    uint32_t e0, e1;  // merged exponents in list order (true value, up to 16)
+};
+
+G2048_HD LineMerges line_merges(uint32_t o, uint32_t nw) {
+    LineMerges m;
+    uint32_t to = (uint32_t)popc64(nz_bits(o));
+    uint32_t tn = (uint32_t)popc64(nz_bits(nw));
+    m.n = to - tn;
+    uint32_t d = nibble_sum16(o) - nibble_sum16(nw) + 2u;
+    uint32_t e_single = d > 16u ? 16u : d;
+    uint32_t a = (o & 15u) + 1u, b = ((o >> 8) & 15u) + 1u;
+    m.e0 = m.n == 2 ? a : (m.n == 1 ? e_single : 0u);
+    m.e1 = m.n == 2 ? b : 0u;
+    return m;
+}
+
+// Accumulated merge summary of one move (what _compute_reward and Game2048.score consume).
+struct MoveSummary {
+    uint32_t count;   // len(merged)
+    uint32_t sum_e;   // sum(log2(v) for v in merged)  (reward_mode "log2")
+    uint32_t score;   // sum(merged)                   (reward_mode "sum", Game2048.score)
+    uint32_t max_e;   // log2(max(merged, default=0)) (0 if none)
+    uint32_t list;    // merged list, nibble k = e_k - 1, list order
+    uint32_t overflow;
+};
+
+G2048_HD void summary_add(MoveSummary& s, uint32_t e) {
+    // caller guarantees e != 0
+    s.list |= ((e - 1u) & 15u) << (4u * (s.count & 7u));
+    s.count += 1u;
+    s.sum_e += e;
+    s.score += 1u << e;
+    s.max_e = e > s.max_e ? e : s.max_e;
+    s.overflow |= (e >= 16u);
+}
+
+// Game2048._move (src/game2048.py:158-165) for action a given a line table `lut` (move-left of each 16-bit
+// line).  The reference rotates clockwise (3 - a) times and moves left; here the lines of the move-left frame
+// are read directly: left = rows, right = rows reversed, up = columns, down = columns reversed.  The merged
+// list follows the reference's row order in the rotated frame: left rows 0..3, right rows 3..0,
+// up columns 3..0, down columns 0..3 (each line in frame order).
+template <class Lut>
+G2048_HD uint64_t board_move(uint64_t b, uint32_t a, const Lut& lut, MoveSummary& s) {
+    const bool vert = (a == 0u) | (a == 2u);
+    const bool rev = (a == 1u) | (a == 2u);
+    const bool back = (a == 0u) | (a == 1u);  // list order runs from line 3 down to line 0
+    uint64_t f = vert ? transpose(b) : b;
+    f = rev ? reverse_rows(f) : f;
+    uint64_t g = 0;
+    s.count = s.sum_e = s.score = s.max_e = s.list = s.overflow = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int line = back ? 3 - j : j;
+        uint32_t o = (uint32_t)(f >> (16 * line)) & 0xFFFFu;
+        uint32_t nw = (uint32_t)lut(o);
+        g |= (uint64_t)nw << (16 * line);
+        LineMerges m = line_merges(o, nw);
+        if (m.n >= 1u) summary_add(s, m.e0);
+        if (m.n == 2u) summary_add(s, m.e1);
+    }
+    g = rev ? reverse_rows(g) : g;
+    g = vert ? transpose(g) : g;
+    return g;
+}
+
+// index (0-based) of the k-th empty cell in row-major order (np.argwhere(board == 0)[k], src/game2048.py:109)
+G2048_HD uint32_t kth_empty_cell(uint64_t zbits, uint32_t k) {
+    uint32_t pos = 0;
+    uint32_t c = (uint32_t)popc64(zbits & 0xFFFFFFFFull);
+    if (k >= c) { k -= c; zbits >>= 32; pos += 32; }
+    c = (uint32_t)popc64(zbits & 0xFFFFull);
+    if (k >= c) { k -= c; zbits >>= 16; pos += 16; }
+    c = (uint32_t)popc64(zbits & 0xFFull);
+    if (k >= c) { k -= c; zbits >>= 8; pos += 8; }
+    c = (uint32_t)popc64(zbits & 0xFull);
+    if (k >= c) { pos += 4; }
+    return pos >> 2;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// numpy PCG64 (np.random.default_rng) -- the RNG of Game2048._spawn (src/game2048.py:113,117) and of
+// ReinforceAgent.select_action (src/reinforce_agent.py:187).  Restated from numpy's published algorithm.
+// ---------------------------------------------------------------------------------------------------------
+struct Pcg64 {
+    uint64_t s_lo, s_hi, i_lo, i_hi;
+    uint32_t has_uint32, uinteger;
+};
+
+constexpr uint64_t kPcgMulHi = 0x2360ED051FC65DA4ull;
+constexpr uint64_t kPcgMulLo = 0x4385DF649FCCF645ull;
+
+G2048_HD uint64_t mulhi64(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
+
+G2048_HD void pcg_step(Pcg64& g) {
+    uint64_t lo = g.s_lo * kPcgMulLo;
+    uint64_t hi = mulhi64(g.s_lo, kPcgMulLo) + g.s_lo * kPcgMulHi + g.s_hi * kPcgMulLo;
+    uint64_t nlo = lo + g.i_lo;
+    g.s_hi = hi + g.i_hi + (nlo < lo);
+    g.s_lo = nlo;
+}
+
+G2048_HD uint64_t pcg_next64(Pcg64& g) {
+    pcg_step(g);
+    uint64_t x = g.s_hi ^ g.s_lo;
+    uint32_t rot = (uint32_t)(g.s_hi >> 58);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+G2048_HD uint32_t pcg_next32(Pcg64& g) {
+    if (g.has_uint32) {
+        g.has_uint32 = 0;
+        return g.uinteger;
+    }
+    uint64_t v = pcg_next64(g);
+    g.has_uint32 = 1;
+    g.uinteger = (uint32_t)(v >> 32);
+    return (uint32_t)v;
+}
+
+// Generator.random(): (next_uint64 >> 11) * 2**-53
+G2048_HD double pcg_random(Pcg64& g) { return (double)(pcg_next64(g) >> 11) * (1.0 / 9007199254740992.0); }
+
+// Generator.integers(n) for 1 <= n <= 16 (32-bit Lemire with rejection; n == 1 draws nothing)
+G2048_HD uint32_t pcg_bounded(Pcg64& g, uint32_t n) {
+    if (n <= 1u) return 0u;
+    const uint32_t rng = n - 1u;
+    uint64_t m = (uint64_t)pcg_next32(g) * n;
+    uint32_t left = (uint32_t)m;
+    if (left < n) {
+        const uint32_t thr = (0xFFFFFFFFu - rng) % n;
+        while (left < thr) {
+            m = (uint64_t)pcg_next32(g) * n;
+            left = (uint32_t)m;
+        }
+    }
+    return (uint32_t)(m >> 32);
+}
+
+// SeedSequence(seed).generate_state(4, uint64) -> pcg_setseq_128_srandom_r (np.random.PCG64(seed))
+G2048_HD uint32_t ss_hashmix(uint32_t v, uint32_t& hc) {
+    v ^= hc;
+    hc *= 0x931e8875u;
+    v *= hc;
+    v ^= v >> 16;
+    return v;
+}
+
+G2048_HD uint32_t ss_mix(uint32_t x, uint32_t y) {
+    uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y;
+    return r ^ (r >> 16);
+}
+
+G2048_HD Pcg64 pcg_seed(uint64_t seed) {
+    const uint32_t w0 = (uint32_t)seed, w1 = (uint32_t)(seed >> 32);
+    const bool two = w1 != 0u;  // python int -> uint32 words, little-endian, at least one word
+    uint32_t pool[4];
+    uint32_t hc = 0x43b0d7e5u;
+    pool[0] = ss_hashmix(w0, hc);
+    pool[1] = ss_hashmix(two ? w1 : 0u, hc);
+    pool[2] = ss_hashmix(0u, hc);
+    pool[3] = ss_hashmix(0u, hc);
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+            if (s != d) pool[d] = ss_mix(pool[d], ss_hashmix(pool[s], hc));
+    uint32_t w[8];
+    uint32_t hb = 0x8b51f9ddu;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint32_t v = pool[i & 3];
+        v ^= hb;
+        hb *= 0x58f38dedu;
+        v *= hb;
+        v ^= v >> 16;
+        w[i] = v;
+    }
+    // generate_state(4, uint64) words: v[k] = w[2k] | w[2k+1] << 32; initstate = v0:v1, initseq = v2:v3
+    const uint64_t st_hi = ((uint64_t)w[1] << 32) | w[0], st_lo = ((uint64_t)w[3] << 32) | w[2];
+    const uint64_t sq_hi = ((uint64_t)w[5] << 32) | w[4], sq_lo = ((uint64_t)w[7] << 32) | w[6];
+    Pcg64 g;
+    g.i_hi = (sq_hi << 1) | (sq_lo >> 63);
+    g.i_lo = (sq_lo << 1) | 1u;
+    g.s_lo = 0;
+    g.s_hi = 0;
+    pcg_step(g);
+    uint64_t lo = g.s_lo + st_lo;
+    g.s_hi = g.s_hi + st_hi + (lo < g.s_lo);
+    g.s_lo = lo;
+    pcg_step(g);
+    g.has_uint32 = 0;
+    g.uinteger = 0;
+    return g;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Philox4x32-10 (throughput mode; distributionally equal, not stream-equal, to numpy)
+// ---------------------------------------------------------------------------------------------------------
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+G2048_HD U4 philox4x32(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+        U4 n;
+        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        n.y = (uint32_t)p1;
+        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        n.w = (uint32_t)p0;
+        c = n;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Game2048._spawn (src/game2048.py:108-118): uniform empty cell, then 2 (p=0.9) or 4.
+// ---------------------------------------------------------------------------------------------------------
+G2048_HD uint64_t spawn_pcg(uint64_t b, Pcg64& g) {
+    uint64_t z = ~nz_bits(b) & kNibLsb;
+    uint32_t n = (uint32_t)popc64(z);
+    if (n == 0u) return b;
+    uint32_t k = pcg_bounded(g, n);
+    uint32_t cell = kth_empty_cell(z, k);
+    uint64_t e = pcg_random(g) < 0.9 ? 1u : 2u;
+    return b | (e << (4u * cell));
+}
+
+// Philox spawn: r.x picks the cell (Lemire, no rejection), r.y < 0.9 * 2**32 picks the 2
+G2048_HD uint64_t spawn_philox(uint64_t b, U4 r) {
+    uint64_t z = ~nz_bits(b) & kNibLsb;
+    uint32_t n = (uint32_t)popc64(z);
+    if (n == 0u) return b;
+    uint32_t k = (uint32_t)(((uint64_t)r.x * n) >> 32);
+    uint32_t cell = kth_empty_cell(z, k);
+    uint64_t e = r.y < 3865470566u ? 1u : 2u;
+    return b | (e << (4u * cell));
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Game2048Env._compute_reward (src/env.py:197-261), fp64 with the reference's operation order.
+// max_tile_e is log2(Game2048Env.max_tile_seen) and is updated in place.
+// ---------------------------------------------------------------------------------------------------------
+struct RewardCfg {
+    int32_t reward_mode, bonus_mode, use_action_mask;
+    double base_reward_scale, empty_tile_reward, merge_reward, bonus_scale, step_reward, endgame_penalty,
+        invalid_action_penalty;
+};
+
+G2048_HD double env_reward(const RewardCfg& c, const MoveSummary& s, uint64_t final_board, bool done, bool invalid,
+                           uint32_t& max_tile_e) {
+    if (!c.use_action_mask && invalid) return c.invalid_action_penalty;
+    double r = c.reward_mode == 0 ? (double)s.score : (double)s.sum_e;
+    r *= c.base_reward_scale;
+    if (c.empty_tile_reward != 0.0) {
+        const int ne = 16 - popc64(nz_bits(final_board));
+        r += c.empty_tile_reward * (double)ne;
+    }
+    if (c.merge_reward != 0.0) r += c.merge_reward * (double)s.count;
+    if (s.max_e >= 3u && s.max_e > max_tile_e) {
+        double bonus = 0.0;
+        if (c.bonus_mode == 1) bonus = (double)(1u << s.max_e);
+        else if (c.bonus_mode == 2) bonus = (double)s.max_e;
+        max_tile_e = s.max_e;
+        bonus *= c.bonus_scale;
+        r += bonus;
+    }
+    r += c.step_reward;
+    if (done && c.endgame_penalty != 0.0) r += c.endgame_penalty;
+    return r;
+}
+
+// Dihedral symmetry k of a board (Game2048Env.get_symmetries order, src/env.py:355-396):
+// k = 0..3: k counter-clockwise quarter turns (np.rot90 k=1 per step); k = 4..7: fliplr, then (k-4) turns.
+G2048_HD uint64_t rot_ccw(uint64_t b) { return transpose(reverse_rows(b)); }  // out[i][j] = b[j][3-i]
+
+G2048_HD uint64_t symmetry_board(uint64_t b, int k) {
+    uint64_t x = k >= 4 ? reverse_rows(b) : b;
+    const int t = k & 3;
+    for (int i = 0; i < t; i++) x = rot_ccw(x);
+    return x;
+}
+
+// action remap of the same symmetry: rotate_action_ccw90 (a-1)%4, flip_action_horiz 1<->3
+G2048_HD uint32_t symmetry_action(uint32_t a, int k) {
+    if (k >= 4) a = (a == 1u) ? 3u : (a == 3u ? 1u : a);
+    return (a + 4u - (uint32_t)(k & 3)) & 3u;
+}
+
+}  // namespace g2048

@@ -1,0 +1,126 @@
+"""The policy / critic MLP of src/MLP.py on PyTorch-ROCm (fp32; the dense layers run on hipBLASLt).
+
+Same names, parameter layout and numbers as the reference: params = {"W": [W_0..W_L], "b": [b_0..b_L]} with
+W_l of shape [in, out] (``x @ W + b``), fp32, initialised by the SAME numpy Generator draws in the same order
+(src/MLP.py:45-94), so a given model_seed yields bit-identical weights.  Tensors live on the agent's device.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Literal
+
+import numpy as np
+import torch
+
+ActivationMode = Literal["Sigmoid", "ReLU"]
+
+
+@dataclass
+class MLPConfig:
+    hidden_sizes: list[int] = field(default_factory=list)
+    activation: ActivationMode = "Sigmoid"
+    init_distribution: str = "XavierNormal"
+    last_init_normal: bool = True   # accepted for config compatibility; dead code in the reference (src/MLP.py:69)
+
+    @property
+    def num_layers(self) -> int:
+        return len(self.hidden_sizes)
+
+
+def encode_observation(obs):
+    """src/MLP.py:22-43.  obs: dict {"board", "action_mask"} or a bare board; numpy or torch, single or batched
+    (a leading batch dim is kept when the board has 3 (raw/log2) or 4 (onehot) dims)."""
+    if isinstance(obs, dict):
+        board, mask = obs["board"], obs["action_mask"]
+    else:
+        board, mask = obs, None
+    if isinstance(board, torch.Tensor):
+        batched = board.dim() in (3, 4) and not (board.dim() == 3 and board.shape[-1] == 17)
+        x = board.to(torch.float32).reshape(board.shape[0], -1) if batched else board.to(torch.float32).reshape(-1)
+    else:
+        x = np.asarray(board).astype(np.float32).flatten()
+    return x, mask
+
+
+def _draw_layer(rng: np.random.Generator, dist: str, din: int, dout: int) -> np.ndarray:
+    if dist == "XavierNormal":
+        return rng.normal(0.0, np.sqrt(2.0 / (din + dout)), size=(din, dout)).astype(np.float32)
+    if dist == "HeNormal":
+        return rng.normal(0.0, np.sqrt(2.0 / din), size=(din, dout)).astype(np.float32)
+    if dist == "XavierUniform":
+        lim = np.sqrt(6.0 / (din + dout))
+        return rng.uniform(-lim, lim, size=(din, dout)).astype(np.float32)
+    if dist == "Normal":
+        return rng.standard_normal((din, dout), dtype=np.float32) * 0.01
+    raise ValueError(f"Unsupported init_distribution: {dist}")
+
+
+def init_model_params(input_dim: int, hidden_sizes: list[int], output_dim: int, rng: np.random.Generator,
+                      init_distribution: str = "normal", last_init_normal: bool = True, device=None) -> dict[str, Any]:
+    """src/MLP.py:45-94: one draw per layer, in order, from `rng` (host numpy -- the reference's init stream),
+    biases zero, then the fp32 tensors are placed on `device`."""
+    sizes = [input_dim] + list(hidden_sizes) + [output_dim]
+    Ws, bs = [], []
+    for din, dout in zip(sizes[:-1], sizes[1:]):
+        Ws.append(torch.from_numpy(_draw_layer(rng, init_distribution, din, dout)).to(device))
+        bs.append(torch.zeros(dout, dtype=torch.float32, device=device))
+    return {"W": Ws, "b": bs}
+
+
+def load_model_params(file_path: str = "params.npz", device=None) -> dict[str, Any]:
+    """src/MLP.py:97-107 (npz keys n_layers, W_i, b_i; loaded without pickle)."""
+    with np.load(file_path, allow_pickle=False) as data:
+        n = int(data["n_layers"])
+        return {"W": [torch.from_numpy(np.array(data[f"W_{i}"], dtype=np.float32)).to(device) for i in range(n)],
+                "b": [torch.from_numpy(np.array(data[f"b_{i}"], dtype=np.float32)).to(device) for i in range(n)]}
+
+
+def save_model_params(params: dict[str, Any], file_path: str = "params.npz") -> None:
+    """src/MLP.py:110-126 -- the same npz layout, so checkpoints interoperate with the reference."""
+    Ws, bs = list(params["W"]), list(params["b"])
+    assert len(Ws) == len(bs), "W/b layer count mismatch"
+    data = {"n_layers": np.array(len(Ws), dtype=np.int64)}
+    for i, (W, b) in enumerate(zip(Ws, bs)):
+        data[f"W_{i}"] = W.detach().cpu().numpy() if isinstance(W, torch.Tensor) else np.asarray(W)
+        data[f"b_{i}"] = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b)
+    np.savez(file_path, **data)
+
+
+def apply_activation(x: torch.Tensor, mode: str) -> torch.Tensor:
+    """src/MLP.py:130-136"""
+    if mode == "Sigmoid":
+        return torch.sigmoid(x)
+    if mode == "ReLU":
+        return torch.relu(x)
+    raise ValueError(f"Unsupported activation: {mode}")
+
+
+def forward_logits(params: dict[str, list[torch.Tensor]], x: torch.Tensor, activation_mode: str,
+                   keep_cache: bool = True):
+    """src/MLP.py:159-196: z_i = a_i @ W_i + b_i, activation on hidden layers, identity on the last.
+    Returns (logits, activations [a_0..a_L], pre_activations [z_0..z_{L-1}]) like the reference."""
+    Ws, bs = params["W"], params["b"]
+    assert len(Ws) == len(bs), "W/b layer count mismatch"
+    act = x.to(torch.float32)
+    acts, pres = ([act], []) if keep_cache else (None, None)
+    for i, (W, b) in enumerate(zip(Ws, bs)):
+        z = torch.addmm(b, act, W) if act.dim() == 2 else act @ W + b
+        if keep_cache:
+            pres.append(z)
+        act = apply_activation(z, activation_mode) if i < len(Ws) - 1 else z
+        if keep_cache:
+            acts.append(act)
+    return act, acts, pres
+
+
+def masked_logits(logits: torch.Tensor, action_mask: torch.Tensor | None) -> torch.Tensor:
+    if action_mask is None:
+        return logits
+    return torch.where(action_mask.to(torch.bool), logits, torch.full_like(logits, -1e9))
+
+
+def logits_to_probs(logits: torch.Tensor, action_mask: torch.Tensor | None = None) -> torch.Tensor:
+    """src/MLP.py:139-156: where(mask, logits, -1e9), max-shifted softmax over the last axis."""
+    z = masked_logits(logits, action_mask)
+    e = torch.exp(z - z.max(dim=-1, keepdim=True).values)
+    return e / e.sum(dim=-1, keepdim=True)

@@ -1,0 +1,193 @@
+"""VecGame2048Env: n 2048 boards stepped together on one HIP device by libg2048.so.
+
+The batched form of Game2048Env (src/env.py:44-302) and Game2048 (src/game2048.py:11-237).  Per-lane state
+lives in device tensors (structure of arrays, see include/g2048.h ``g2048_lanes``); every call is one kernel
+launch on the current torch stream and never synchronises the host.
+
+Observations follow src/env.py:131-159 (+ the flattening of src/MLP.py:22-43): ``obs["board"]`` is
+float32 [n,4,4] (raw / log2) or [n,4,4,17] (onehot) and ``obs["action_mask"]`` int8 [n,4].  The returned tensors
+are the env's own buffers and are overwritten by the next step (clone to keep them).  Lanes that finished
+(without auto-reset) keep their final obs and report ``F_INACTIVE`` until reset.
+"""
+from __future__ import annotations
+
+import ctypes
+import secrets
+
+import torch
+
+from . import _lib as L
+from .config import Game2048EnvConfig, env_cfg_struct, obs_width
+
+
+def _signed64(v: int) -> int:
+    v &= 0xFFFFFFFFFFFFFFFF
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+def _as_u64_seeds(seed, n: int, offset: int, device) -> torch.Tensor:
+    """seed: None (fresh entropy, like Game2048._set_seed src/game2048.py:103-104), int (lane i gets
+    seed + offset + i, mod 2**64), or a sequence / tensor of n seeds (python ints in [0, 2**64)).
+    Returned as int64 tensors holding the uint64 bit patterns."""
+    if seed is None:
+        seed = secrets.randbits(63)
+    if isinstance(seed, int):
+        if seed < 0:
+            raise ValueError("expected non-negative integer")  # numpy SeedSequence raises the same
+        return torch.arange(n, dtype=torch.int64, device=device) + _signed64(seed + offset)
+    if isinstance(seed, torch.Tensor):
+        if seed.numel() != n:
+            raise ValueError(f"expected {n} seeds, got {seed.numel()}")
+        return seed.to(device=device, dtype=torch.int64).contiguous()
+    vals = [int(s) for s in seed]
+    if len(vals) != n:
+        raise ValueError(f"expected {n} seeds, got {len(vals)}")
+    for v in vals:
+        if v < 0:
+            raise ValueError("expected non-negative integer")
+        if v >= 1 << 64:
+            raise ValueError("seeds >= 2**64 are not supported by the device SeedSequence")
+    return torch.tensor([_signed64(v) for v in vals], dtype=torch.int64, device=device)
+
+
+class VecGame2048Env:
+    """n independent Game2048Env lanes on one device.
+
+    rng="pcg64": every lane's spawn stream is numpy's default_rng(seed) (bit-exact with the reference).
+    rng="philox": Philox4x32-10 keyed by (philox_key, lane seed, step) -- same distribution, no RNG state traffic.
+    auto_reset: a lane that terminates/truncates restarts in the same call with seed += reset_stride.
+    lane_offset: global index of lane 0 (for sharding a global board batch across ranks).
+    """
+
+    def __init__(self, num_envs: int, config: Game2048EnvConfig | None = None, device=None, rng: str = "pcg64",
+                 auto_reset: bool = False, reset_stride: int | None = None, philox_key: int = 0x2048,
+                 lane_offset: int = 0, record_merged: bool = False, record_prev_board: bool = False):
+        if num_envs <= 0:
+            raise ValueError("num_envs must be positive")
+        self.config = config or Game2048EnvConfig()
+        self._cfg = env_cfg_struct(self.config)          # validates modes (ValueError like src/env.py:110,223,249)
+        self.n = int(num_envs)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        L.ensure_device(self.device)
+        if rng not in ("pcg64", "philox"):
+            raise ValueError(f"Unsupported rng: {rng}")
+        self.rng_mode = L.RNG_PCG64 if rng == "pcg64" else L.RNG_PHILOX
+        self.auto_reset = bool(auto_reset)
+        self.reset_stride = int(reset_stride if reset_stride is not None else num_envs)
+        self.philox_key = int(philox_key) & 0xFFFFFFFFFFFFFFFF
+        self.lane_offset = int(lane_offset)
+        n, dev = self.n, self.device
+        z = lambda dt, *s: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
+        # lane state (g2048_lanes)
+        self.board = z(torch.int64, n)
+        self.step_count = z(torch.int32, n)
+        self.score = z(torch.int32, n)
+        self.max_tile = z(torch.uint8, n)
+        self.status = z(torch.uint8, n)
+        self.seed = z(torch.int64, n)
+        pcg = self.rng_mode == L.RNG_PCG64
+        self.rng_state = z(torch.int64, 2 * n) if pcg else None
+        self.rng_inc = z(torch.int64, 2 * n) if pcg else None
+        self.rng_buf = z(torch.int64, n) if pcg else None
+        # outputs (g2048_step_out)
+        self.reward = z(torch.float32, n)
+        self.flags = z(torch.uint8, n)
+        self.mask = z(torch.int8, n, 4)
+        self.obs_width = obs_width(self.config.obs_mode)
+        self.obs = z(torch.float32, n, self.obs_width)
+        self.merged = z(torch.int32, n) if record_merged else None
+        self.prev_board = z(torch.int64, n) if record_prev_board else None
+        self._lanes = L.Lanes(*[L.ptr(t) for t in (self.board, self.step_count, self.score, self.max_tile, self.status,
+                                                   self.seed, self.rng_state, self.rng_inc, self.rng_buf)])
+        self._out = L.StepOut(L.ptr(self.reward), L.ptr(self.flags), L.ptr(self.mask), L.ptr(self.obs),
+                              L.ptr(self.merged), L.ptr(self.prev_board))
+        self._lib = L.lib()
+        self._stream = L.stream_handle(self.device)
+
+    # ------------------------------------------------------------------------------------------------------
+    def _obs_view(self):
+        board = self.obs.view(self.n, 4, 4, 17) if self.obs_width == 272 else self.obs.view(self.n, 4, 4)
+        if self.config.use_action_mask:
+            return {"board": board, "action_mask": self.mask}
+        return board
+
+    def reset(self, *, seed=None, options=None, mask: torch.Tensor | None = None):
+        """Game2048Env.reset (src/env.py:174-194) for every lane (or the lanes where ``mask`` is nonzero).
+        Returns (obs, info) with info = {"score", "board"}."""
+        seeds = _as_u64_seeds(seed, self.n, self.lane_offset, self.device)
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        with torch.cuda.device(self.device):
+            L.check(self._lib.g2048_reset(ctypes.byref(self._lanes), L.ptr(seeds), L.ptr(m), ctypes.byref(self._cfg),
+                                          self.rng_mode, self.philox_key, L.ptr(self.mask), L.ptr(self.obs), self.n,
+                                          L.stream_handle(self.device)))
+        return self._obs_view(), {"score": self.score, "board": self.board}
+
+    def step_into(self, actions: torch.Tensor, reward: torch.Tensor | None = None, flags: torch.Tensor | None = None,
+                  prev_board: torch.Tensor | None = None) -> None:
+        """Launch one step writing reward/flags (and the pre-step board) into caller tensors (trajectory rows)."""
+        if actions.dtype != torch.uint8 or actions.device != self.device or actions.numel() != self.n:
+            raise ValueError("actions must be a uint8 tensor of num_envs elements on the env device")
+        out = self._out
+        if reward is not None or flags is not None or prev_board is not None:
+            out = L.StepOut(L.ptr(reward if reward is not None else self.reward),
+                            L.ptr(flags if flags is not None else self.flags), L.ptr(self.mask), L.ptr(self.obs),
+                            L.ptr(self.merged), L.ptr(prev_board if prev_board is not None else self.prev_board))
+        if torch.cuda.current_device() != self.device.index:
+            with torch.cuda.device(self.device):
+                return self.step_into(actions, reward, flags, prev_board)
+        L.check(self._lib.g2048_step(ctypes.byref(self._lanes), L.ptr(actions), ctypes.byref(self._cfg),
+                                     ctypes.byref(out), self.rng_mode, self.philox_key, int(self.auto_reset),
+                                     self.reset_stride, self.n, L.stream_handle(self.device)))
+
+    def step(self, actions):
+        """Game2048Env.step (src/env.py:264-302) for every lane.  actions: int tensor/sequence of n in 0..3.
+        Returns (obs, reward[n] f32, terminated[n] bool, truncated[n] bool, info)."""
+        a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(actions)
+        if a.dtype.is_floating_point:
+            raise AssertionError("Invalid action dtype")
+        a = a.to(device=self.device, dtype=torch.uint8 if a.dtype == torch.uint8 else torch.int64)
+        if a.dtype != torch.uint8:
+            if bool(((a < 0) | (a > 3)).any()):
+                raise AssertionError("Invalid action: outside 0..3")
+            a = a.to(torch.uint8)
+        self.step_into(a.contiguous())
+        f = self.flags
+        info = {"score": self.score, "flags": f, "changed": (f & L.F_CHANGED) != 0,
+                "invalid_action": (f & L.F_INVALID) != 0, "step_index": self.step_count,
+                "reset": (f & L.F_RESET) != 0, "overflow": (f & L.F_OVERFLOW) != 0}
+        if self.merged is not None:
+            info["merged_packed"] = self.merged
+        return (self._obs_view(), self.reward, (f & L.F_TERMINATED) != 0, (f & L.F_TRUNCATED) != 0, info)
+
+    @property
+    def active(self) -> torch.Tensor:
+        return (self.status & L.S_ACTIVE) != 0
+
+    @property
+    def max_tile_seen(self) -> torch.Tensor:
+        """Game2048Env.max_tile_seen per lane (4 at reset; raised by merges >= 8, src/env.py:238-250)."""
+        return torch.ones_like(self.max_tile, dtype=torch.int64) << self.max_tile.to(torch.int64)
+
+    def boards_exponents(self) -> torch.Tensor:
+        """[n,4,4] int64 exponents (0 = empty) of the current boards."""
+        b = self.board
+        shifts = torch.arange(0, 64, 4, device=self.device, dtype=torch.int64)
+        return ((b.unsqueeze(1) >> shifts) & 15).view(self.n, 4, 4)
+
+    def boards_values(self) -> torch.Tensor:
+        e = self.boards_exponents()
+        return torch.where(e > 0, torch.ones_like(e) << e, torch.zeros_like(e))
+
+
+def decode_merged(word: int) -> list[int]:
+    """g2048_step_out.merged -> the reference's merged list (tile values, src/game2048.py:131)."""
+    out = []
+    w = int(word) & 0xFFFFFFFF
+    for k in range(8):
+        nib = (w >> (4 * k)) & 15
+        if nib == 0:
+            break
+        out.append(1 << (nib + 1))
+    return out

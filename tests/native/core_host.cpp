@@ -1,0 +1,69 @@
+// TEST-ONLY host build of rl-2048-with-reinforce-and-actor-critic_amd/csrc/g2048_core.h (the arithmetic the
+// gfx950 kernels run), exported with C linkage so tests/test_core_host.py can check it against the CPU oracle
+// and the golden fixtures without a GPU.  Never loaded by the product package.
+#include <stdint.h>
+#include "g2048_core.h"
+
+using namespace g2048;
+
+static uint16_t g_lut[65536];
+static int g_lut_ready = 0;
+
+struct HostLut {
+    uint32_t operator()(uint32_t i) const { return g_lut[i]; }
+};
+
+static void ensure_lut() {
+    if (g_lut_ready) return;
+    for (uint32_t r = 0; r < 65536u; r++) g_lut[r] = (uint16_t)line_move_left(r);
+    g_lut_ready = 1;
+}
+
+extern "C" {
+uint64_t ch_board_move(uint64_t b, uint32_t a, uint32_t* list, uint32_t* count, uint32_t* score, uint32_t* sum_e,
+                       uint32_t* max_e, uint32_t* overflow) {
+    ensure_lut();
+    MoveSummary s;
+    uint64_t m = board_move(b, a, HostLut{}, s);
+    *list = s.list; *count = s.count; *score = s.score; *sum_e = s.sum_e; *max_e = s.max_e; *overflow = s.overflow;
+    return m;
+}
+uint32_t ch_action_mask(uint64_t b) { return action_mask(b); }
+int ch_is_done(uint64_t b) { return is_done(b) ? 1 : 0; }
+uint64_t ch_transpose(uint64_t b) { return transpose(b); }
+uint64_t ch_symmetry(uint64_t b, int k) { return symmetry_board(b, k); }
+uint32_t ch_symmetry_action(uint32_t a, int k) { return symmetry_action(a, k); }
+void ch_pcg_seed(uint64_t seed, uint64_t out[4]) {
+    Pcg64 g = pcg_seed(seed);
+    out[0] = g.s_hi; out[1] = g.s_lo; out[2] = g.i_hi; out[3] = g.i_lo;
+}
+// run a whole seeded episode of Game2048 with the given actions; writes boards / flags per step
+int ch_episode(uint64_t seed, const uint8_t* actions, int64_t n, uint64_t* boards, uint8_t* changed, uint8_t* done,
+               uint32_t* score, uint64_t* reset_board) {
+    ensure_lut();
+    Pcg64 g = pcg_seed(seed);
+    uint64_t b = spawn_pcg(spawn_pcg(0, g), g);
+    *reset_board = b;
+    uint32_t sc = 0;
+    for (int64_t t = 0; t < n; t++) {
+        MoveSummary s;
+        uint64_t m = board_move(b, actions[t], HostLut{}, s);
+        bool ch = m != b;
+        sc += s.score;
+        if (ch) m = spawn_pcg(m, g);
+        boards[t] = m; changed[t] = ch; done[t] = is_done(m); score[t] = sc;
+        b = m;
+    }
+    return 0;
+}
+double ch_reward(int reward_mode, int bonus_mode, int use_mask, const double* scal, uint32_t count, uint32_t sum_e,
+                 uint32_t score, uint32_t max_e, uint64_t final_board, int done, int invalid, uint32_t* max_tile_e) {
+    RewardCfg c;
+    c.reward_mode = reward_mode; c.bonus_mode = bonus_mode; c.use_action_mask = use_mask;
+    c.base_reward_scale = scal[0]; c.empty_tile_reward = scal[1]; c.merge_reward = scal[2]; c.bonus_scale = scal[3];
+    c.step_reward = scal[4]; c.endgame_penalty = scal[5]; c.invalid_action_penalty = scal[6];
+    MoveSummary s{};
+    s.count = count; s.sum_e = sum_e; s.score = score; s.max_e = max_e;
+    return env_reward(c, s, final_board, done != 0, invalid != 0, *max_tile_e);
+}
+}

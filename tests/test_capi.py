@@ -1,0 +1,104 @@
+"""CPU checks of the drop-in boundary: libg2048.so loads, exports every function include/g2048.h declares, the
+ctypes struct images match the C layouts, and argument validation rejects bad calls before any launch.
+No compute call is made (there is no GPU here)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "g2048.h")
+
+
+@pytest.fixture(scope="module")
+def L():
+    from rl2048_amd import _lib
+
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    return _lib
+
+
+def _declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(g2048_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_expected_api():
+    assert _declared_functions() == sorted([
+        "g2048_abi_version", "g2048_last_error", "g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step",
+        "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries"])
+
+
+def test_library_exports_every_declared_symbol(L):
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (g2048_\w+)", out))
+    missing = set(_declared_functions()) - exported
+    assert not missing, missing
+    lib = L.lib()
+    assert lib.g2048_abi_version() == L.ABI_VERSION
+    assert set(L.EXPORTED_SYMBOLS) == set(_declared_functions())
+
+
+def test_gfx950_code_object_present(L):
+    """The fat binary embeds an amdgcn gfx950 code object (the offload bundle id names the target)."""
+    data = open(L.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_struct_layouts_match_header(L, tmp_path):
+    import ctypes
+
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "g2048.h"\nint main(void){printf("%zu %zu %zu %zu %zu\\n",'
+                   ' sizeof(g2048_env_cfg), sizeof(g2048_lanes), sizeof(g2048_step_out),'
+                   ' offsetof(g2048_env_cfg, base_reward_scale), offsetof(g2048_env_cfg, max_steps)); return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I" + os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [ctypes.sizeof(L.EnvCfg), ctypes.sizeof(L.Lanes), ctypes.sizeof(L.StepOut),
+                   L.EnvCfg.base_reward_scale.offset, L.EnvCfg.max_steps.offset]
+
+
+def test_argument_validation_without_gpu(L):
+    """Bad arguments are rejected with G2048_EINVAL before anything touches a device."""
+    import ctypes
+
+    lib = L.lib()
+    assert lib.g2048_obs(None, 1, 1.0, None, None, 4, None) == L.G2048_EINVAL
+    assert lib.g2048_obs(ctypes.c_void_p(8), 7, 1.0, None, None, 4, None) == L.G2048_EINVAL
+    assert b"obs_mode" in lib.g2048_last_error()
+    assert lib.g2048_returns(None, None, 0.9, None, 4, 4, None) == L.G2048_EINVAL
+    assert lib.g2048_symmetries(None, None, None, None, -1, None) == L.G2048_EINVAL
+    cfg = L.EnvCfg()
+    cfg.reward_mode = 5
+    lanes = L.Lanes()
+    out = L.StepOut()
+    rc = lib.g2048_step(ctypes.byref(lanes), None, ctypes.byref(cfg), ctypes.byref(out), 0, 0, 0, 0, 1, None)
+    assert rc == L.G2048_EINVAL and b"reward mode" in lib.g2048_last_error()
+    with pytest.raises(ValueError):
+        L.check(L.G2048_EINVAL)
+
+
+def test_config_validation_messages():
+    from rl2048_amd.config import Game2048EnvConfig, env_cfg_struct
+
+    for kw, msg in ((dict(obs_mode="x"), "Unsupported obs_mode"), (dict(reward_mode="x"), "Unsupported reward mode"),
+                    (dict(bonus_mode="x"), "Unsupported bonus mode")):
+        with pytest.raises(ValueError, match=msg):
+            env_cfg_struct(Game2048EnvConfig(**kw))
+    assert env_cfg_struct(Game2048EnvConfig(max_steps=None)).max_steps == -1
+    assert env_cfg_struct(Game2048EnvConfig(max_steps=0)).max_steps == 0
+
+
+def test_no_cpu_fallback():
+    """The product path refuses to run without a HIP device instead of falling back to CPU."""
+    import torch
+
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError, match="no CPU fallback|no HIP device"):
+        VecGame2048Env(4, Game2048EnvConfig(), device="cpu")

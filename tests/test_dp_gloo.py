@@ -1,0 +1,109 @@
+"""CPU, world_size 2 (gloo): the data-parallel collectives of the update (rl2048_amd/dp.py) give every rank the
+result of the concatenated global batch -- rank weights, weighted baseline statistics and the fused gradient
+all-reduce -- which is what makes the N-GPU update equal to the 1-GPU update."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from rl2048_amd import dp
+
+        rng = np.random.default_rng(0)
+        totals = rng.integers(0, 50, size=13).astype(np.float64) + rng.random(13)   # distinct totals
+        sizes = [6, 7]
+        off = sum(sizes[:rank])
+        mine = torch.tensor(totals[off:off + sizes[rank]])
+        conf = [3.0, 2.0, 1.0, 1.0]
+        w_local = dp.rank_weights(mine, conf)
+        allg, o = dp.gather_varlen(mine)
+        vals = torch.tensor(rng.standard_normal(40), dtype=torch.float32)
+        wts = torch.tensor(rng.random(40), dtype=torch.float32)
+        vshard, wshard = vals[rank * 20:(rank + 1) * 20], wts[rank * 20:(rank + 1) * 20]
+        mean, std = dp.weighted_stats(vshard, wshard)
+        g = [torch.full((3, 2), float(rank + 1)), torch.arange(4, dtype=torch.float32) * (rank + 1)]
+        dp.fused_all_reduce_(g)
+        n = dp.global_count(sizes[rank], "cpu")
+        q.put((rank, w_local.numpy(), allg.numpy(), o, mean, std, [t.numpy() for t in g], n))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_collectives_equal_single_process():
+    from rl2048_amd import dp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(0)
+    totals = rng.integers(0, 50, size=13).astype(np.float64) + rng.random(13)
+    vals = rng.standard_normal(40).astype(np.float32)
+    wts = rng.random(40).astype(np.float32)
+    w_single = dp.rank_weights(torch.tensor(totals), [3.0, 2.0, 1.0, 1.0]).numpy()
+    np.testing.assert_array_equal(np.concatenate([res[0][1], res[1][1]]), w_single)
+    np.testing.assert_array_equal(res[0][2], totals)
+    assert res[0][3] == 0 and res[1][3] == 6
+    m1, s1 = dp.weighted_stats(torch.tensor(vals), torch.tensor(wts))
+    for r in (0, 1):
+        assert abs(res[r][4] - m1) < 1e-12 and abs(res[r][5] - s1) < 1e-12
+        np.testing.assert_array_equal(res[r][6][0], np.full((3, 2), 3.0))
+        np.testing.assert_array_equal(res[r][6][1], np.arange(4) * 3.0)
+        assert res[r][7] == 13
+
+
+def test_rank_weights_match_reference_formula():
+    """src/reinforce_agent.py:681-716 on distinct totals (single process)."""
+    from rl2048_amd import dp
+    from oracle import agent_oracle as AO
+
+    rng = np.random.default_rng(5)
+    for n in (1, 2, 7, 64):
+        totals = rng.permutation(n).astype(np.float64) * 1.5
+        for conf in ([1.0, 0.0], [3.0, 2.0, 1.0, 1.0], [1.0], None):
+            ref = AO.OracleAgent({"W": [], "b": []}, None, AO.AgentCfg(reward_rank_weights=conf)).rank_weights(
+                list(totals))
+            got = dp.rank_weights(torch.tensor(totals), conf).numpy()
+            np.testing.assert_allclose(got, ref, rtol=1e-6)
+
+
+@pytest.mark.parametrize("n", [0, 5])
+def test_weighted_stats_single(n):
+    from rl2048_amd import dp
+    from oracle import agent_oracle as AO
+
+    v = np.arange(n, dtype=np.float32)
+    w = np.ones(n, dtype=np.float32)
+    got = dp.weighted_stats(torch.tensor(v), torch.tensor(w))
+    ref = AO.OracleAgent.weighted_stats(v, w)
+    assert abs(got[0] - float(ref[0])) < 1e-6 and abs(got[1] - float(ref[1])) < 1e-6

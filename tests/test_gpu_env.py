@@ -1,0 +1,410 @@
+"""GPU parity of the env hot path (libg2048.so through its C ABI) against the reference's golden fixtures and
+the CPU oracle.  Bit-exact for boards / flags / masks / obs / merged lists / spawn streams; rewards equal the
+oracle's fp64 reward rounded once to fp32 (the kernel computes in fp64 and stores fp32)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from rl2048_amd import _lib
+
+    _lib.ensure_device(DEV)
+    return _lib
+
+
+def _u64(arr) -> torch.Tensor:
+    a = np.asarray(arr, dtype=np.uint64).view(np.int64)
+    return torch.from_numpy(a.copy()).to(DEV)
+
+
+def _to_u64(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint64)
+
+
+def _move(lib, boards: np.ndarray, actions: np.ndarray):
+    n = len(boards)
+    b = _u64(boards)
+    a = torch.from_numpy(np.asarray(actions, dtype=np.uint8)).to(DEV)
+    out = torch.zeros(n, dtype=torch.int64, device=DEV)
+    merged = torch.zeros(n, dtype=torch.int32, device=DEV)
+    flags = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    lib.check(lib.lib().g2048_move(b.data_ptr(), a.data_ptr(), out.data_ptr(), merged.data_ptr(), flags.data_ptr(), n,
+                                   lib.stream_handle(DEV)))
+    return _to_u64(out), merged.cpu().numpy().view(np.uint32), flags.cpu().numpy()
+
+
+def _merged_exps(word):
+    out = []
+    for k in range(8):
+        nib = (int(word) >> (4 * k)) & 15
+        if nib == 0:
+            break
+        out.append(nib + 1)
+    return out
+
+
+def test_row_table_exhaustive(lib, golden_dir):
+    """All 65,536 rows (src/game2048.py:120-137 golden) as row 0 of a left move, and reversed as a right move."""
+    d = np.load(os.path.join(golden_dir, "row_table.npz"))
+    rows = np.arange(65536, dtype=np.uint64)
+    out, merged, flags = _move(lib, rows, np.full(65536, 3))
+    exp = d["out_exp"].astype(np.uint64)
+    ovf = exp.max(axis=1) == 16
+    packed = (np.minimum(exp, 15) << (np.arange(4, dtype=np.uint64) * 4)).sum(axis=1)  # saturated image
+    np.testing.assert_array_equal(out, packed)
+    np.testing.assert_array_equal((flags & 0x10) != 0, ovf)
+    for r in range(65536):
+        assert _merged_exps(merged[r]) == list(d["merged_exp"][r][: d["n_merged"][r]]), r
+    changed = (out != rows)
+    np.testing.assert_array_equal((flags & 1) != 0, changed)
+
+
+def test_move_random_boards_vs_oracle(lib):
+    rng = np.random.default_rng(21)
+    e = rng.integers(1, 16, size=(20000, 16))
+    e[rng.random((20000, 16)) < 0.375] = 0
+    boards = np.array([O.pack_exponents(x) for x in e], dtype=np.uint64)
+    acts = rng.integers(0, 4, size=20000)
+    out, merged, flags = _move(lib, boards, acts)
+    for i in range(0, 20000, 7):
+        ob, om, och, ok = O.move_packed(int(boards[i]), int(acts[i]))
+        assert _merged_exps(merged[i]) == [int(v).bit_length() - 1 for v in om], i
+        assert bool(flags[i] & 1) == och
+        if ok:
+            assert int(out[i]) == ob, i
+
+
+def test_episodes_bit_exact_vs_golden(golden_dir):
+    """Every golden episode of the real Game2048 in its own lane: spawn stream, boards, flags, merged, score."""
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+
+    d = np.load(os.path.join(golden_dir, "episodes.npz"))
+    E = len(d["ep_seed"])
+    T = int(d["ep_len"].max())
+    env = VecGame2048Env(E, Game2048EnvConfig(max_steps=None), device=DEV, record_merged=True)
+    env.reset(seed=[int(s) for s in d["ep_seed"]])
+    np.testing.assert_array_equal(_to_u64(env.board), d["reset_board"])
+    m = env.mask.cpu().numpy()
+    np.testing.assert_array_equal((m * (1 << np.arange(4))).sum(1), d["reset_mask"])
+    for t in range(T):
+        idx = d["ep_start"] + np.minimum(t, d["ep_len"] - 1)
+        live = t < d["ep_len"]
+        acts = np.where(live, d["action"][idx], 0).astype(np.uint8)
+        env.step(torch.from_numpy(acts).to(DEV))
+        b = _to_u64(env.board)
+        fl = env.flags.cpu().numpy()
+        sc = env.score.cpu().numpy()
+        mg = env.merged.cpu().numpy().view(np.uint32)
+        mk = (env.mask.cpu().numpy() * (1 << np.arange(4))).sum(1)
+        for e in np.nonzero(live)[0]:
+            j = idx[e]
+            assert b[e] == d["board"][j], (e, t)
+            assert bool(fl[e] & 1) == d["changed"][j] and bool(fl[e] & 2) == d["done"][j], (e, t)
+            assert sc[e] == d["score"][j]
+            assert mk[e] == d["mask"][j]
+            gm = [int((int(d["merged"][j]) >> (5 * k)) & 31) for k in range(int(d["n_merged"][j]))]
+            assert _merged_exps(mg[e]) == gm, (e, t)
+
+
+def test_crafted_boards_vs_golden(golden_dir):
+    """High tiles (2**14/2**15 incl. the 65536 overflow), full / terminal / empty boards with a seeded spawn."""
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+
+    d = np.load(os.path.join(golden_dir, "crafted.npz"))
+    n = len(d["board_in"])
+    env = VecGame2048Env(n, Game2048EnvConfig(max_steps=None), device=DEV, record_merged=True)
+    env.reset(seed=[int(s) for s in d["seed"]])
+    env.board.copy_(_u64(d["board_in"]))          # Game2048.reset(seed) then board overwritten, as the fixture did
+    env.step(torch.from_numpy(d["action"].astype(np.uint8)).to(DEV))
+    b = _to_u64(env.board)
+    fl = env.flags.cpu().numpy()
+    mg = env.merged.cpu().numpy().view(np.uint32)
+    mk = (env.mask.cpu().numpy() * (1 << np.arange(4))).sum(1)
+    for i in range(n):
+        gm = [int((int(d["merged"][i]) >> (5 * k)) & 31) for k in range(int(d["n_merged"][i]))]
+        assert _merged_exps(mg[i]) == gm, i
+        assert bool(fl[i] & 1) == d["changed"][i] and bool(fl[i] & 2) == d["done"][i], i
+        assert bool(fl[i] & 0x10) == d["overflow"][i]
+        if not d["overflow"][i]:
+            assert b[i] == d["board_out"][i], i
+            assert mk[i] == d["mask"][i], i
+
+
+ENV_CFGS = [
+    dict(obs_mode="raw"),
+    dict(obs_mode="log2", obs_log2_scale=0.0625, reward_mode="log2", base_reward_scale=0.5),
+    dict(obs_mode="onehot", reward_mode="log2", base_reward_scale=0.5, empty_tile_reward=0.1, merge_reward=0.25,
+         bonus_mode="raw", bonus_scale=0.01, step_reward=-0.003, endgame_penalty=-7.5),
+    dict(obs_mode="log2", bonus_mode="log2", bonus_scale=2.0, use_action_mask=False, invalid_action_penalty=-1.5),
+    dict(obs_mode="onehot", reward_mode="sum", base_reward_scale=1.0 / 3.0, empty_tile_reward=-0.07, max_steps=37),
+    dict(obs_mode="raw", max_steps=0),
+]
+
+
+@pytest.mark.parametrize("rng_kind", ["pcg64"])
+@pytest.mark.parametrize("cfg", ENV_CFGS)
+def test_env_step_vs_oracle(cfg, rng_kind):
+    """Game2048Env.step semantics per lane (reward, terminated/truncated, invalid, obs, mask, max_tile_seen)."""
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+
+    n, T = 300, 150
+    env = VecGame2048Env(n, Game2048EnvConfig(**cfg), device=DEV, rng=rng_kind)
+    seeds = [7000 + 13 * i for i in range(n)]
+    obs, _ = env.reset(seed=seeds)
+    ref = [O.Env(**cfg) for _ in range(n)]
+    for e, s in zip(ref, seeds):
+        e.reset(s)
+    width = 272 if cfg["obs_mode"] == "onehot" else 16
+    o0 = (obs["board"] if isinstance(obs, dict) else obs).reshape(n, width).cpu().numpy()
+    for i in range(0, n, 17):
+        np.testing.assert_array_equal(o0[i], ref[i].obs())
+    rng = np.random.default_rng(5)
+    alive = np.ones(n, dtype=bool)
+    for t in range(T):
+        acts = rng.integers(0, 4, size=n)
+        obs, rew, term, trunc, info = env.step(torch.as_tensor(acts, device=DEV))
+        ob = (obs["board"] if isinstance(obs, dict) else obs).reshape(n, width).cpu().numpy()
+        rw, te, tr = rew.cpu().numpy(), term.cpu().numpy(), trunc.cpu().numpy()
+        inv = info["invalid_action"].cpu().numpy()
+        mk = env.mask.cpu().numpy()
+        mt = env.max_tile_seen.cpu().numpy()
+        sc = env.step_count.cpu().numpy()
+        for i in np.nonzero(alive)[0]:
+            r = ref[i].step(int(acts[i]))
+            assert rw[i] == np.float32(r["reward"]), (t, i, rw[i], r["reward"])
+            assert bool(te[i]) == r["terminated"] and bool(tr[i]) == r["truncated"], (t, i)
+            assert bool(inv[i]) == r["invalid"], (t, i)
+            np.testing.assert_array_equal(ob[i], ref[i].obs())
+            np.testing.assert_array_equal(mk[i], ref[i].mask())
+            assert mt[i] == ref[i].max_tile_seen and sc[i] == ref[i].step_count
+            if r["terminated"] or r["truncated"]:
+                alive[i] = False
+        if not alive.any():
+            break
+
+
+def test_auto_reset_matches_reseeded_oracle():
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+
+    n, T, stride = 64, 400, 1000
+    cfg = dict(obs_mode="log2", max_steps=60)
+    env = VecGame2048Env(n, Game2048EnvConfig(**cfg), device=DEV, auto_reset=True, reset_stride=stride)
+    env.reset(seed=5)
+    ref = [O.Env(**cfg) for _ in range(n)]
+    seeds = [5 + i for i in range(n)]
+    for e, s in zip(ref, seeds):
+        e.reset(s)
+    rng = np.random.default_rng(9)
+    n_resets = 0
+    for t in range(T):
+        acts = rng.integers(0, 4, size=n)
+        env.step(torch.as_tensor(acts, device=DEV))
+        fl = env.flags.cpu().numpy()
+        b = env.boards_values().cpu().numpy()
+        for i in range(n):
+            r = ref[i].step(int(acts[i]))
+            if r["terminated"] or r["truncated"]:
+                assert fl[i] & 0x20
+                seeds[i] += stride
+                ref[i].reset(seeds[i])
+                n_resets += 1
+            np.testing.assert_array_equal(b[i], ref[i].board)
+    assert n_resets > n
+
+
+def test_obs_kernel_vs_oracle(lib):
+    rng = np.random.default_rng(2)
+    n = 1000 + 37  # not a multiple of the wave
+    e = rng.integers(1, 16, size=(n, 16))
+    e[rng.random((n, 16)) < 0.4] = 0
+    boards = np.array([O.pack_exponents(x) for x in e], dtype=np.uint64)
+    b = _u64(boards)
+    for mode, name, width in ((0, "raw", 16), (1, "log2", 16), (2, "onehot", 272)):
+        obs = torch.full((n, width), -3.0, device=DEV)
+        mask = torch.zeros(n, 4, dtype=torch.int8, device=DEV)
+        lib.check(lib.lib().g2048_obs(b.data_ptr(), mode, 0.25, obs.data_ptr(), mask.data_ptr(), n,
+                                      lib.stream_handle(DEV)))
+        oh, mh = obs.cpu().numpy(), mask.cpu().numpy()
+        for i in range(0, n, 11):
+            env = O.Env(obs_mode=name, obs_log2_scale=0.25)
+            env.e.game.board[:] = [int(v) for v in np.where(e[i] > 0, np.left_shift(1, e[i]), 0)]
+            np.testing.assert_array_equal(oh[i], env.obs())
+            np.testing.assert_array_equal(mh[i], env.mask())
+
+
+def test_sample_given_identical_probs(lib, golden_dir):
+    """select_action: device masked softmax ~= numpy logits_to_probs (<= 2 ulp-ish), and the drawn action equals
+    Generator.choice(4, p) replayed on the device's own probs with the same PCG64 stream (bit-exact)."""
+    d = np.load(os.path.join(golden_dir, "mlp.npz"))
+    rng = np.random.default_rng(8)
+    n = 4096
+    logits = (rng.standard_normal((n, 4)) * 4).astype(np.float32)
+    mask = (rng.random((n, 4)) < 0.7).astype(np.int8)
+    mask[mask.sum(1) == 0, 1] = 1
+    seeds = [int(s) for s in rng.integers(0, 2**62, size=n)]
+    st = torch.zeros(2 * n, dtype=torch.int64, device=DEV)
+    inc = torch.zeros(2 * n, dtype=torch.int64, device=DEV)
+    buf = torch.zeros(n, dtype=torch.int64, device=DEV)
+    sd = _u64(seeds)
+    L = lib.lib()
+    s = lib.stream_handle(DEV)
+    lib.check(L.g2048_seed_pcg64(sd.data_ptr(), st.data_ptr(), inc.data_ptr(), buf.data_ptr(), n, s))
+    lg = torch.from_numpy(logits).to(DEV)
+    mk = torch.from_numpy(mask).to(DEV)
+    probs = torch.zeros(n, 4, device=DEV)
+    acts = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    refs = [O.PCG64(x) for x in seeds]
+    for rep in range(3):
+        lib.check(L.g2048_sample(lg.data_ptr(), mk.data_ptr(), None, 0, 0, st.data_ptr(), inc.data_ptr(),
+                                 buf.data_ptr(), 0, None, None, probs.data_ptr(), acts.data_ptr(), n, s))
+        p = probs.cpu().numpy()
+        a = acts.cpu().numpy()
+        lgm = np.where(mask.astype(bool), logits, np.float32(-1e9))
+        ex = np.exp(lgm - lgm.max(-1, keepdims=True))
+        p_ref = ex / ex.sum(-1, keepdims=True)
+        np.testing.assert_allclose(p, p_ref, rtol=2e-6, atol=1e-7)
+        for i in range(n):
+            assert a[i] == refs[i].choice4(p[i]), (rep, i)
+    # greedy: argmax(probs * mask)
+    lib.check(L.g2048_sample(lg.data_ptr(), mk.data_ptr(), None, 1, 0, None, None, None, 0, None, None, None,
+                             acts.data_ptr(), n, s))
+    np.testing.assert_array_equal(acts.cpu().numpy(), np.argmax(p * mask, axis=1))
+    del d
+
+
+def test_returns_kernel(lib):
+    rng = np.random.default_rng(3)
+    T, n = 200, 777
+    lengths = rng.integers(0, T + 1, size=n).astype(np.int32)
+    rew = rng.standard_normal((T, n)).astype(np.float32)
+    out = torch.zeros(T, n, device=DEV)
+    r = torch.from_numpy(rew).to(DEV)
+    ln = torch.from_numpy(lengths).to(DEV)
+    for gamma in (1.0, 0.99, 0.5):
+        lib.check(lib.lib().g2048_returns(r.data_ptr(), ln.data_ptr(), gamma, out.data_ptr(), T, n,
+                                          lib.stream_handle(DEV)))
+        o = out.cpu().numpy()
+        for i in range(0, n, 5):
+            G = 0.0
+            exp = np.zeros(lengths[i], dtype=np.float32)
+            for t in reversed(range(lengths[i])):   # src/reinforce_agent.py:269-271
+                G = float(rew[t, i]) + gamma * G
+                exp[t] = G
+            np.testing.assert_array_equal(o[: lengths[i], i], exp)
+
+
+def test_symmetries_kernel(lib):
+    rng = np.random.default_rng(4)
+    n = 999
+    e = rng.integers(0, 16, size=(n, 16))
+    boards = np.array([O.pack_exponents(x) for x in e], dtype=np.uint64)
+    acts = rng.integers(0, 4, size=n).astype(np.uint8)
+    ob = torch.zeros(8 * n, dtype=torch.int64, device=DEV)
+    oa = torch.zeros(8 * n, dtype=torch.uint8, device=DEV)
+    b = _u64(boards)
+    a = torch.from_numpy(acts).to(DEV)
+    lib.check(lib.lib().g2048_symmetries(b.data_ptr(), a.data_ptr(), ob.data_ptr(), oa.data_ptr(), n,
+                                         lib.stream_handle(DEV)))
+    obh, oah = _to_u64(ob).reshape(8, n), oa.cpu().numpy().reshape(8, n)
+    from rl2048_amd.env import Game2048Env
+
+    for i in range(0, n, 13):
+        B = e[i].reshape(4, 4).astype(np.float32)
+        syms = Game2048Env.get_symmetries(B, int(acts[i]))   # host restatement of src/env.py:317-398
+        for k in range(8):
+            sb, sa = syms[k]
+            assert O.unpack_exponents(int(obh[k, i])).tolist() == sb.astype(np.int64).tolist(), (i, k)
+            assert oah[k, i] == sa
+
+
+def test_game2048_dropin_vs_golden(golden_dir):
+    """The single-board Game2048 drop-in returns exactly what the reference returned (first 6 episodes)."""
+    from rl2048_amd import Game2048
+
+    d = np.load(os.path.join(golden_dir, "episodes.npz"))
+    for e in range(6):
+        g = Game2048(device=DEV)
+        st = g.reset(seed=int(d["ep_seed"][e]))
+        assert O.pack_exponents(O.values_to_exponents(np.array(st))) == d["reset_board"][e]
+        s0, n = int(d["ep_start"][e]), int(d["ep_len"][e])
+        for t in range(s0, s0 + min(n, 120)):
+            ch, s, mg, dn = g.step(int(d["action"][t]))
+            assert O.pack_exponents(O.values_to_exponents(np.array(s))) == d["board"][t]
+            assert ch == bool(d["changed"][t]) and dn == bool(d["done"][t])
+            gm = [int((int(d["merged"][t]) >> (5 * k)) & 31) for k in range(int(d["n_merged"][t]))]
+            assert [int(v).bit_length() - 1 for v in mg] == gm
+            assert g.score == d["score"][t]
+            assert sum(b << i for i, b in enumerate(g.get_action_mask())) == d["mask"][t]
+    with pytest.raises(ValueError):
+        Game2048(device=DEV).step(4)
+
+
+def test_env_dropin_vs_oracle():
+    from rl2048_amd import Game2048Env, Game2048EnvConfig
+
+    cfg = dict(obs_mode="onehot", reward_mode="log2", base_reward_scale=0.5, bonus_mode="log2", max_steps=200)
+    env = Game2048Env(Game2048EnvConfig(**cfg), device=DEV)
+    ref = O.Env(**cfg)
+    obs, info = env.reset(seed=123)
+    ref.reset(123)
+    np.testing.assert_array_equal(obs["board"].reshape(-1), ref.obs())
+    rng = np.random.default_rng(0)
+    for t in range(200):
+        a = int(rng.integers(4))
+        obs, r, te, tr, info = env.step(a)
+        rr = ref.step(a)
+        assert r == float(np.float32(rr["reward"])) and te == rr["terminated"] and tr == rr["truncated"]
+        assert info["invalid_action"] == rr["invalid"] and info["score"] == ref.score
+        np.testing.assert_array_equal(obs["board"].reshape(-1), ref.obs())
+        np.testing.assert_array_equal(obs["action_mask"], ref.mask())
+        assert env.max_tile_seen == ref.max_tile_seen
+        if te or tr:
+            break
+    with pytest.raises(AssertionError):
+        env.step(7)
+    with pytest.raises(ValueError):
+        Game2048Env(Game2048EnvConfig(obs_mode="bogus"), device=DEV)
+
+
+def test_philox_mode_distribution():
+    """Throughput mode: spawn 2:4 = 0.9:0.1 and a uniform empty cell (distributional KAT of _spawn
+    src/game2048.py:108-118), boards still obey the game rules (checked against the oracle's move)."""
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+
+    n = 1 << 16
+    env = VecGame2048Env(n, Game2048EnvConfig(max_steps=None), device=DEV, rng="philox", auto_reset=True)
+    env.reset(seed=11)
+    e = env.boards_exponents().reshape(n, 16).cpu().numpy()
+    nz = e[e > 0]
+    assert len(nz) == 2 * n
+    frac2 = (nz == 1).mean()
+    assert abs(frac2 - 0.9) < 5 * np.sqrt(0.09 / len(nz))
+    cells = np.bincount(np.nonzero(e)[1], minlength=16)
+    assert cells.min() > 0.9 * cells.mean()
+    prev = _to_u64(env.board)
+    acts = np.random.default_rng(1).integers(0, 4, size=n)
+    env.step(torch.as_tensor(acts, device=DEV))
+    nb = _to_u64(env.board)
+    fl = env.flags.cpu().numpy()
+    for i in range(0, n, 97):
+        mv, _, ch, ok = O.move_packed(int(prev[i]), int(acts[i]))
+        if fl[i] & 0x20:
+            continue
+        diff = int(nb[i]) ^ mv
+        if ch:   # exactly one new 2 or 4 in a cell that was empty after the move
+            cell = (diff.bit_length() - 1) // 4
+            assert diff == ((int(nb[i]) >> (4 * cell)) & 15) << (4 * cell)
+            assert ((mv >> (4 * cell)) & 15) == 0
+        else:
+            assert diff == 0
