@@ -60,7 +60,7 @@ class StepOut(ctypes.Structure):
 
 
 _lib = None
-_lock = threading.Lock()
+_lock = threading.RLock()
 _inited_devices: set[int] = set()
 
 

@@ -134,9 +134,10 @@ def test_crafted_boards_vs_golden(golden_dir):
     for i in range(n):
         gm = [int((int(d["merged"][i]) >> (5 * k)) & 31) for k in range(int(d["n_merged"][i]))]
         assert _merged_exps(mg[i]) == gm, i
-        assert bool(fl[i] & 1) == d["changed"][i] and bool(fl[i] & 2) == d["done"][i], i
+        assert bool(fl[i] & 1) == d["changed"][i], i
         assert bool(fl[i] & 0x10) == d["overflow"][i]
-        if not d["overflow"][i]:
+        if not d["overflow"][i]:   # a saturated 2**15+2**15 lane's board (hence done / mask) is not the reference's
+            assert bool(fl[i] & 2) == d["done"][i], i
             assert b[i] == d["board_out"][i], i
             assert mk[i] == d["mask"][i], i
 
