@@ -1,18 +1,23 @@
 // g2048.hip -- gfx950 (MI355X / CDNA4) kernels and the C ABI of libg2048.so (declared in include/g2048.h).
 //
-// One board per lane, uint64 bitboard (nibble r*4+c = log2 tile).  The hot kernel is g2048_step:
-//   * integer/indexing work, no MFMA: the HBM stream of lane state is the roofline ("Kernels");
-//   * the 65,536-entry move-left line table (uint16, 128 KiB) is staged once per workgroup into LDS and each
-//     move is 4 LDS lookups (one per line of the move-left frame);
-//   * action mask / done are 64-bit SWAR expressions (no table);
-//   * the spawn draws the k-th empty cell with popcount bisection on the nibble-empty mask (numpy PCG64
-//     stream in parity mode, Philox4x32-10 in throughput mode);
-//   * observations are written wave-cooperatively: every store instruction covers 1 KiB of contiguous obs,
-//     the owning board is fetched from its lane with a cross-lane shuffle.
-// Workgroups are persistent over the board array (grid <= one 1024-thread workgroup per CU, limited by the
-// 128 KiB LDS table), so the table fill is paid once per CU per launch.
+// One board per lane, uint64 bitboard (nibble r*4+c = log2 tile).  The hot kernel is g2048_step
+// (integer / indexing work, no MFMA; DESIGN.md "Kernels" has its roofline):
+//   * two row tables are staged once per workgroup into LDS and fill it exactly (160 KiB): the move-left image
+//     of every 4-nibble line (65,536 x uint16) and its 4-bit merge code (which output cells are merge results),
+//     so a move is 4 x (one u16 + one nibble LDS lookup) with the merge summary read off the new line;
+//   * action mask and done are 64-bit SWAR expressions sharing one set of neighbour masks;
+//   * the spawn draws the k-th empty cell by popcount bisection (numpy-PCG64 stream in parity mode,
+//     Philox4x32-10 in throughput mode);
+//   * auto-resets (SeedSequence + two spawns) are deferred to the end of the wave's board loop and done in one
+//     batch, so a rare reset costs one divergent pass per wave instead of one per board sweep;
+//   * observations are written wave-cooperatively (every store instruction is 1 KiB of contiguous obs; the
+//     owning board comes from its lane through a cross-lane shuffle);
+//   * 32-bit byte offsets on SGPR bases (the launcher splits calls above kMaxLanesPerLaunch lanes).
+// Workgroups are persistent (one 1024-thread workgroup per CU: the LDS tables allow one), so the table fill
+// is paid once per CU per launch.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <string>
 
@@ -26,7 +31,7 @@ namespace {
 thread_local std::string g_err;
 std::mutex g_mu;
 constexpr int kMaxDev = 64;
-uint16_t* g_lut[kMaxDev] = {};
+uint8_t* g_tab[kMaxDev] = {};   // [65536 x u16 line table][32768 x u8 merge codes, two per byte]
 int g_cus[kMaxDev] = {};
 
 int fail(int code, const std::string& msg) {
@@ -34,19 +39,36 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
-#define G2048_HIP(x)                                                                              \
-    do {                                                                                          \
-        hipError_t e_ = (x);                                                                      \
+#define G2048_HIP(x)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
         if (e_ != hipSuccess) return fail(G2048_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-constexpr int kBlock = 1024;         // 16 waves per CU; one workgroup per CU (LDS table)
-constexpr int kLutEntries = 65536;
-constexpr int kLutSmallN = 16384;    // below this many lanes the table is read from L2 instead of LDS
+constexpr int kBlock = 1024;                  // 16 waves per CU; one workgroup per CU (160 KiB of LDS tables)
+constexpr int kLines = 65536;
+constexpr int kTabBytes = kLines * 2 + kLines / 2;   // 163,840 B = the whole LDS of a gfx950 CU
+constexpr int kTabVec = kTabBytes / 16;
+constexpr int kLutSmallN = 16384;             // below this many lanes the tables are read through L1/L2
+constexpr int64_t kMaxLanesPerLaunch = int64_t(1) << 27;   // keeps every byte offset (<= 16 B/lane) in 32 bits
 
-struct LutFn {
-    const uint16_t* t;
-    __device__ uint32_t operator()(uint32_t i) const { return t[i]; }
+// ------------------------------------------------------------------------------------- addressing helpers
+template <class T>
+__device__ __forceinline__ T ld(const T* p, uint32_t idx) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(p) + idx * (uint32_t)sizeof(T));
+}
+template <class T>
+__device__ __forceinline__ void st(T* p, uint32_t idx, T v) {
+    *reinterpret_cast<T*>(reinterpret_cast<char*>(p) + idx * (uint32_t)sizeof(T)) = v;
+}
+
+struct LineFn {
+    const uint16_t* line;
+    __device__ uint32_t operator()(uint32_t o) const { return line[o]; }
+};
+struct CodeFn {
+    const uint8_t* code;
+    __device__ uint32_t operator()(uint32_t o) const { return (code[o >> 1] >> ((o & 1u) << 2)) & 15u; }
 };
 
 __device__ inline uint64_t shfl64(uint64_t v, int src) {
@@ -55,44 +77,50 @@ __device__ inline uint64_t shfl64(uint64_t v, int src) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// Write obs for the 64 boards [w0, w0+64) held one per lane in `b` (lanes whose bit in `wmask` is clear
-// write nothing).  Every store instruction covers a contiguous 1 KiB slice of the wave's obs region.
+__device__ inline uint32_t nib(uint64_t b, uint32_t cell) { return (uint32_t)(b >> (4u * cell)) & 15u; }
+
+// ------------------------------------------------------------------------------------- observation writers
+// Write obs for the 64 boards [w0, w0+64) held one per lane in `b` (lanes whose bit in `wmask` is clear write
+// nothing).  Every store instruction covers a contiguous 1 KiB slice of the wave's obs region.
 template <int OBS>
-__device__ inline void write_obs_wave(float* __restrict__ obs, int64_t w0, uint64_t b, uint64_t wmask, int lane,
+__device__ inline void write_obs_wave(float* __restrict__ obs, uint32_t w0, uint64_t b, uint64_t wmask, int lane,
                                       float scale) {
     if constexpr (OBS == G2048_OBS_ONEHOT) {
-        float4* dst = reinterpret_cast<float4*>(obs + w0 * 272);
+        float4* dst = reinterpret_cast<float4*>(obs) + (size_t)w0 * 68;
 #pragma unroll 4
         for (int k = 0; k < 68; k++) {
-            const int q = k * 64 + lane;       // float4 index in the wave's region
-            const int src = q / 68;            // owning board (lane)
-            const int j = (q - src * 68) * 4;  // first float index inside the board's 272
+            const int q = k * 64 + lane;         // float4 index in the wave's region
+            const int src = q / 68;              // owning board (lane)
+            const int j = (q - src * 68) * 4;    // first float index inside the board's 272 (a multiple of 4)
             const uint64_t bb = shfl64(b, src);
             if ((wmask >> src) & 1ull) {
-                float v[4];
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const int idx = j + t;
-                    const int cell = idx / 17;
-                    const int ch = idx - cell * 17;
-                    v[t] = ((int)((bb >> (4 * cell)) & 15u) == ch) ? 1.0f : 0.0f;
-                }
-                dst[q] = make_float4(v[0], v[1], v[2], v[3]);
+                // the four floats j..j+3 touch at most two cells; each cell's one-hot 1 sits at 17*cell + e
+                const int c0 = j / 17;
+                const int c1 = c0 + 1 < 16 ? c0 + 1 : 15;
+                const int p0 = 17 * c0 + (int)nib(bb, c0);
+                const int p1 = 17 * c1 + (int)nib(bb, c1);
+                float4 v;
+                v.x = (j == p0 || j == p1) ? 1.0f : 0.0f;
+                v.y = (j + 1 == p0 || j + 1 == p1) ? 1.0f : 0.0f;
+                v.z = (j + 2 == p0 || j + 2 == p1) ? 1.0f : 0.0f;
+                v.w = (j + 3 == p0 || j + 3 == p1) ? 1.0f : 0.0f;
+                dst[q] = v;
             }
         }
     } else if constexpr (OBS == G2048_OBS_LOG2 || OBS == G2048_OBS_RAW) {
-        float4* dst = reinterpret_cast<float4*>(obs + w0 * 16);
+        float4* dst = reinterpret_cast<float4*>(obs) + (size_t)w0 * 4;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int q = k * 64 + lane;
             const int src = q >> 2;
-            const int row = q & 3;
+            const uint32_t row = (uint32_t)q & 3u;
             const uint64_t bb = shfl64(b, src);
             if ((wmask >> src) & 1ull) {
+                const uint32_t r16 = (uint32_t)(bb >> (16u * row));
                 float v[4];
 #pragma unroll
                 for (int t = 0; t < 4; t++) {
-                    const uint32_t e = (uint32_t)(bb >> (16 * row + 4 * t)) & 15u;
+                    const uint32_t e = (r16 >> (4 * t)) & 15u;
                     if constexpr (OBS == G2048_OBS_LOG2) v[t] = (float)e * scale;
                     else v[t] = e ? (float)(1u << e) : 0.0f;
                 }
@@ -102,17 +130,44 @@ __device__ inline void write_obs_wave(float* __restrict__ obs, int64_t w0, uint6
     }
 }
 
-__device__ inline void store_mask(int8_t* mask, int64_t i, uint32_t m) {
-    // int8[4] per board, one 32-bit store: byte a = bit a
-    const uint32_t w = (m & 1u) | ((m & 2u) << 7) | ((m & 4u) << 14) | ((m & 8u) << 21);
-    reinterpret_cast<uint32_t*>(mask)[i] = w;
+// one lane's own obs (used for the rare deferred auto-resets)
+template <int OBS>
+__device__ inline void write_obs_lane(float* __restrict__ obs, uint32_t i, uint64_t b, float scale) {
+    if constexpr (OBS == G2048_OBS_ONEHOT) {
+        float4* dst = reinterpret_cast<float4*>(obs) + (size_t)i * 68;
+        for (int k = 0; k < 68; k++) {
+            const int j = 4 * k;
+            const int c0 = j / 17;
+            const int c1 = c0 + 1 < 16 ? c0 + 1 : 15;
+            const int p0 = 17 * c0 + (int)nib(b, c0), p1 = 17 * c1 + (int)nib(b, c1);
+            dst[k] = make_float4((j == p0 || j == p1) ? 1.f : 0.f, (j + 1 == p0 || j + 1 == p1) ? 1.f : 0.f,
+                                 (j + 2 == p0 || j + 2 == p1) ? 1.f : 0.f, (j + 3 == p0 || j + 3 == p1) ? 1.f : 0.f);
+        }
+    } else if constexpr (OBS == G2048_OBS_LOG2 || OBS == G2048_OBS_RAW) {
+        float4* dst = reinterpret_cast<float4*>(obs) + (size_t)i * 4;
+        for (int r = 0; r < 4; r++) {
+            float v[4];
+            for (int t = 0; t < 4; t++) {
+                const uint32_t e = nib(b, 4 * r + t);
+                if constexpr (OBS == G2048_OBS_LOG2) v[t] = (float)e * scale;
+                else v[t] = e ? (float)(1u << e) : 0.0f;
+            }
+            dst[r] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
 }
 
-__device__ inline Pcg64 load_pcg(const g2048_lanes& L, int64_t i) {
+__device__ inline uint32_t mask_word(uint32_t m) {
+    // int8[4] per board as one 32-bit word: byte a = bit a
+    return (m & 1u) | ((m & 2u) << 7) | ((m & 4u) << 14) | ((m & 8u) << 21);
+}
+
+// ------------------------------------------------------------------------------------- RNG state
+__device__ inline Pcg64 load_pcg(const g2048_lanes& L, uint32_t i) {
     Pcg64 g;
-    const ulonglong2 s = reinterpret_cast<const ulonglong2*>(L.rng_state)[i];
-    const ulonglong2 c = reinterpret_cast<const ulonglong2*>(L.rng_inc)[i];
-    const uint64_t buf = L.rng_buf[i];
+    const ulonglong2 s = ld(reinterpret_cast<const ulonglong2*>(L.rng_state), i);
+    const ulonglong2 c = ld(reinterpret_cast<const ulonglong2*>(L.rng_inc), i);
+    const uint64_t buf = ld(L.rng_buf, i);
     g.s_lo = s.x;
     g.s_hi = s.y;
     g.i_lo = c.x;
@@ -122,10 +177,10 @@ __device__ inline Pcg64 load_pcg(const g2048_lanes& L, int64_t i) {
     return g;
 }
 
-__device__ inline void store_pcg(const g2048_lanes& L, int64_t i, const Pcg64& g, bool with_inc) {
-    reinterpret_cast<ulonglong2*>(L.rng_state)[i] = make_ulonglong2(g.s_lo, g.s_hi);
-    if (with_inc) reinterpret_cast<ulonglong2*>(L.rng_inc)[i] = make_ulonglong2(g.i_lo, g.i_hi);
-    L.rng_buf[i] = ((uint64_t)g.has_uint32 << 32) | g.uinteger;
+__device__ inline void store_pcg(const g2048_lanes& L, uint32_t i, const Pcg64& g, bool with_inc) {
+    st(reinterpret_cast<ulonglong2*>(L.rng_state), i, make_ulonglong2(g.s_lo, g.s_hi));
+    if (with_inc) st(reinterpret_cast<ulonglong2*>(L.rng_inc), i, make_ulonglong2(g.i_lo, g.i_hi));
+    st(L.rng_buf, i, ((uint64_t)g.has_uint32 << 32) | g.uinteger);
 }
 
 __device__ inline U4 philox_ctr(uint64_t key, uint64_t seed, uint32_t ctr, uint32_t tag) {
@@ -142,12 +197,14 @@ __device__ inline uint64_t fresh_board(uint64_t seed, uint64_t key, Pcg64& g) {
         b = spawn_pcg(b, g);
         b = spawn_pcg(b, g);
     } else {
-        b = spawn_philox(b, philox_ctr(key, seed, 0u, 1u));
-        b = spawn_philox(b, philox_ctr(key, seed, 0u, 2u));
+        const U4 r = philox_ctr(key, seed, 0u, 1u);
+        b = spawn_philox(b, U4{r.x, r.y, 0u, 0u});
+        b = spawn_philox(b, U4{r.z, r.w, 0u, 0u});
     }
     return b;
 }
 
+// ------------------------------------------------------------------------------------- step
 struct StepArgs {
     g2048_lanes L;
     const uint8_t* actions;
@@ -157,107 +214,160 @@ struct StepArgs {
     int auto_reset;
     int64_t max_steps;
     uint64_t stride, key;
-    const uint16_t* lut;
-    int64_t n;
+    const uint8_t* tab;
+    uint32_t n;
 };
 
-// One lane of Game2048Env.step (src/env.py:264-302).  Returns the board the obs/mask describe and whether
-// this lane writes obs.
-template <int RNG>
-__device__ inline uint64_t step_lane(const StepArgs& a, int64_t i, const uint16_t* lut, bool& wobs) {
+// Auto-reset of one lane (deferred to the end of the wave's loop): Game2048Env.reset with seed += stride.
+template <int OBS, int RNG>
+__device__ inline void reset_lane(const StepArgs& a, uint32_t i) {
     const g2048_lanes& L = a.L;
-    const uint64_t b = L.board[i];
-    const uint8_t st = L.status[i];
-    const uint32_t act = a.actions[i];
-    if (a.out.prev_board) a.out.prev_board[i] = b;
-    if (!(st & G2048_S_ACTIVE) || act > 3u) {
-        a.out.reward[i] = 0.0f;
-        a.out.flags[i] = (st & G2048_S_ACTIVE) ? G2048_F_BADACTION : G2048_F_INACTIVE;
-        if (a.out.merged) a.out.merged[i] = 0u;
-        wobs = false;
+    const uint64_t seed = ld(L.seed, i) + a.stride;
+    Pcg64 g;
+    const uint64_t b = fresh_board<RNG>(seed, a.key, g);
+    st(L.seed, i, seed);
+    st(L.board, i, b);
+    st(L.step_count, i, 0u);
+    st(L.score, i, 0u);
+    st(L.max_tile, i, (uint8_t)2);
+    if constexpr (RNG == G2048_RNG_PCG64) store_pcg(L, i, g, true);
+    if (a.out.mask) st(reinterpret_cast<uint32_t*>(a.out.mask), i, mask_word(action_mask(b)));
+    if constexpr (OBS != G2048_OBS_NONE)
+        if (a.out.obs) write_obs_lane<OBS>(a.out.obs, i, b, a.obs_scale);
+}
+
+// Everything one lane reads for one board's step (all boards of a sweep are loaded before any is computed).
+struct LaneIn {
+    uint64_t b, seed;
+    uint32_t stt, act, sc, mt, score;
+    Pcg64 g;
+};
+
+template <int RNG>
+__device__ inline void load_lane(const StepArgs& a, uint32_t i, LaneIn& x) {
+    const g2048_lanes& L = a.L;
+    x.b = ld(L.board, i);
+    x.stt = ld(L.status, i);
+    x.act = ld(a.actions, i);
+    x.sc = ld(L.step_count, i);
+    x.mt = ld(L.max_tile, i);
+    x.score = ld(L.score, i);
+    if constexpr (RNG == G2048_RNG_PCG64) x.g = load_pcg(L, i);   // PCG64 mode reads the seed only on reset
+    else x.seed = ld(L.seed, i);
+}
+
+// One lane of Game2048Env.step (src/env.py:264-302).  Returns the final board; wobs = this lane's obs/mask are
+// written by the wave; reset = the episode ended and an auto-reset is pending for this lane.
+template <int RNG, bool LIST>
+__device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, const LineFn& lut,
+                                     const CodeFn& code, bool& wobs, bool& reset, uint32_t& mbits) {
+    const g2048_lanes& L = a.L;
+    const uint64_t b = x.b;
+    if (a.out.prev_board) st(a.out.prev_board, i, b);
+    wobs = false;
+    reset = false;
+    if (!(x.stt & G2048_S_ACTIVE) || x.act > 3u) {
+        st(a.out.reward, i, 0.0f);
+        st(a.out.flags, i, (uint8_t)((x.stt & G2048_S_ACTIVE) ? G2048_F_BADACTION : G2048_F_INACTIVE));
+        if (a.out.merged) st(a.out.merged, i, 0u);
         return b;
     }
-    uint32_t sc = L.step_count[i] + 1u;
-    uint32_t mt = L.max_tile[i];
-    uint32_t score = L.score[i];
-    uint64_t seed = 0;
-    if constexpr (RNG == G2048_RNG_PHILOX) seed = L.seed[i];  // PCG64 mode reads it only on auto-reset
-    Pcg64 g;
-    if constexpr (RNG == G2048_RNG_PCG64) g = load_pcg(L, i);
+    const uint32_t sc = x.sc + 1u;
+    uint32_t mt = x.mt;
 
     // Game2048.step (src/game2048.py:40-70): move, score, spawn only if changed, done of the final board
     MoveSummary s;
-    uint64_t m = board_move(b, act, LutFn{lut}, s);
+    uint64_t m = board_move_coded<LIST>(b, x.act, lut, code, s);
     const bool changed = m != b;
-    score += s.score;
     if (changed) {
-        if constexpr (RNG == G2048_RNG_PCG64) m = spawn_pcg(m, g);
-        else m = spawn_philox(m, philox_ctr(a.key, seed, sc, 0u));
+        if constexpr (RNG == G2048_RNG_PCG64) m = spawn_pcg(m, x.g);
+        else m = spawn_philox(m, philox_ctr(a.key, x.seed, sc, 0u));
     }
-    const bool done = is_done(m);
+    const BoardBits bits = board_bits(m);
+    const bool done = bits_done(bits);
     const bool invalid = !changed && !done;
     const double r = env_reward(a.rc, s, m, done, invalid, mt);
     const bool trunc = a.max_steps >= 0 && (int64_t)sc >= a.max_steps && !done;
-    uint32_t fl = (changed ? G2048_F_CHANGED : 0u) | (done ? G2048_F_TERMINATED : 0u) |
-                  (trunc ? G2048_F_TRUNCATED : 0u) | (invalid ? G2048_F_INVALID : 0u) |
-                  (s.overflow ? G2048_F_OVERFLOW : 0u);
-    uint8_t nst = st;
-    bool new_inc = false;
-    if (done || trunc) {
-        if (a.auto_reset) {
-            if constexpr (RNG == G2048_RNG_PCG64) seed = L.seed[i];
-            seed += a.stride;
-            m = fresh_board<RNG>(seed, a.key, g);
-            new_inc = true;
-            sc = 0u;
-            score = 0u;
-            mt = 2u;
-            fl |= G2048_F_RESET;
-            L.seed[i] = seed;
-        } else {
-            nst = (uint8_t)(st & ~G2048_S_ACTIVE);
-            L.status[i] = nst;
-        }
+    const uint32_t fl = (changed ? G2048_F_CHANGED : 0u) | (done ? G2048_F_TERMINATED : 0u) |
+                        (trunc ? G2048_F_TRUNCATED : 0u) | (invalid ? G2048_F_INVALID : 0u) |
+                        (s.overflow ? G2048_F_OVERFLOW : 0u);
+    st(a.out.reward, i, (float)r);
+    if (LIST && a.out.merged) st(a.out.merged, i, s.list);
+    if ((done || trunc) && a.auto_reset) {
+        reset = true;   // board / lane state / obs are written by reset_lane after the loop
+        st(a.out.flags, i, (uint8_t)(fl | G2048_F_RESET));
+        return m;
     }
-    L.board[i] = m;
-    L.step_count[i] = sc;
-    L.score[i] = score;
-    L.max_tile[i] = (uint8_t)mt;
-    if constexpr (RNG == G2048_RNG_PCG64) store_pcg(L, i, g, new_inc);
-    a.out.reward[i] = (float)r;
-    a.out.flags[i] = (uint8_t)fl;
-    if (a.out.merged) a.out.merged[i] = s.list;
+    if (done || trunc) st(L.status, i, (uint8_t)(x.stt & ~G2048_S_ACTIVE));
+    st(a.out.flags, i, (uint8_t)fl);
+    st(L.board, i, m);
+    st(L.step_count, i, sc);
+    st(L.score, i, x.score + s.score);
+    st(L.max_tile, i, (uint8_t)mt);
+    if constexpr (RNG == G2048_RNG_PCG64) store_pcg(L, i, x.g, false);
     wobs = true;
+    mbits = bits_mask(bits);
     return m;
 }
 
-template <int OBS, int RNG, bool LDS>
+// Persistent over the board array in sweeps of U*64 boards per wave: a lane loads its U boards (lane,
+// lane+64, ...) before computing any, so each wave keeps U boards of HBM traffic in flight; the first sweep's
+// loads are issued before the LDS table fill so they overlap it.  LDS: stage the two row tables in LDS, else
+// read them through L1/L2 (small batches).  Sweeps * U <= 64 (launcher): the `pending` reset bitmask.
+template <int OBS, int RNG, bool LDS, bool LIST, int U>
 __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
-    __shared__ uint4 lut_lds[LDS ? kLutEntries / 8 : 1];
-    const uint16_t* lut = a.lut;
-    if constexpr (LDS) {
-        const uint4* src = reinterpret_cast<const uint4*>(a.lut);
-#pragma unroll 8
-        for (int k = threadIdx.x; k < kLutEntries / 8; k += kBlock) lut_lds[k] = src[k];
-        __syncthreads();
-        lut = reinterpret_cast<const uint16_t*>(lut_lds);
-    }
+    __shared__ uint4 tab_lds[LDS ? kTabVec : 1];
     const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t wstride = ((int64_t)gridDim.x * kBlock) >> 6;
-    for (int64_t w0 = wave * 64; w0 < a.n; w0 += wstride * 64) {
-        const int64_t i = w0 + lane;
-        bool wobs = false;
-        uint64_t b = 0;
-        if (i < a.n) b = step_lane<RNG>(a, i, lut, wobs);
-        if (wobs && a.out.mask) store_mask(a.out.mask, i, action_mask(b));
-        if constexpr (OBS != G2048_OBS_NONE) {
-            const uint64_t wm = __ballot(wobs);
-            if (a.out.obs && wm) write_obs_wave<OBS>(a.out.obs, w0, b, wm, lane, a.obs_scale);
+    const uint32_t w_first = ((blockIdx.x * kBlock + threadIdx.x) & ~63u) * U;
+    const uint32_t wstride = gridDim.x * kBlock * U;
+    LaneIn in[U];
+    uint32_t w0 = w_first;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        if (w0 + 64u * u + lane < a.n) load_lane<RNG>(a, w0 + 64u * u + lane, in[u]);
+    const uint8_t* tab = a.tab;
+    if constexpr (LDS) {
+        const uint4* src = reinterpret_cast<const uint4*>(a.tab);
+#pragma unroll
+        for (int k = threadIdx.x; k < kTabVec; k += kBlock) tab_lds[k] = src[k];
+        __syncthreads();
+        tab = reinterpret_cast<const uint8_t*>(tab_lds);
+    }
+    const LineFn lut{reinterpret_cast<const uint16_t*>(tab)};
+    const CodeFn code{tab + 2 * kLines};
+    uint64_t pending = 0;
+    uint32_t k = 0;
+    for (; w0 < a.n; w0 += wstride, k += U) {
+        if (k) {
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (w0 + 64u * u + lane < a.n) load_lane<RNG>(a, w0 + 64u * u + lane, in[u]);
         }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t base = w0 + 64u * u;
+            if (base >= a.n) break;   // wave-uniform
+            const uint32_t i = base + lane;
+            bool wobs = false, reset = false;
+            uint32_t mbits = 0;
+            uint64_t b = 0;
+            if (i < a.n) b = step_lane<RNG, LIST>(a, i, in[u], lut, code, wobs, reset, mbits);
+            if (reset) pending |= 1ull << (k + u);
+            if (wobs && a.out.mask) st(reinterpret_cast<uint32_t*>(a.out.mask), i, mask_word(mbits));
+            if constexpr (OBS != G2048_OBS_NONE) {
+                const uint64_t wm = __ballot(wobs);
+                if (a.out.obs && wm) write_obs_wave<OBS>(a.out.obs, base, b, wm, lane, a.obs_scale);
+            }
+        }
+    }
+    while (pending) {   // deferred auto-resets of this lane, one pass per pending board
+        const uint32_t kk = (uint32_t)__builtin_ctzll(pending);
+        pending &= pending - 1ull;
+        reset_lane<OBS, RNG>(a, w_first + (kk / U) * wstride + 64u * (kk % U) + lane);
     }
 }
 
+// ------------------------------------------------------------------------------------- other kernels
 struct ResetArgs {
     g2048_lanes L;
     const uint64_t* seeds;
@@ -266,31 +376,31 @@ struct ResetArgs {
     float* obs_out;
     float obs_scale;
     uint64_t key;
-    int64_t n;
+    uint32_t n;
 };
 
 template <int OBS, int RNG>
 __global__ void __launch_bounds__(256) reset_kernel(ResetArgs a) {
     const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t wstride = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t w0 = wave * 64; w0 < a.n; w0 += wstride * 64) {
-        const int64_t i = w0 + lane;
+    const uint32_t w_first = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u;
+    const uint32_t wstride = gridDim.x * blockDim.x;
+    for (uint32_t w0 = w_first; w0 < a.n; w0 += wstride) {
+        const uint32_t i = w0 + lane;
         bool w = false;
         uint64_t b = 0;
-        if (i < a.n && (!a.reset_mask || a.reset_mask[i])) {
-            const uint64_t seed = a.seeds ? a.seeds[i] : a.L.seed[i];
+        if (i < a.n && (!a.reset_mask || ld(a.reset_mask, i))) {
+            const uint64_t seed = a.seeds ? ld(a.seeds, i) : ld(a.L.seed, i);
             Pcg64 g;
             b = fresh_board<RNG>(seed, a.key, g);
-            a.L.seed[i] = seed;
-            a.L.board[i] = b;
-            a.L.step_count[i] = 0u;
-            a.L.score[i] = 0u;
-            a.L.max_tile[i] = 2u;  // Game2048Env.max_tile_seen = 4 (src/env.py:183)
-            a.L.status[i] = G2048_S_ACTIVE;
+            st(a.L.seed, i, seed);
+            st(a.L.board, i, b);
+            st(a.L.step_count, i, 0u);
+            st(a.L.score, i, 0u);
+            st(a.L.max_tile, i, (uint8_t)2);  // Game2048Env.max_tile_seen = 4 (src/env.py:183)
+            st(a.L.status, i, (uint8_t)G2048_S_ACTIVE);
             if constexpr (RNG == G2048_RNG_PCG64) store_pcg(a.L, i, g, true);
             w = true;
-            if (a.mask_out) store_mask(a.mask_out, i, action_mask(b));
+            if (a.mask_out) st(reinterpret_cast<uint32_t*>(a.mask_out), i, mask_word(action_mask(b)));
         }
         if constexpr (OBS != G2048_OBS_NONE) {
             const uint64_t wm = __ballot(w);
@@ -301,15 +411,15 @@ __global__ void __launch_bounds__(256) reset_kernel(ResetArgs a) {
 
 template <int OBS>
 __global__ void __launch_bounds__(256) obs_kernel(const uint64_t* __restrict__ boards, float* obs, int8_t* mask,
-                                                  float scale, int64_t n) {
+                                                  float scale, uint32_t n) {
     const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t wstride = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t w0 = wave * 64; w0 < n; w0 += wstride * 64) {
-        const int64_t i = w0 + lane;
+    const uint32_t w_first = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u;
+    const uint32_t wstride = gridDim.x * blockDim.x;
+    for (uint32_t w0 = w_first; w0 < n; w0 += wstride) {
+        const uint32_t i = w0 + lane;
         const bool v = i < n;
-        const uint64_t b = v ? boards[i] : 0ull;
-        if (v && mask) store_mask(mask, i, action_mask(b));
+        const uint64_t b = v ? ld(boards, i) : 0ull;
+        if (v && mask) st(reinterpret_cast<uint32_t*>(mask), i, mask_word(action_mask(b)));
         if constexpr (OBS != G2048_OBS_NONE) {
             const uint64_t wm = __ballot(v);
             if (obs) write_obs_wave<OBS>(obs, w0, b, wm, lane, scale);
@@ -318,32 +428,34 @@ __global__ void __launch_bounds__(256) obs_kernel(const uint64_t* __restrict__ b
 }
 
 __global__ void __launch_bounds__(256) move_kernel(const uint64_t* __restrict__ boards, const uint8_t* __restrict__ actions,
-                                                   const uint16_t* __restrict__ lut, uint64_t* out, uint32_t* merged,
-                                                   uint8_t* flags, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t b = boards[i];
-        const uint32_t act = actions[i];
+                                                   const uint8_t* __restrict__ tab, uint64_t* out, uint32_t* merged,
+                                                   uint8_t* flags, uint32_t n) {
+    const LineFn lut{reinterpret_cast<const uint16_t*>(tab)};
+    const CodeFn code{tab + 2 * kLines};
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t b = ld(boards, i);
+        const uint32_t act = ld(actions, i);
         if (act > 3u) {
-            out[i] = b;
-            if (merged) merged[i] = 0u;
-            if (flags) flags[i] = G2048_F_BADACTION;
+            st(out, i, b);
+            if (merged) st(merged, i, 0u);
+            if (flags) st(flags, i, (uint8_t)G2048_F_BADACTION);
             continue;
         }
         MoveSummary s;
-        const uint64_t m = board_move(b, act, LutFn{lut}, s);
-        out[i] = m;
-        if (merged) merged[i] = s.list;
-        if (flags) flags[i] = (uint8_t)((m != b ? G2048_F_CHANGED : 0u) | (s.overflow ? G2048_F_OVERFLOW : 0u));
+        const uint64_t m = board_move_coded<true>(b, act, lut, code, s);
+        st(out, i, m);
+        if (merged) st(merged, i, s.list);
+        if (flags) st(flags, i, (uint8_t)((m != b ? G2048_F_CHANGED : 0u) | (s.overflow ? G2048_F_OVERFLOW : 0u)));
     }
 }
 
-__global__ void __launch_bounds__(256) seed_kernel(const uint64_t* __restrict__ seeds, uint64_t* st, uint64_t* inc,
-                                                   uint64_t* buf, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const Pcg64 g = pcg_seed(seeds[i]);
-        reinterpret_cast<ulonglong2*>(st)[i] = make_ulonglong2(g.s_lo, g.s_hi);
-        reinterpret_cast<ulonglong2*>(inc)[i] = make_ulonglong2(g.i_lo, g.i_hi);
-        buf[i] = 0ull;
+__global__ void __launch_bounds__(256) seed_kernel(const uint64_t* __restrict__ seeds, uint64_t* rs, uint64_t* inc,
+                                                   uint64_t* buf, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const Pcg64 g = pcg_seed(ld(seeds, i));
+        st(reinterpret_cast<ulonglong2*>(rs), i, make_ulonglong2(g.s_lo, g.s_hi));
+        st(reinterpret_cast<ulonglong2*>(inc), i, make_ulonglong2(g.i_lo, g.i_hi));
+        st(buf, i, (uint64_t)0);
     }
 }
 
@@ -351,31 +463,31 @@ struct SampleArgs {
     const float* logits;
     const int8_t* mask;
     const uint8_t* active;
-    uint64_t *st, *inc, *buf;
+    uint64_t *rs, *inc, *buf;
     uint64_t key;
     const uint64_t* lane_seed;
     const uint32_t* counter;
     float* probs_out;
     uint8_t* actions;
-    int64_t n;
+    uint32_t n;
     int greedy;
 };
 
 // logits_to_probs (src/MLP.py:139-156) + select_action (src/reinforce_agent.py:178-190)
 template <int RNG>
 __global__ void __launch_bounds__(256) sample_kernel(SampleArgs a) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
-        if (a.active && !a.active[i]) continue;
-        const float4 lg = reinterpret_cast<const float4*>(a.logits)[i];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+        if (a.active && !ld(a.active, i)) continue;
+        const float4 lg = ld(reinterpret_cast<const float4*>(a.logits), i);
         uint32_t mw = 0x01010101u;
-        if (a.mask) mw = reinterpret_cast<const uint32_t*>(a.mask)[i];
+        if (a.mask) mw = ld(reinterpret_cast<const uint32_t*>(a.mask), i);
         const bool m0 = mw & 0xFFu, m1 = (mw >> 8) & 0xFFu, m2 = (mw >> 16) & 0xFFu, m3 = mw >> 24;
         const float l0 = m0 ? lg.x : -1e9f, l1 = m1 ? lg.y : -1e9f, l2 = m2 ? lg.z : -1e9f, l3 = m3 ? lg.w : -1e9f;
         const float mx = fmaxf(fmaxf(l0, l1), fmaxf(l2, l3));
         const float e0 = expf(l0 - mx), e1 = expf(l1 - mx), e2 = expf(l2 - mx), e3 = expf(l3 - mx);
         const float s = ((e0 + e1) + e2) + e3;
         const float p[4] = {e0 / s, e1 / s, e2 / s, e3 / s};
-        if (a.probs_out) reinterpret_cast<float4*>(a.probs_out)[i] = make_float4(p[0], p[1], p[2], p[3]);
+        if (a.probs_out) st(reinterpret_cast<float4*>(a.probs_out), i, make_float4(p[0], p[1], p[2], p[3]));
         uint32_t act = 0;
         if (a.greedy) {
             // probs = probs * action_mask; argmax (first maximum)
@@ -393,22 +505,23 @@ __global__ void __launch_bounds__(256) sample_kernel(SampleArgs a) {
             double u;
             if constexpr (RNG == G2048_RNG_PCG64) {
                 Pcg64 g;
-                const ulonglong2 st = reinterpret_cast<const ulonglong2*>(a.st)[i];
-                const ulonglong2 ic = reinterpret_cast<const ulonglong2*>(a.inc)[i];
-                const uint64_t bf = a.buf[i];
-                g.s_lo = st.x; g.s_hi = st.y; g.i_lo = ic.x; g.i_hi = ic.y;
+                const ulonglong2 sv = ld(reinterpret_cast<const ulonglong2*>(a.rs), i);
+                const ulonglong2 ic = ld(reinterpret_cast<const ulonglong2*>(a.inc), i);
+                const uint64_t bf = ld(a.buf, i);
+                g.s_lo = sv.x; g.s_hi = sv.y; g.i_lo = ic.x; g.i_hi = ic.y;
                 g.has_uint32 = (uint32_t)(bf >> 32); g.uinteger = (uint32_t)bf;
                 u = pcg_random(g);
-                reinterpret_cast<ulonglong2*>(a.st)[i] = make_ulonglong2(g.s_lo, g.s_hi);
+                st(reinterpret_cast<ulonglong2*>(a.rs), i, make_ulonglong2(g.s_lo, g.s_hi));
             } else {
-                const U4 r = philox_ctr(a.key, a.lane_seed ? a.lane_seed[i] : (uint64_t)i, a.counter ? a.counter[i] : 0u, 3u);
+                const U4 r = philox_ctr(a.key, a.lane_seed ? ld(a.lane_seed, i) : (uint64_t)i,
+                                        a.counter ? ld(a.counter, i) : 0u, 3u);
                 const uint64_t x = ((uint64_t)r.x << 32) | r.y;
                 u = (double)(x >> 11) * (1.0 / 9007199254740992.0);
             }
 #pragma unroll
             for (int k = 0; k < 4; k++) act += (cdf[k] / cdf[3] <= u) ? 1u : 0u;
         }
-        a.actions[i] = (uint8_t)act;
+        st(a.actions, i, (uint8_t)act);
     }
 }
 
@@ -416,10 +529,10 @@ __global__ void __launch_bounds__(256) sample_kernel(SampleArgs a) {
 __global__ void __launch_bounds__(256) returns_kernel(const float* __restrict__ r, const int32_t* __restrict__ len,
                                                       double gamma, float* __restrict__ out, int64_t T, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t L = len[i];
-        L = L > T ? T : L;
+        int64_t Li = len[i];
+        Li = Li > T ? T : Li;
         double G = 0.0;
-        for (int64_t t = L - 1; t >= 0; t--) {
+        for (int64_t t = Li - 1; t >= 0; t--) {
             G = (double)r[t * n + i] + gamma * G;
             out[t * n + i] = (float)G;
         }
@@ -439,19 +552,20 @@ __global__ void __launch_bounds__(256) sym_kernel(const uint64_t* __restrict__ b
     }
 }
 
+// ------------------------------------------------------------------------------------- host helpers
 int current_device(int& dev) {
     G2048_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= kMaxDev) return fail(G2048_EINVAL, "device ordinal out of range");
     return G2048_OK;
 }
 
-int lut_for_current(const uint16_t*& lut, int& cus) {
+int tab_for_current(const uint8_t*& tab, int& cus) {
     int dev = 0;
     int rc = current_device(dev);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_lut[dev]) return fail(G2048_ENOINIT, "g2048_init() was not called for device " + std::to_string(dev));
-    lut = g_lut[dev];
+    if (!g_tab[dev]) return fail(G2048_ENOINIT, "g2048_init() was not called for device " + std::to_string(dev));
+    tab = g_tab[dev];
     cus = g_cus[dev];
     return G2048_OK;
 }
@@ -499,24 +613,57 @@ int check_lanes(const g2048_lanes* L, int rng_mode) {
     return G2048_OK;
 }
 
+// offset every per-lane buffer by `off` lanes (for launches split at kMaxLanesPerLaunch)
+g2048_lanes shift_lanes(const g2048_lanes& L, int64_t off) {
+    g2048_lanes r = L;
+    r.board += off;
+    r.step_count += off;
+    r.score += off;
+    r.max_tile += off;
+    r.status += off;
+    r.seed += off;
+    if (r.rng_state) r.rng_state += 2 * off;
+    if (r.rng_inc) r.rng_inc += 2 * off;
+    if (r.rng_buf) r.rng_buf += off;
+    return r;
+}
+
+// boards per lane per sweep.  U = 2 measured equal or slower on MI355X at 1M boards (and 4 spills past the
+// 128-VGPR budget of 4 waves/SIMD), so one board per lane per sweep.
+constexpr int kStepU = 1;
+
+template <int OBS, int RNG, bool LDS, int U>
+void launch_step3(const StepArgs& a, int grid, bool list, hipStream_t s) {
+    if (list) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, true, U>), dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, false, U>), dim3(grid), dim3(kBlock), 0, s, a);
+}
+
+template <int OBS, int RNG, int kU>
+void launch_step_u(const StepArgs& a, int cus, hipStream_t s) {
+    const bool lds = a.n >= (uint32_t)kLutSmallN;
+    // persistent grid: <= one workgroup per CU (LDS), but enough workgroups that sweeps * kU <= 64 (the per-lane
+    // pending-reset bitmask)
+    const int64_t per_block_sweep = (int64_t)kBlock * kU;
+    const int64_t min_blocks = ((int64_t)a.n + per_block_sweep * (64 / kU) - 1) / (per_block_sweep * (64 / kU));
+    int grid = grid_for((a.n + kU - 1) / kU, kBlock, lds ? cus : cus * 2);
+    if (grid < min_blocks) grid = (int)min_blocks;
+    const bool list = a.out.merged != nullptr;
+    if (lds) launch_step3<OBS, RNG, true, kU>(a, grid, list, s);
+    else launch_step3<OBS, RNG, false, kU>(a, grid, list, s);
+}
+
 template <int OBS, int RNG>
-void launch_step(const StepArgs& a, bool lds, int cus, hipStream_t s) {
-    if (lds) {
-        const int grid = grid_for(a.n, kBlock, cus);
-        hipLaunchKernelGGL((step_kernel<OBS, RNG, true>), dim3(grid), dim3(kBlock), 0, s, a);
-    } else {
-        const int grid = grid_for(a.n, kBlock, cus * 2);
-        hipLaunchKernelGGL((step_kernel<OBS, RNG, false>), dim3(grid), dim3(kBlock), 0, s, a);
-    }
+void launch_step(const StepArgs& a, int cus, hipStream_t s) {
+    launch_step_u<OBS, RNG, kStepU>(a, cus, s);
 }
 
 template <int RNG>
-void launch_step_obs(const StepArgs& a, int obs, bool lds, int cus, hipStream_t s) {
+void launch_step_obs(const StepArgs& a, int obs, int cus, hipStream_t s) {
     switch (obs) {
-        case G2048_OBS_RAW: launch_step<G2048_OBS_RAW, RNG>(a, lds, cus, s); break;
-        case G2048_OBS_LOG2: launch_step<G2048_OBS_LOG2, RNG>(a, lds, cus, s); break;
-        case G2048_OBS_ONEHOT: launch_step<G2048_OBS_ONEHOT, RNG>(a, lds, cus, s); break;
-        default: launch_step<G2048_OBS_NONE, RNG>(a, lds, cus, s); break;
+        case G2048_OBS_RAW: launch_step<G2048_OBS_RAW, RNG>(a, cus, s); break;
+        case G2048_OBS_LOG2: launch_step<G2048_OBS_LOG2, RNG>(a, cus, s); break;
+        case G2048_OBS_ONEHOT: launch_step<G2048_OBS_ONEHOT, RNG>(a, cus, s); break;
+        default: launch_step<G2048_OBS_NONE, RNG>(a, cus, s); break;
     }
 }
 
@@ -548,13 +695,20 @@ const char* g2048_last_error(void) { return g_err.c_str(); }
 int g2048_init(int device) {
     if (device < 0 || device >= kMaxDev) return fail(G2048_EINVAL, "device ordinal out of range");
     std::lock_guard<std::mutex> lk(g_mu);
-    if (g_lut[device]) return G2048_OK;
+    if (g_tab[device]) return G2048_OK;
     int prev = 0;
     G2048_HIP(hipGetDevice(&prev));
     G2048_HIP(hipSetDevice(device));
-    static uint16_t host[kLutEntries];
-    for (uint32_t r = 0; r < (uint32_t)kLutEntries; r++) host[r] = (uint16_t)line_move_left(r);
-    uint16_t* d = nullptr;
+    static uint8_t host[kTabBytes];
+    uint16_t* line = reinterpret_cast<uint16_t*>(host);
+    uint8_t* code = host + 2 * kLines;
+    for (uint32_t r = 0; r < (uint32_t)kLines; r++) {
+        line[r] = (uint16_t)line_move_left(r);
+        const uint32_t c = line_merge_code(r);
+        if (r & 1u) code[r >> 1] = (uint8_t)(code[r >> 1] | (c << 4));
+        else code[r >> 1] = (uint8_t)c;
+    }
+    uint8_t* d = nullptr;
     hipError_t e = hipMalloc(&d, sizeof(host));
     if (e == hipSuccess) e = hipMemcpy(d, host, sizeof(host), hipMemcpyHostToDevice);
     const hipError_t e2 = hipSetDevice(prev);
@@ -563,7 +717,7 @@ int g2048_init(int device) {
         return fail(G2048_EHIP, std::string("g2048_init: ") + hipGetErrorString(e));
     }
     if (e2 != hipSuccess) return fail(G2048_EHIP, std::string("g2048_init: ") + hipGetErrorString(e2));
-    g_lut[device] = d;
+    g_tab[device] = d;
     g_cus[device] = device_cus(device);
     return G2048_OK;
 }
@@ -571,10 +725,12 @@ int g2048_init(int device) {
 int g2048_seed_pcg64(const uint64_t* seeds, uint64_t* rng_state, uint64_t* rng_inc, uint64_t* rng_buf, int64_t n,
                      void* stream) {
     if (n < 0) return fail(G2048_EINVAL, "n < 0");
-    if (n == 0) return G2048_OK;
     if (!seeds || !rng_state || !rng_inc || !rng_buf) return fail(G2048_EINVAL, "NULL buffer");
-    hipLaunchKernelGGL(seed_kernel, dim3(grid_for(n, 256, 2048)), dim3(256), 0, (hipStream_t)stream, seeds, rng_state,
-                       rng_inc, rng_buf, n);
+    for (int64_t off = 0; off < n; off += kMaxLanesPerLaunch) {
+        const uint32_t m = (uint32_t)(n - off < kMaxLanesPerLaunch ? n - off : kMaxLanesPerLaunch);
+        hipLaunchKernelGGL(seed_kernel, dim3(grid_for(m, 256, 2048)), dim3(256), 0, (hipStream_t)stream, seeds + off,
+                           rng_state + 2 * off, rng_inc + 2 * off, rng_buf + off, m);
+    }
     G2048_HIP(hipGetLastError());
     return G2048_OK;
 }
@@ -585,13 +741,19 @@ int g2048_reset(const g2048_lanes* lanes, const uint64_t* seeds, const uint8_t* 
     if (!rc) rc = check_lanes(lanes, rng_mode);
     if (rc) return rc;
     if (n < 0) return fail(G2048_EINVAL, "n < 0");
-    if (n == 0) return G2048_OK;
-    const uint16_t* lut = nullptr;
+    const uint8_t* tab = nullptr;
     int cus = 256;
-    if ((rc = lut_for_current(lut, cus))) return rc;
-    ResetArgs a{*lanes, seeds, reset_mask, mask_out, obs_out, cfg->obs_log2_scale, philox_key, n};
-    if (rng_mode == G2048_RNG_PCG64) launch_reset<G2048_RNG_PCG64>(a, obs_out ? cfg->obs_mode : G2048_OBS_NONE, cus, (hipStream_t)stream);
-    else launch_reset<G2048_RNG_PHILOX>(a, obs_out ? cfg->obs_mode : G2048_OBS_NONE, cus, (hipStream_t)stream);
+    if ((rc = tab_for_current(tab, cus))) return rc;
+    const int obs = obs_out ? cfg->obs_mode : G2048_OBS_NONE;
+    const int width = cfg->obs_mode == G2048_OBS_ONEHOT ? 272 : 16;
+    for (int64_t off = 0; off < n; off += kMaxLanesPerLaunch) {
+        const uint32_t m = (uint32_t)(n - off < kMaxLanesPerLaunch ? n - off : kMaxLanesPerLaunch);
+        ResetArgs a{shift_lanes(*lanes, off), seeds ? seeds + off : nullptr, reset_mask ? reset_mask + off : nullptr,
+                    mask_out ? mask_out + 4 * off : nullptr, obs_out ? obs_out + width * off : nullptr,
+                    cfg->obs_log2_scale, philox_key, m};
+        if (rng_mode == G2048_RNG_PCG64) launch_reset<G2048_RNG_PCG64>(a, obs, cus, (hipStream_t)stream);
+        else launch_reset<G2048_RNG_PHILOX>(a, obs, cus, (hipStream_t)stream);
+    }
     G2048_HIP(hipGetLastError());
     return G2048_OK;
 }
@@ -604,26 +766,34 @@ int g2048_step(const g2048_lanes* lanes, const uint8_t* actions, const g2048_env
     if (!actions) return fail(G2048_EINVAL, "actions is NULL");
     if (!out || !out->reward || !out->flags) return fail(G2048_EINVAL, "out.reward / out.flags are required");
     if (n < 0) return fail(G2048_EINVAL, "n < 0");
-    if (n == 0) return G2048_OK;
-    const uint16_t* lut = nullptr;
+    const uint8_t* tab = nullptr;
     int cus = 256;
-    if ((rc = lut_for_current(lut, cus))) return rc;
-    StepArgs a;
-    a.L = *lanes;
-    a.actions = actions;
-    a.out = *out;
-    a.rc = reward_cfg(*cfg);
-    a.obs_scale = cfg->obs_log2_scale;
-    a.auto_reset = auto_reset;
-    a.max_steps = cfg->max_steps;
-    a.stride = reset_stride;
-    a.key = philox_key;
-    a.lut = lut;
-    a.n = n;
+    if ((rc = tab_for_current(tab, cus))) return rc;
     const int obs = out->obs ? cfg->obs_mode : G2048_OBS_NONE;
-    const bool lds = n >= kLutSmallN;
-    if (rng_mode == G2048_RNG_PCG64) launch_step_obs<G2048_RNG_PCG64>(a, obs, lds, cus, (hipStream_t)stream);
-    else launch_step_obs<G2048_RNG_PHILOX>(a, obs, lds, cus, (hipStream_t)stream);
+    const int width = cfg->obs_mode == G2048_OBS_ONEHOT ? 272 : 16;
+    for (int64_t off = 0; off < n; off += kMaxLanesPerLaunch) {
+        const uint32_t m = (uint32_t)(n - off < kMaxLanesPerLaunch ? n - off : kMaxLanesPerLaunch);
+        StepArgs a;
+        a.L = shift_lanes(*lanes, off);
+        a.actions = actions + off;
+        a.out = *out;
+        a.out.reward += off;
+        a.out.flags += off;
+        if (a.out.mask) a.out.mask += 4 * off;
+        if (a.out.obs) a.out.obs += width * off;
+        if (a.out.merged) a.out.merged += off;
+        if (a.out.prev_board) a.out.prev_board += off;
+        a.rc = reward_cfg(*cfg);
+        a.obs_scale = cfg->obs_log2_scale;
+        a.auto_reset = auto_reset;
+        a.max_steps = cfg->max_steps;
+        a.stride = reset_stride;
+        a.key = philox_key;
+        a.tab = tab;
+        a.n = m;
+        if (rng_mode == G2048_RNG_PCG64) launch_step_obs<G2048_RNG_PCG64>(a, obs, cus, (hipStream_t)stream);
+        else launch_step_obs<G2048_RNG_PHILOX>(a, obs, cus, (hipStream_t)stream);
+    }
     G2048_HIP(hipGetLastError());
     return G2048_OK;
 }
@@ -634,14 +804,20 @@ int g2048_obs(const uint64_t* boards, int obs_mode, float obs_log2_scale, float*
     if (!boards) return fail(G2048_EINVAL, "boards is NULL");
     if (obs_mode < G2048_OBS_NONE || obs_mode > G2048_OBS_ONEHOT)
         return fail(G2048_EINVAL, "Unsupported obs_mode: " + std::to_string(obs_mode));
-    if (n == 0) return G2048_OK;
-    const int grid = grid_for(n, 256, 2048);
+    const int width = obs_mode == G2048_OBS_ONEHOT ? 272 : 16;
     hipStream_t s = (hipStream_t)stream;
-    switch (obs ? obs_mode : G2048_OBS_NONE) {
-        case G2048_OBS_RAW: hipLaunchKernelGGL(obs_kernel<G2048_OBS_RAW>, dim3(grid), dim3(256), 0, s, boards, obs, mask, obs_log2_scale, n); break;
-        case G2048_OBS_LOG2: hipLaunchKernelGGL(obs_kernel<G2048_OBS_LOG2>, dim3(grid), dim3(256), 0, s, boards, obs, mask, obs_log2_scale, n); break;
-        case G2048_OBS_ONEHOT: hipLaunchKernelGGL(obs_kernel<G2048_OBS_ONEHOT>, dim3(grid), dim3(256), 0, s, boards, obs, mask, obs_log2_scale, n); break;
-        default: hipLaunchKernelGGL(obs_kernel<G2048_OBS_NONE>, dim3(grid), dim3(256), 0, s, boards, obs, mask, obs_log2_scale, n); break;
+    for (int64_t off = 0; off < n; off += kMaxLanesPerLaunch) {
+        const uint32_t m = (uint32_t)(n - off < kMaxLanesPerLaunch ? n - off : kMaxLanesPerLaunch);
+        const uint64_t* b = boards + off;
+        float* o = obs ? obs + width * off : nullptr;
+        int8_t* mk = mask ? mask + 4 * off : nullptr;
+        const int grid = grid_for(m, 256, 2048);
+        switch (o ? obs_mode : G2048_OBS_NONE) {
+            case G2048_OBS_RAW: hipLaunchKernelGGL(obs_kernel<G2048_OBS_RAW>, dim3(grid), dim3(256), 0, s, b, o, mk, obs_log2_scale, m); break;
+            case G2048_OBS_LOG2: hipLaunchKernelGGL(obs_kernel<G2048_OBS_LOG2>, dim3(grid), dim3(256), 0, s, b, o, mk, obs_log2_scale, m); break;
+            case G2048_OBS_ONEHOT: hipLaunchKernelGGL(obs_kernel<G2048_OBS_ONEHOT>, dim3(grid), dim3(256), 0, s, b, o, mk, obs_log2_scale, m); break;
+            default: hipLaunchKernelGGL(obs_kernel<G2048_OBS_NONE>, dim3(grid), dim3(256), 0, s, b, o, mk, obs_log2_scale, m); break;
+        }
     }
     G2048_HIP(hipGetLastError());
     return G2048_OK;
@@ -651,13 +827,16 @@ int g2048_move(const uint64_t* boards, const uint8_t* actions, uint64_t* out_boa
                int64_t n, void* stream) {
     if (n < 0) return fail(G2048_EINVAL, "n < 0");
     if (!boards || !actions || !out_board) return fail(G2048_EINVAL, "NULL buffer");
-    if (n == 0) return G2048_OK;
-    const uint16_t* lut = nullptr;
+    const uint8_t* tab = nullptr;
     int cus = 256;
-    int rc = lut_for_current(lut, cus);
+    int rc = tab_for_current(tab, cus);
     if (rc) return rc;
-    hipLaunchKernelGGL(move_kernel, dim3(grid_for(n, 256, 2048)), dim3(256), 0, (hipStream_t)stream, boards, actions,
-                       lut, out_board, merged, flags, n);
+    for (int64_t off = 0; off < n; off += kMaxLanesPerLaunch) {
+        const uint32_t m = (uint32_t)(n - off < kMaxLanesPerLaunch ? n - off : kMaxLanesPerLaunch);
+        hipLaunchKernelGGL(move_kernel, dim3(grid_for(m, 256, 2048)), dim3(256), 0, (hipStream_t)stream, boards + off,
+                           actions + off, tab, out_board + off, merged ? merged + off : nullptr,
+                           flags ? flags + off : nullptr, m);
+    }
     G2048_HIP(hipGetLastError());
     return G2048_OK;
 }
@@ -672,11 +851,17 @@ int g2048_sample(const float* logits, const int8_t* mask, const uint8_t* active,
         return fail(G2048_EINVAL, "PCG64 sampling needs rng_state / rng_inc / rng_buf");
     if (rng_mode != G2048_RNG_PCG64 && rng_mode != G2048_RNG_PHILOX)
         return fail(G2048_EINVAL, "Unsupported rng_mode: " + std::to_string(rng_mode));
-    if (n == 0) return G2048_OK;
-    SampleArgs a{logits, mask, active, rng_state, rng_inc, rng_buf, philox_key, lane_seed, counter, probs_out, actions, n, greedy};
-    const int grid = grid_for(n, 256, 2048);
-    if (rng_mode == G2048_RNG_PCG64) hipLaunchKernelGGL(sample_kernel<G2048_RNG_PCG64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL(sample_kernel<G2048_RNG_PHILOX>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    for (int64_t off = 0; off < n; off += kMaxLanesPerLaunch) {
+        const uint32_t m = (uint32_t)(n - off < kMaxLanesPerLaunch ? n - off : kMaxLanesPerLaunch);
+        SampleArgs a{logits + 4 * off, mask ? mask + 4 * off : nullptr, active ? active + off : nullptr,
+                     rng_state ? rng_state + 2 * off : nullptr, rng_inc ? rng_inc + 2 * off : nullptr,
+                     rng_buf ? rng_buf + off : nullptr, philox_key, lane_seed ? lane_seed + off : nullptr,
+                     counter ? counter + off : nullptr, probs_out ? probs_out + 4 * off : nullptr, actions + off, m,
+                     greedy};
+        const int grid = grid_for(m, 256, 2048);
+        if (rng_mode == G2048_RNG_PCG64) hipLaunchKernelGGL(sample_kernel<G2048_RNG_PCG64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+        else hipLaunchKernelGGL(sample_kernel<G2048_RNG_PHILOX>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    }
     G2048_HIP(hipGetLastError());
     return G2048_OK;
 }

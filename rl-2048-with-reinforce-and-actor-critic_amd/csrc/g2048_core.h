@@ -128,6 +128,51 @@ G2048_HD LineMerges line_merges(uint32_t o, uint32_t nw) {
     return m;
 }
 
+// 4-bit merge code of a line (second row table, so the kernel need not re-derive merges arithmetically):
+//   0 no merge; 1..3 one merge, its result at output position code-1; 4 two merges (results at positions 0, 1);
+//   5..7 one merge at position code-5 that saturated (15+15: true exponent 16);
+//   8 two merges, first saturated; 9 two merges, second saturated; 10 two merges, both saturated.
+G2048_HD uint32_t line_merge_code(uint32_t row) {
+    uint32_t c[4];
+    int n = 0;
+    for (int k = 0; k < 4; k++) {
+        uint32_t e = (row >> (4 * k)) & 15u;
+        if (e) c[n++] = e;
+    }
+    int w = 0, i = 0, np = 0;
+    int pos[2] = {0, 0};
+    bool sat[2] = {false, false};
+    while (i < n) {
+        if (i + 1 < n && c[i] == c[i + 1]) {
+            pos[np] = w;
+            sat[np] = c[i] == 15u;
+            np++;
+            i += 2;
+        } else {
+            i += 1;
+        }
+        w++;
+    }
+    if (np == 0) return 0u;
+    if (np == 1) return (uint32_t)(sat[0] ? 5 + pos[0] : 1 + pos[0]);
+    return sat[0] ? (sat[1] ? 10u : 8u) : (sat[1] ? 9u : 4u);
+}
+
+// merged exponents (list order) of a line from its new line and merge code
+G2048_HD void decode_merge_code(uint32_t code, uint32_t nw, uint32_t& e0, uint32_t& e1) {
+    if (code <= 4u) {
+        const uint32_t p = code == 4u ? 0u : code - 1u;
+        e0 = code ? (nw >> (4u * p)) & 15u : 0u;
+        e1 = code == 4u ? (nw >> 4) & 15u : 0u;
+    } else if (code <= 7u) {
+        e0 = 16u;
+        e1 = 0u;
+    } else {
+        e0 = code == 9u ? (nw & 15u) : 16u;
+        e1 = code == 8u ? ((nw >> 4) & 15u) : 16u;
+    }
+}
+
 // Accumulated merge summary of one move (what _compute_reward and Game2048.score consume).
 struct MoveSummary {
     uint32_t count;   // len(merged)
@@ -175,6 +220,79 @@ G2048_HD uint64_t board_move(uint64_t b, uint32_t a, const Lut& lut, MoveSummary
     g = rev ? reverse_rows(g) : g;
     g = vert ? transpose(g) : g;
     return g;
+}
+
+// Board move with the two row tables (`lut(o)` -> new line, `code(o)` -> line_merge_code).  Same result and
+// merged-list order as board_move; the merge summary is accumulated branch-free, the list only if wanted.
+template <bool WANT_LIST, class Lut, class Code>
+G2048_HD uint64_t board_move_coded(uint64_t b, uint32_t a, const Lut& lut, const Code& code, MoveSummary& s) {
+    const bool vert = (a == 0u) | (a == 2u);
+    const bool rev = (a == 1u) | (a == 2u);
+    const bool back = (a == 0u) | (a == 1u);
+    uint64_t f = vert ? transpose(b) : b;
+    f = rev ? reverse_rows(f) : f;
+    uint64_t g = 0;
+    uint32_t count = 0, sum_e = 0, score = 0, max_e = 0, ovf = 0, list = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int line = back ? 3 - j : j;
+        const uint32_t o = (uint32_t)(f >> (16 * line)) & 0xFFFFu;
+        const uint32_t nw = (uint32_t)lut(o);
+        const uint32_t c = (uint32_t)code(o);
+        g |= (uint64_t)nw << (16 * line);
+        uint32_t e0, e1;
+        if (c <= 4u) {
+            const uint32_t p = c == 4u ? 0u : c - 1u;
+            e0 = c ? (nw >> (4u * p)) & 15u : 0u;
+            e1 = c == 4u ? (nw >> 4) & 15u : 0u;
+        } else {
+            decode_merge_code(c, nw, e0, e1);
+        }
+        const uint32_t n0 = e0 != 0u, n1 = e1 != 0u;
+        score += (n0 ? 1u << e0 : 0u) + (n1 ? 1u << e1 : 0u);
+        sum_e += e0 + e1;
+        max_e = max_e > e0 ? max_e : e0;
+        max_e = max_e > e1 ? max_e : e1;
+        ovf |= (e0 | e1) >> 4;
+        if (WANT_LIST) {
+            if (n0) list |= ((e0 - 1u) & 15u) << (4u * (count & 7u));
+            if (n1) list |= ((e1 - 1u) & 15u) << (4u * ((count + n0) & 7u));
+        }
+        count += n0 + n1;
+    }
+    s.count = count;
+    s.sum_e = sum_e;
+    s.score = score;
+    s.max_e = max_e;
+    s.overflow = ovf;
+    s.list = list;
+    g = rev ? reverse_rows(g) : g;
+    g = vert ? transpose(g) : g;
+    return g;
+}
+
+// nz / equal-neighbour masks of a board, shared by is_done and action_mask
+struct BoardBits {
+    uint64_t nz, z, eqh, eqv;
+};
+
+G2048_HD BoardBits board_bits(uint64_t b) {
+    BoardBits r;
+    r.nz = nz_bits(b);
+    r.z = ~r.nz & kNibLsb;
+    r.eqh = ~nz_bits(b ^ (b >> 4)) & r.nz & kHMask;
+    r.eqv = ~nz_bits(b ^ (b >> 16)) & r.nz & kVMask;
+    return r;
+}
+
+G2048_HD bool bits_done(const BoardBits& r) { return r.z == 0 && (r.eqh | r.eqv) == 0; }
+
+G2048_HD uint32_t bits_mask(const BoardBits& r) {
+    uint32_t up = ((r.z & (r.nz >> 16) & kVMask) | r.eqv) != 0;
+    uint32_t down = ((r.nz & (r.z >> 16) & kVMask) | r.eqv) != 0;
+    uint32_t left = ((r.z & (r.nz >> 4) & kHMask) | r.eqh) != 0;
+    uint32_t right = ((r.nz & (r.z >> 4) & kHMask) | r.eqh) != 0;
+    return up | (right << 1) | (down << 2) | (left << 3);
 }
 
 // index (0-based) of the k-th empty cell in row-major order (np.argwhere(board == 0)[k], src/game2048.py:109)

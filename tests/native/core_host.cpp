@@ -7,15 +7,23 @@
 using namespace g2048;
 
 static uint16_t g_lut[65536];
+static uint8_t g_code[32768];
 static int g_lut_ready = 0;
 
 struct HostLut {
     uint32_t operator()(uint32_t i) const { return g_lut[i]; }
 };
+struct HostCode {
+    uint32_t operator()(uint32_t o) const { return (g_code[o >> 1] >> ((o & 1u) << 2)) & 15u; }
+};
 
 static void ensure_lut() {
     if (g_lut_ready) return;
-    for (uint32_t r = 0; r < 65536u; r++) g_lut[r] = (uint16_t)line_move_left(r);
+    for (uint32_t r = 0; r < 65536u; r++) {
+        g_lut[r] = (uint16_t)line_move_left(r);
+        const uint32_t c = line_merge_code(r);
+        g_code[r >> 1] = (r & 1u) ? (uint8_t)(g_code[r >> 1] | (c << 4)) : (uint8_t)c;
+    }
     g_lut_ready = 1;
 }
 
@@ -28,6 +36,16 @@ uint64_t ch_board_move(uint64_t b, uint32_t a, uint32_t* list, uint32_t* count, 
     *list = s.list; *count = s.count; *score = s.score; *sum_e = s.sum_e; *max_e = s.max_e; *overflow = s.overflow;
     return m;
 }
+uint64_t ch_board_move_coded(uint64_t b, uint32_t a, uint32_t* list, uint32_t* count, uint32_t* score,
+                             uint32_t* sum_e, uint32_t* max_e, uint32_t* overflow) {
+    ensure_lut();
+    MoveSummary s;
+    uint64_t m = board_move_coded<true>(b, a, HostLut{}, HostCode{}, s);
+    *list = s.list; *count = s.count; *score = s.score; *sum_e = s.sum_e; *max_e = s.max_e; *overflow = s.overflow;
+    return m;
+}
+uint32_t ch_bits_mask(uint64_t b) { return bits_mask(board_bits(b)); }
+int ch_bits_done(uint64_t b) { return bits_done(board_bits(b)) ? 1 : 0; }
 uint32_t ch_action_mask(uint64_t b) { return action_mask(b); }
 int ch_is_done(uint64_t b) { return is_done(b) ? 1 : 0; }
 uint64_t ch_transpose(uint64_t b) { return transpose(b); }

@@ -28,6 +28,11 @@ def ch():
     u32p = ctypes.POINTER(ctypes.c_uint32)
     L.ch_board_move.restype = ctypes.c_uint64
     L.ch_board_move.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [u32p] * 6
+    L.ch_board_move_coded.restype = ctypes.c_uint64
+    L.ch_board_move_coded.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [u32p] * 6
+    L.ch_bits_mask.restype = ctypes.c_uint32
+    L.ch_bits_mask.argtypes = [ctypes.c_uint64]
+    L.ch_bits_done.argtypes = [ctypes.c_uint64]
     L.ch_action_mask.restype = ctypes.c_uint32
     L.ch_action_mask.argtypes = [ctypes.c_uint64]
     L.ch_is_done.argtypes = [ctypes.c_uint64]
@@ -47,9 +52,10 @@ def ch():
     return L
 
 
-def _move(ch, b, a):
+def _move(ch, b, a, coded=False):
     vals = [ctypes.c_uint32() for _ in range(6)]
-    m = ch.ch_board_move(b, a, *[ctypes.byref(v) for v in vals])
+    fn = ch.ch_board_move_coded if coded else ch.ch_board_move
+    m = fn(b, a, *[ctypes.byref(v) for v in vals])
     lst, cnt, score, sum_e, max_e, ovf = [v.value for v in vals]
     merged = [((lst >> (4 * k)) & 15) + 1 for k in range(cnt)]
     return m, merged, score, sum_e, max_e, ovf
@@ -61,12 +67,15 @@ def _rand_boards(rng, n, p_empty=0.375, hi=15):
     return [O.pack_exponents(x) for x in e]
 
 
-def test_board_move_vs_oracle(ch):
+@pytest.mark.parametrize("coded", [False, True])
+def test_board_move_vs_oracle(ch, coded):
     rng = np.random.default_rng(3)
     boards = _rand_boards(rng, 3000) + _rand_boards(rng, 2000, p_empty=0.0, hi=4) + _rand_boards(rng, 1000, 0.7)
+    boards += _rand_boards(rng, 1500, p_empty=0.2, hi=15) + [O.pack_exponents([15] * 16), O.pack_exponents([15, 15, 14, 14] * 4),
+                                                             O.pack_exponents([14, 14, 15, 15] * 4)]
     for b in boards:
         for a in range(4):
-            m, merged, score, sum_e, max_e, ovf = _move(ch, b, a)
+            m, merged, score, sum_e, max_e, ovf = _move(ch, b, a, coded)
             ob, omerged, ochanged, ok = O.move_packed(b, a)
             oe = [int(v).bit_length() - 1 for v in omerged]
             assert merged == oe, (hex(b), a)
@@ -85,7 +94,9 @@ def test_mask_done_vs_oracle(ch):
         g.board = np.where(O.unpack_exponents(b) > 0, np.left_shift(1, O.unpack_exponents(b)), 0)
         m = g.mask()
         assert ch.ch_action_mask(b) == sum(int(x) << i for i, x in enumerate(m)), hex(b)
+        assert ch.ch_bits_mask(b) == ch.ch_action_mask(b)
         assert bool(ch.ch_is_done(b)) == bool(O.lib().or_game_is_done(ctypes.byref(g.g)))
+        assert ch.ch_bits_done(b) == ch.ch_is_done(b)
 
 
 def test_transpose_and_symmetries(ch):
