@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"])
     ap.add_argument("--no-policy", action="store_true")
+    ap.add_argument("--no-auto-reset", action="store_true", help="diagnostic: finished lanes go inactive")
+    ap.add_argument("--trace-steps", type=int, default=0,
+                    help="diagnostic: print per-launch kernel us and reset fraction for the first N steps, then exit")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -88,7 +91,7 @@ def make_env(torch, args, B, lane_offset, device):
 
     cfg = Game2048EnvConfig(obs_mode="log2" if args.obs == "none" else args.obs, obs_log2_scale=0.0625,
                             reward_mode="log2", base_reward_scale=0.5, max_steps=1024)
-    env = VecGame2048Env(B, cfg, device=device, rng=args.rng, auto_reset=True,
+    env = VecGame2048Env(B, cfg, device=device, rng=args.rng, auto_reset=not args.no_auto_reset,
                          reset_stride=B * max(args.gpus, 1), lane_offset=lane_offset)
     if args.obs == "none":
         env._out.obs = None
@@ -235,6 +238,20 @@ def main():
     g = torch.Generator(device=device)
     g.manual_seed(1 + rank)
     actions = torch.randint(0, 4, (K + W, B), dtype=torch.uint8, device=device, generator=g)
+    if args.trace_steps:
+        from rl2048_amd import _lib as L
+
+        for k in range(args.trace_steps):
+            s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_.record()
+            env.step_into(actions[k % (K + W)])
+            e_.record()
+            torch.cuda.synchronize()
+            rf = float(((env.flags & L.F_RESET) != 0).float().mean())
+            act = float(((env.status & L.S_ACTIVE) != 0).float().mean())
+            print(json.dumps({"step": k, "us": round(s_.elapsed_time(e_) * 1e3, 2), "reset_frac": round(rf, 5),
+                              "active_frac": round(act, 4)}), flush=True)
+        return
     for k in range(W):
         env.step_into(actions[k])
     torch.cuda.synchronize()

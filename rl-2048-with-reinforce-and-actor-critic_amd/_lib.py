@@ -15,7 +15,11 @@ import torch
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_ROOT = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "libg2048.so")
+SHIPPED_LIB = os.path.join(PKG_DIR, "libg2048.so")
+LIB_PATH = SHIPPED_LIB
+# tools/diag_build.sh only: load the -DG2048_DIAG=1 timing-attribution build instead of the shipped library
+if os.environ.get("G2048_DIAG_LIB"):
+    LIB_PATH = os.environ["G2048_DIAG_LIB"]
 SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
 INCLUDE = os.path.join(REPO_ROOT, "include")
 ABI_VERSION = 1
@@ -31,14 +35,15 @@ G2048_OK, G2048_EINVAL, G2048_EHIP, G2048_ENOINIT = 0, 1, 2, 3
 
 def build(verbose: bool = False) -> str:
     """Compile libg2048.so for gfx950 in-tree (hipcc cross-compiles; no GPU needed)."""
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-I" + INCLUDE,
-           "-I" + os.path.dirname(SRC), "-o", LIB_PATH, SRC]
+    # -ffp-contract=off: the fp64 reward keeps the reference's separately rounded multiply and add (no FMA)
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", "-I" + INCLUDE,
+           "-I" + os.path.dirname(SRC), "-o", SHIPPED_LIB, SRC]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
     if verbose:
         print(" ".join(cmd))
-    return LIB_PATH
+    return SHIPPED_LIB
 
 
 class EnvCfg(ctypes.Structure):

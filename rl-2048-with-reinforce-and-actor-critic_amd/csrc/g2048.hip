@@ -45,6 +45,14 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess) return fail(G2048_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// G2048_DIAG=1 (tools/diag_build.sh only; never the shipped library): G2048_DIAG_FLAGS in the environment
+// removes pieces of the step kernel for timing attribution: 1 no LDS table fill, 2 no deferred resets,
+// 4 no game compute (the board is xor'ed with the action, everything else stored as if computed),
+// 8 one sweep per wave per launch-equivalent grid (grid = ceil(n / 1024)), 16 no obs writes.
+#ifndef G2048_DIAG
+#define G2048_DIAG 0
+#endif
+
 constexpr int kBlock = 1024;                  // 16 waves per CU; one workgroup per CU (160 KiB of LDS tables)
 constexpr int kLines = 65536;
 constexpr int kTabBytes = kLines * 2 + kLines / 2;   // 163,840 B = the whole LDS of a gfx950 CU
@@ -216,13 +224,14 @@ struct StepArgs {
     uint64_t stride, key;
     const uint8_t* tab;
     uint32_t n;
+    int diag;
 };
 
-// Auto-reset of one lane (deferred to the end of the wave's loop): Game2048Env.reset with seed += stride.
+// Auto-reset of lane i (deferred to the end of the loop): Game2048Env.reset with seed = prev_seed + stride.
 template <int OBS, int RNG>
-__device__ inline void reset_lane(const StepArgs& a, uint32_t i) {
+__device__ inline void reset_lane(const StepArgs& a, uint32_t i, uint64_t prev_seed) {
     const g2048_lanes& L = a.L;
-    const uint64_t seed = ld(L.seed, i) + a.stride;
+    const uint64_t seed = prev_seed + a.stride;
     Pcg64 g;
     const uint64_t b = fresh_board<RNG>(seed, a.key, g);
     st(L.seed, i, seed);
@@ -277,9 +286,15 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
 
     // Game2048.step (src/game2048.py:40-70): move, score, spawn only if changed, done of the final board
     MoveSummary s;
-    uint64_t m = board_move_coded<LIST>(b, x.act, lut, code, s);
+    uint64_t m;
+    if (G2048_DIAG && (a.diag & 4)) {
+        s = MoveSummary{0, 0, 0, 0, 0, 0};
+        m = b ^ ((uint64_t)x.act << 60);
+    } else {
+        m = board_move_coded<LIST>(b, x.act, lut, code, s);
+    }
     const bool changed = m != b;
-    if (changed) {
+    if (changed && !(G2048_DIAG && (a.diag & 4))) {
         if constexpr (RNG == G2048_RNG_PCG64) m = spawn_pcg(m, x.g);
         else m = spawn_philox(m, philox_ctr(a.key, x.seed, sc, 0u));
     }
@@ -310,60 +325,132 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     return m;
 }
 
-// Persistent over the board array in sweeps of U*64 boards per wave: a lane loads its U boards (lane,
-// lane+64, ...) before computing any, so each wave keeps U boards of HBM traffic in flight; the first sweep's
-// loads are issued before the LDS table fill so they overlap it.  LDS: stage the two row tables in LDS, else
-// read them through L1/L2 (small batches).  Sweeps * U <= 64 (launcher): the `pending` reset bitmask.
+// One sweep of one wave: the step of board w0 + lane (inputs already in registers), its mask, the wave's obs.
+// A lane's first pending reset has its seed read here (`pseed`), so the read is long complete at the tail.
+template <int OBS, int RNG, bool LIST>
+__device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, LaneIn& x, const LineFn& lut,
+                                      const CodeFn& code, uint64_t& pending, uint64_t& pseed, uint32_t k) {
+    const uint32_t i = w0 + lane;
+    bool wobs = false, reset = false;
+    uint32_t mbits = 0;
+    uint64_t b = 0;
+    if (i < a.n) b = step_lane<RNG, LIST>(a, i, x, lut, code, wobs, reset, mbits);
+    if (reset) {
+        if (!pending) {
+            if constexpr (RNG == G2048_RNG_PCG64) pseed = ld(a.L.seed, i);
+            else pseed = x.seed;
+        }
+        pending |= 1ull << k;
+    }
+    if (wobs && a.out.mask) st(reinterpret_cast<uint32_t*>(a.out.mask), i, mask_word(mbits));
+    if constexpr (OBS != G2048_OBS_NONE) {
+        const uint64_t wm = __ballot(wobs);
+        if (G2048_DIAG && (a.diag & 16)) return;
+        if (a.out.obs && wm) write_obs_wave<OBS>(a.out.obs, w0, b, wm, lane, a.obs_scale);
+    }
+}
+
+// LDS reuse after the last sweep: the block's reset list (counter, lane indices, previous seeds)
+constexpr int kResetCap = (kTabBytes - 16) / 12;
+static_assert(16 + kResetCap * 4 + kResetCap * 8 <= kTabBytes, "reset list fits the table area");
+static_assert(kTabVec % kBlock == 0, "table fill: whole chunks per thread");
+
+// Persistent over the board array, one board per lane per sweep, software-pipelined with two register buffers
+// A / B (no back-edge copy, which would force a wait on in-flight loads): the loads of sweep s+1 are in flight
+// while sweep s computes.  The first loads are issued before the LDS table fill so they overlap it; each
+// workgroup fills its 10 chunks starting at a different one (blockIdx % 10), so the CUs sharing an L2 do not all
+// read the same lines at once.
+// LDS: stage the two row tables in LDS, else read them through L1/L2 (small batches).  Sweeps per wave <= 64
+// (launcher): the `pending` reset bitmask.
+// Auto-resets are deferred to the end.  With the LDS tables dead after the last sweep, the block compacts its
+// pending resets into an LDS list and runs them densely (thread t takes entries t, t + 1024, ...): ~30 resets of a
+// 1M-board step per CU cost one pass of one wave instead of one divergent pass in most of the 16 waves.
 template <int OBS, int RNG, bool LDS, bool LIST, int U>
 __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
+    static_assert(U == 1, "one board per lane per sweep");
     __shared__ uint4 tab_lds[LDS ? kTabVec : 1];
     const int lane = threadIdx.x & 63;
-    const uint32_t w_first = ((blockIdx.x * kBlock + threadIdx.x) & ~63u) * U;
-    const uint32_t wstride = gridDim.x * kBlock * U;
-    LaneIn in[U];
+    const uint32_t w_first = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
+    const uint32_t wstride = gridDim.x * kBlock;
+    LaneIn A, B;
     uint32_t w0 = w_first;
-#pragma unroll
-    for (int u = 0; u < U; u++)
-        if (w0 + 64u * u + lane < a.n) load_lane<RNG>(a, w0 + 64u * u + lane, in[u]);
+    if (w0 + lane < a.n) load_lane<RNG>(a, w0 + lane, A);
     const uint8_t* tab = a.tab;
     if constexpr (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(a.tab);
+        if (!(G2048_DIAG && (a.diag & 1))) {
+            constexpr uint32_t kChunks = kTabVec / kBlock;
+            const uint32_t rot = blockIdx.x % kChunks;
 #pragma unroll
-        for (int k = threadIdx.x; k < kTabVec; k += kBlock) tab_lds[k] = src[k];
+            for (uint32_t j = 0; j < kChunks; j++) {
+                uint32_t c = j + rot;
+                c -= c >= kChunks ? kChunks : 0u;
+                const uint32_t k = c * kBlock + threadIdx.x;
+                tab_lds[k] = src[k];
+            }
+        }
         __syncthreads();
         tab = reinterpret_cast<const uint8_t*>(tab_lds);
     }
     const LineFn lut{reinterpret_cast<const uint16_t*>(tab)};
     const CodeFn code{tab + 2 * kLines};
-    uint64_t pending = 0;
+    uint64_t pending = 0, pseed = 0;
     uint32_t k = 0;
-    for (; w0 < a.n; w0 += wstride, k += U) {
-        if (k) {
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                if (w0 + 64u * u + lane < a.n) load_lane<RNG>(a, w0 + 64u * u + lane, in[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t base = w0 + 64u * u;
-            if (base >= a.n) break;   // wave-uniform
-            const uint32_t i = base + lane;
-            bool wobs = false, reset = false;
-            uint32_t mbits = 0;
-            uint64_t b = 0;
-            if (i < a.n) b = step_lane<RNG, LIST>(a, i, in[u], lut, code, wobs, reset, mbits);
-            if (reset) pending |= 1ull << (k + u);
-            if (wobs && a.out.mask) st(reinterpret_cast<uint32_t*>(a.out.mask), i, mask_word(mbits));
-            if constexpr (OBS != G2048_OBS_NONE) {
-                const uint64_t wm = __ballot(wobs);
-                if (a.out.obs && wm) write_obs_wave<OBS>(a.out.obs, base, b, wm, lane, a.obs_scale);
-            }
-        }
+    while (w0 < a.n) {                         // wave-uniform
+        const uint32_t w1 = w0 + wstride;
+        if (w1 + lane < a.n) load_lane<RNG>(a, w1 + lane, B);
+        sweep<OBS, RNG, LIST>(a, w0, lane, A, lut, code, pending, pseed, k);
+        if (w1 >= a.n) break;
+        const uint32_t w2 = w1 + wstride;
+        if (w2 + lane < a.n) load_lane<RNG>(a, w2 + lane, A);
+        sweep<OBS, RNG, LIST>(a, w1, lane, B, lut, code, pending, pseed, k + 1);
+        w0 = w2;
+        k += 2;
     }
-    while (pending) {   // deferred auto-resets of this lane, one pass per pending board
-        const uint32_t kk = (uint32_t)__builtin_ctzll(pending);
-        pending &= pending - 1ull;
-        reset_lane<OBS, RNG>(a, w_first + (kk / U) * wstride + 64u * (kk % U) + lane);
+    if (G2048_DIAG && (a.diag & 2)) pending = 0;
+    if constexpr (LDS) {
+        uint32_t* cnt = reinterpret_cast<uint32_t*>(tab_lds);
+        uint32_t* ridx = cnt + 4;
+        uint64_t* rseed = reinterpret_cast<uint64_t*>(ridx + kResetCap + (kResetCap & 1));
+        __syncthreads();                       // every wave is past its last table read
+        if (threadIdx.x == 0) *cnt = 0u;
+        __syncthreads();
+        bool first = true;
+        while (__ballot(pending != 0ull)) {    // wave-uniform; one round per pending board of the busiest lane
+            const bool has = pending != 0ull;
+            const uint32_t kk = has ? (uint32_t)__builtin_ctzll(pending) : 0u;
+            const uint32_t i = w_first + kk * wstride + lane;
+            const uint64_t sd = first ? pseed : (has ? ld(a.L.seed, i) : 0ull);
+            const uint64_t bal = __ballot(has);
+            const int leader = __builtin_ctzll(bal);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(bal));
+            base = (uint32_t)__shfl((int)base, leader, 64);
+            const uint32_t slot =
+                base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            if (has) {
+                if (slot < (uint32_t)kResetCap) {
+                    ridx[slot] = i;
+                    rseed[slot] = sd;
+                } else {
+                    reset_lane<OBS, RNG>(a, i, sd);   // list full (mass reset): the lane does its own
+                }
+                pending &= pending - 1ull;
+            }
+            first = false;
+        }
+        __syncthreads();
+        const uint32_t R = *cnt < (uint32_t)kResetCap ? *cnt : (uint32_t)kResetCap;
+        for (uint32_t r = threadIdx.x; r < R; r += kBlock) reset_lane<OBS, RNG>(a, ridx[r], rseed[r]);
+    } else {
+        bool first = true;
+        while (pending) {   // deferred auto-resets of this lane, one pass per pending board
+            const uint32_t kk = (uint32_t)__builtin_ctzll(pending);
+            pending &= pending - 1ull;
+            const uint32_t i = w_first + kk * wstride + lane;
+            reset_lane<OBS, RNG>(a, i, first ? pseed : ld(a.L.seed, i));
+            first = false;
+        }
     }
 }
 
@@ -647,6 +734,7 @@ void launch_step_u(const StepArgs& a, int cus, hipStream_t s) {
     const int64_t min_blocks = ((int64_t)a.n + per_block_sweep * (64 / kU) - 1) / (per_block_sweep * (64 / kU));
     int grid = grid_for((a.n + kU - 1) / kU, kBlock, lds ? cus : cus * 2);
     if (grid < min_blocks) grid = (int)min_blocks;
+    if (G2048_DIAG && (a.diag & 8)) grid = grid_for(a.n, kBlock, 1 << 30);
     const bool list = a.out.merged != nullptr;
     if (lds) launch_step3<OBS, RNG, true, kU>(a, grid, list, s);
     else launch_step3<OBS, RNG, false, kU>(a, grid, list, s);
@@ -791,6 +879,11 @@ int g2048_step(const g2048_lanes* lanes, const uint8_t* actions, const g2048_env
         a.key = philox_key;
         a.tab = tab;
         a.n = m;
+        a.diag = 0;
+        if (G2048_DIAG) {
+            static const int diag_flags = std::getenv("G2048_DIAG_FLAGS") ? std::atoi(std::getenv("G2048_DIAG_FLAGS")) : 0;
+            a.diag = diag_flags;
+        }
         if (rng_mode == G2048_RNG_PCG64) launch_step_obs<G2048_RNG_PCG64>(a, obs, cus, (hipStream_t)stream);
         else launch_step_obs<G2048_RNG_PHILOX>(a, obs, cus, (hipStream_t)stream);
     }

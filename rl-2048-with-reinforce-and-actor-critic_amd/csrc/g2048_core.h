@@ -158,21 +158,6 @@ G2048_HD uint32_t line_merge_code(uint32_t row) {
     return sat[0] ? (sat[1] ? 10u : 8u) : (sat[1] ? 9u : 4u);
 }
 
-// merged exponents (list order) of a line from its new line and merge code
-G2048_HD void decode_merge_code(uint32_t code, uint32_t nw, uint32_t& e0, uint32_t& e1) {
-    if (code <= 4u) {
-        const uint32_t p = code == 4u ? 0u : code - 1u;
-        e0 = code ? (nw >> (4u * p)) & 15u : 0u;
-        e1 = code == 4u ? (nw >> 4) & 15u : 0u;
-    } else if (code <= 7u) {
-        e0 = 16u;
-        e1 = 0u;
-    } else {
-        e0 = code == 9u ? (nw & 15u) : 16u;
-        e1 = code == 8u ? ((nw >> 4) & 15u) : 16u;
-    }
-}
-
 // Accumulated merge summary of one move (what _compute_reward and Game2048.score consume).
 struct MoveSummary {
     uint32_t count;   // len(merged)
@@ -222,52 +207,97 @@ G2048_HD uint64_t board_move(uint64_t b, uint32_t a, const Lut& lut, MoveSummary
     return g;
 }
 
+// Branch-free decode of line_merge_code: three constants with two bits per code c (at bit 2c).
+//   kDecA: slot-0 kind (0 none, 1 result in the new line at cell kDecP, 2 saturated = exponent 16)
+//   kDecB: slot-1 kind (0 none, 1 result at cell 1, 2 saturated)
+constexpr uint32_t dec_pack(const uint32_t (&v)[11]) {
+    uint32_t r = 0;
+    for (int c = 0; c < 11; c++) r |= v[c] << (2 * c);
+    return r;
+}
+constexpr uint32_t kDecAv[11] = {0, 1, 1, 1, 1, 2, 2, 2, 2, 1, 2};
+constexpr uint32_t kDecPv[11] = {0, 0, 1, 2, 0, 0, 0, 0, 0, 0, 0};
+constexpr uint32_t kDecBv[11] = {0, 0, 0, 0, 1, 0, 0, 0, 1, 2, 2};
+constexpr uint32_t kDecA = dec_pack(kDecAv), kDecP = dec_pack(kDecPv), kDecB = dec_pack(kDecBv);
+
+G2048_HD uint32_t bfe32(uint32_t x, uint32_t off, uint32_t w) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_ubfe(x, off, w);
+#else
+    return (x >> off) & ((1u << w) - 1u);
+#endif
+}
+
+// merged exponents of one line (list order; 16 = saturated 15+15) from its new line and merge code
+G2048_HD void decode_merge_code(uint32_t code, uint32_t nw, uint32_t& e0, uint32_t& e1) {
+    const uint32_t sh = 2u * code;
+    const uint32_t ka = bfe32(kDecA, sh, 2), kb = bfe32(kDecB, sh, 2), p = bfe32(kDecP, sh, 2);
+    e0 = (ka == 1u ? bfe32(nw, 4u * p, 4) : 0u) | ((ka & 2u) << 3);
+    e1 = (kb == 1u ? bfe32(nw, 4u, 4) : 0u) | ((kb & 2u) << 3);
+}
+
 // Board move with the two row tables (`lut(o)` -> new line, `code(o)` -> line_merge_code).  Same result and
-// merged-list order as board_move; the merge summary is accumulated branch-free, the list only if wanted.
+// merged-list order as board_move.  Straight-line code (no per-lane branches, so a wave whose lanes hold all
+// four actions runs it once): the frame transforms are computed and mask-selected, all eight table reads
+// are issued before any is used, the merge summary is accumulated arithmetically (the list only if wanted).
 template <bool WANT_LIST, class Lut, class Code>
 G2048_HD uint64_t board_move_coded(uint64_t b, uint32_t a, const Lut& lut, const Code& code, MoveSummary& s) {
-    const bool vert = (a == 0u) | (a == 2u);
-    const bool rev = (a == 1u) | (a == 2u);
+    const uint64_t mvert = 0ull - (uint64_t)((a == 0u) | (a == 2u));
+    const uint64_t mrev = 0ull - (uint64_t)((a == 1u) | (a == 2u));
     const bool back = (a == 0u) | (a == 1u);
-    uint64_t f = vert ? transpose(b) : b;
-    f = rev ? reverse_rows(f) : f;
-    uint64_t g = 0;
-    uint32_t count = 0, sum_e = 0, score = 0, max_e = 0, ovf = 0, list = 0;
+    uint64_t f = b ^ ((b ^ transpose(b)) & mvert);
+    f ^= (f ^ reverse_rows(f)) & mrev;
+    uint32_t o[4], nw[4], c[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) o[j] = (uint32_t)(f >> (16 * j)) & 0xFFFFu;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const int line = back ? 3 - j : j;
-        const uint32_t o = (uint32_t)(f >> (16 * line)) & 0xFFFFu;
-        const uint32_t nw = (uint32_t)lut(o);
-        const uint32_t c = (uint32_t)code(o);
-        g |= (uint64_t)nw << (16 * line);
+        nw[j] = (uint32_t)lut(o[j]);
+        c[j] = (uint32_t)code(o[j]);
+    }
+    uint64_t g = 0;
+    uint32_t sum_e = 0, score = 0, max_e = 0, count = 0, list = 0;
+#pragma unroll
+    for (int jj = 0; jj < 4; jj++) {
+        const int j = jj;
+        g |= (uint64_t)nw[j] << (16 * j);
         uint32_t e0, e1;
-        if (c <= 4u) {
-            const uint32_t p = c == 4u ? 0u : c - 1u;
-            e0 = c ? (nw >> (4u * p)) & 15u : 0u;
-            e1 = c == 4u ? (nw >> 4) & 15u : 0u;
-        } else {
-            decode_merge_code(c, nw, e0, e1);
-        }
-        const uint32_t n0 = e0 != 0u, n1 = e1 != 0u;
-        score += (n0 ? 1u << e0 : 0u) + (n1 ? 1u << e1 : 0u);
+        decode_merge_code(c[j], nw[j], e0, e1);
+        score += ((1u << e0) & ~1u) + ((1u << e1) & ~1u);
         sum_e += e0 + e1;
         max_e = max_e > e0 ? max_e : e0;
         max_e = max_e > e1 ? max_e : e1;
-        ovf |= (e0 | e1) >> 4;
-        if (WANT_LIST) {
+    }
+    if (WANT_LIST) {
+        // list order: lines 0..3 of the frame, or 3..0 for left/up (the reference's rotated-frame row order)
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            const int j0 = jj, j1 = 3 - jj;
+            const uint32_t cc = back ? c[j1] : c[j0];
+            const uint32_t nn = back ? nw[j1] : nw[j0];
+            uint32_t e0, e1;
+            decode_merge_code(cc, nn, e0, e1);
+            const uint32_t n0 = e0 != 0u, n1 = e1 != 0u;
             if (n0) list |= ((e0 - 1u) & 15u) << (4u * (count & 7u));
             if (n1) list |= ((e1 - 1u) & 15u) << (4u * ((count + n0) & 7u));
+            count += n0 + n1;
         }
-        count += n0 + n1;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            uint32_t e0, e1;
+            decode_merge_code(c[j], nw[j], e0, e1);
+            count += (e0 != 0u) + (e1 != 0u);
+        }
     }
     s.count = count;
     s.sum_e = sum_e;
     s.score = score;
     s.max_e = max_e;
-    s.overflow = ovf;
+    s.overflow = max_e >> 4;
     s.list = list;
-    g = rev ? reverse_rows(g) : g;
-    g = vert ? transpose(g) : g;
+    g ^= (g ^ reverse_rows(g)) & mrev;
+    g ^= (g ^ transpose(g)) & mvert;
     return g;
 }
 

@@ -44,6 +44,14 @@ uint64_t ch_board_move_coded(uint64_t b, uint32_t a, uint32_t* list, uint32_t* c
     *list = s.list; *count = s.count; *score = s.score; *sum_e = s.sum_e; *max_e = s.max_e; *overflow = s.overflow;
     return m;
 }
+uint64_t ch_board_move_coded_nolist(uint64_t b, uint32_t a, uint32_t* list, uint32_t* count, uint32_t* score,
+                                    uint32_t* sum_e, uint32_t* max_e, uint32_t* overflow) {
+    ensure_lut();
+    MoveSummary s;
+    uint64_t m = board_move_coded<false>(b, a, HostLut{}, HostCode{}, s);
+    *list = s.list; *count = s.count; *score = s.score; *sum_e = s.sum_e; *max_e = s.max_e; *overflow = s.overflow;
+    return m;
+}
 uint32_t ch_bits_mask(uint64_t b) { return bits_mask(board_bits(b)); }
 int ch_bits_done(uint64_t b) { return bits_done(board_bits(b)) ? 1 : 0; }
 uint32_t ch_action_mask(uint64_t b) { return action_mask(b); }

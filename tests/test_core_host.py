@@ -30,6 +30,8 @@ def ch():
     L.ch_board_move.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [u32p] * 6
     L.ch_board_move_coded.restype = ctypes.c_uint64
     L.ch_board_move_coded.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [u32p] * 6
+    L.ch_board_move_coded_nolist.restype = ctypes.c_uint64
+    L.ch_board_move_coded_nolist.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [u32p] * 6
     L.ch_bits_mask.restype = ctypes.c_uint32
     L.ch_bits_mask.argtypes = [ctypes.c_uint64]
     L.ch_bits_done.argtypes = [ctypes.c_uint64]
@@ -54,9 +56,12 @@ def ch():
 
 def _move(ch, b, a, coded=False):
     vals = [ctypes.c_uint32() for _ in range(6)]
-    fn = ch.ch_board_move_coded if coded else ch.ch_board_move
+    fn = {False: ch.ch_board_move, True: ch.ch_board_move_coded, "nolist": ch.ch_board_move_coded_nolist}[coded]
     m = fn(b, a, *[ctypes.byref(v) for v in vals])
     lst, cnt, score, sum_e, max_e, ovf = [v.value for v in vals]
+    if coded == "nolist":
+        # the list is not built; its length (the merge count) still is
+        return m, cnt, score, sum_e, max_e, ovf
     merged = [((lst >> (4 * k)) & 15) + 1 for k in range(cnt)]
     return m, merged, score, sum_e, max_e, ovf
 
@@ -67,7 +72,7 @@ def _rand_boards(rng, n, p_empty=0.375, hi=15):
     return [O.pack_exponents(x) for x in e]
 
 
-@pytest.mark.parametrize("coded", [False, True])
+@pytest.mark.parametrize("coded", [False, True, "nolist"])
 def test_board_move_vs_oracle(ch, coded):
     rng = np.random.default_rng(3)
     boards = _rand_boards(rng, 3000) + _rand_boards(rng, 2000, p_empty=0.0, hi=4) + _rand_boards(rng, 1000, 0.7)
@@ -78,7 +83,10 @@ def test_board_move_vs_oracle(ch, coded):
             m, merged, score, sum_e, max_e, ovf = _move(ch, b, a, coded)
             ob, omerged, ochanged, ok = O.move_packed(b, a)
             oe = [int(v).bit_length() - 1 for v in omerged]
-            assert merged == oe, (hex(b), a)
+            if coded == "nolist":
+                assert merged == len(oe), (hex(b), a)
+            else:
+                assert merged == oe, (hex(b), a)
             assert score == sum(omerged) and sum_e == sum(oe) and max_e == max(oe, default=0)
             assert bool(ovf) == (not ok)
             if ok:
