@@ -53,6 +53,22 @@ int fail(int code, const std::string& msg) {
 #define G2048_DIAG 0
 #endif
 
+#if G2048_DIAG
+// per-workgroup phase timestamps of the last step launch (s_memrealtime, 100 MHz): entry, tables filled,
+// main loop done, reset list built, end
+constexpr int kDiagSlots = 5, kDiagBlocks = 4096;
+__device__ uint64_t g_diag_ts[kDiagBlocks * kDiagSlots];
+#define G2048_TS(slot)                                                                          \
+    do {                                                                                        \
+        if (threadIdx.x == 0 && blockIdx.x < kDiagBlocks)                                       \
+            g_diag_ts[blockIdx.x * kDiagSlots + (slot)] = __builtin_amdgcn_s_memrealtime();     \
+    } while (0)
+#else
+#define G2048_TS(slot) \
+    do {               \
+    } while (0)
+#endif
+
 constexpr int kBlock = 1024;                  // 16 waves per CU; one workgroup per CU (160 KiB of LDS tables)
 constexpr int kLines = 65536;
 constexpr int kTabBytes = kLines * 2 + kLines / 2;   // 163,840 B = the whole LDS of a gfx950 CU
@@ -326,6 +342,7 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
 }
 
 // One sweep of one wave: the step of board w0 + lane (inputs already in registers), its mask, the wave's obs.
+// One sweep of one wave: the step of board w0 + lane (inputs already in registers), its mask, the wave's obs.
 // A lane's first pending reset has its seed read here (`pseed`), so the read is long complete at the tail.
 template <int OBS, int RNG, bool LIST>
 __device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, LaneIn& x, const LineFn& lut,
@@ -355,16 +372,21 @@ constexpr int kResetCap = (kTabBytes - 16) / 12;
 static_assert(16 + kResetCap * 4 + kResetCap * 8 <= kTabBytes, "reset list fits the table area");
 static_assert(kTabVec % kBlock == 0, "table fill: whole chunks per thread");
 
-// Persistent over the board array, one board per lane per sweep, software-pipelined with two register buffers
-// A / B (no back-edge copy, which would force a wait on in-flight loads): the loads of sweep s+1 are in flight
-// while sweep s computes.  The first loads are issued before the LDS table fill so they overlap it; each
-// workgroup fills its 10 chunks starting at a different one (blockIdx % 10), so the CUs sharing an L2 do not all
-// read the same lines at once.
-// LDS: stage the two row tables in LDS, else read them through L1/L2 (small batches).  Sweeps per wave <= 64
+// Persistent over the board array, one board per lane per sweep (wave g of W takes the chunks of 64 boards
+// g, g + W, g + 2W, ...), software-pipelined with three register buffers A / B / C (no back-edge copy, which
+// would force a wait on in-flight loads): the loads of the next two sweeps are in flight while one computes.
+// Prefetch loads are issued unconditionally from a clamped lane index (lanes past n re-read lane n-1 and compute
+// nothing): a load skipped on some path would make the compiler's vmcnt accounting assume that path and wait for
+// every load in flight, including those of the sweeps being prefetched.
+// LDS: stage the two row tables in LDS, else read them through L1/L2 (small batches).  The first two sweeps'
+// loads are issued before the table fill; each workgroup fills its 10 chunks starting at a different one
+// (blockIdx % 10), so the CUs sharing an L2 do not read the same lines at once.  Sweeps per wave <= 64
 // (launcher): the `pending` reset bitmask.
 // Auto-resets are deferred to the end.  With the LDS tables dead after the last sweep, the block compacts its
-// pending resets into an LDS list and runs them densely (thread t takes entries t, t + 1024, ...): ~30 resets of a
-// 1M-board step per CU cost one pass of one wave instead of one divergent pass in most of the 16 waves.
+// pending resets into an LDS list and runs them densely (thread t takes entries t, t + 1024, ...): ~30 resets
+// of a 1M-board step per CU cost one pass of one wave instead of one divergent pass in most of the 16 waves.
+// (A dynamic schedule -- chunks claimed with device-scope atomics -- measured slower on MI355X: under this
+// kernel's streaming load an atomic's return takes microseconds, and same-address atomics serialize.)
 template <int OBS, int RNG, bool LDS, bool LIST, int U>
 __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     static_assert(U == 1, "one board per lane per sweep");
@@ -372,9 +394,13 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     const int lane = threadIdx.x & 63;
     const uint32_t w_first = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
     const uint32_t wstride = gridDim.x * kBlock;
-    LaneIn A, B;
-    uint32_t w0 = w_first;
-    if (w0 + lane < a.n) load_lane<RNG>(a, w0 + lane, A);
+    const uint32_t last = a.n - 1u;           // n >= 1 (the launcher never launches n == 0)
+    const auto lane_at = [&](uint32_t w) { return w + lane < last ? w + lane : last; };
+    G2048_TS(0);
+    LaneIn A, B, C;
+    uint32_t w0 = w_first, w1 = w_first + wstride;
+    load_lane<RNG>(a, lane_at(w0), A);
+    load_lane<RNG>(a, lane_at(w1), B);
     const uint8_t* tab = a.tab;
     if constexpr (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(a.tab);
@@ -392,20 +418,26 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
         __syncthreads();
         tab = reinterpret_cast<const uint8_t*>(tab_lds);
     }
+    G2048_TS(1);
     const LineFn lut{reinterpret_cast<const uint16_t*>(tab)};
     const CodeFn code{tab + 2 * kLines};
     uint64_t pending = 0, pseed = 0;
     uint32_t k = 0;
     while (w0 < a.n) {                         // wave-uniform
-        const uint32_t w1 = w0 + wstride;
-        if (w1 + lane < a.n) load_lane<RNG>(a, w1 + lane, B);
+        const uint32_t w2 = w1 + wstride;
+        load_lane<RNG>(a, lane_at(w2), C);
         sweep<OBS, RNG, LIST>(a, w0, lane, A, lut, code, pending, pseed, k);
         if (w1 >= a.n) break;
-        const uint32_t w2 = w1 + wstride;
-        if (w2 + lane < a.n) load_lane<RNG>(a, w2 + lane, A);
+        const uint32_t w3 = w2 + wstride;
+        load_lane<RNG>(a, lane_at(w3), A);
         sweep<OBS, RNG, LIST>(a, w1, lane, B, lut, code, pending, pseed, k + 1);
-        w0 = w2;
-        k += 2;
+        if (w2 >= a.n) break;
+        const uint32_t w4 = w3 + wstride;
+        load_lane<RNG>(a, lane_at(w4), B);
+        sweep<OBS, RNG, LIST>(a, w2, lane, C, lut, code, pending, pseed, k + 2);
+        w0 = w3;
+        w1 = w4;
+        k += 3;
     }
     if (G2048_DIAG && (a.diag & 2)) pending = 0;
     if constexpr (LDS) {
@@ -413,6 +445,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
         uint32_t* ridx = cnt + 4;
         uint64_t* rseed = reinterpret_cast<uint64_t*>(ridx + kResetCap + (kResetCap & 1));
         __syncthreads();                       // every wave is past its last table read
+        G2048_TS(2);
         if (threadIdx.x == 0) *cnt = 0u;
         __syncthreads();
         bool first = true;
@@ -440,6 +473,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
             first = false;
         }
         __syncthreads();
+        G2048_TS(3);
         const uint32_t R = *cnt < (uint32_t)kResetCap ? *cnt : (uint32_t)kResetCap;
         for (uint32_t r = threadIdx.x; r < R; r += kBlock) reset_lane<OBS, RNG>(a, ridx[r], rseed[r]);
     } else {
@@ -452,6 +486,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
             first = false;
         }
     }
+#if G2048_DIAG
+    __syncthreads();
+    G2048_TS(4);
+#endif
 }
 
 // ------------------------------------------------------------------------------------- other kernels
@@ -777,6 +815,17 @@ int device_cus(int dev) {
 extern "C" {
 
 int g2048_abi_version(void) { return G2048_ABI_VERSION; }
+
+#if G2048_DIAG
+// diag build only: copy the phase timestamps of the last step launch (blocks x 5 u64) to host memory
+int g2048_diag_times(uint64_t* out, int blocks) {
+    if (blocks > kDiagBlocks) blocks = kDiagBlocks;
+    G2048_HIP(hipDeviceSynchronize());
+    G2048_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_ts), sizeof(uint64_t) * kDiagSlots * blocks, 0,
+                                  hipMemcpyDeviceToHost));
+    return blocks;
+}
+#endif
 
 const char* g2048_last_error(void) { return g_err.c_str(); }
 
