@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import os
 from dataclasses import dataclass
 from typing import Any, Callable, Literal
 
@@ -201,6 +202,70 @@ class ReinforceAgent:
     def save_model(self, file_path: str = "params.npz") -> None:
         """src/reinforce_agent.py:119-123"""
         save_model_params(self.params, file_path)
+
+    # ============================================================================================ checkpoints
+    # Resume-capable checkpoints (SURVEY.md section 8f item 4; the reference's model_*.npz holds the actor only,
+    # runner.py:642-660).  One npz, no pickle: the actor under the reference's keys (n_layers, W_i, b_i -- so a
+    # checkpoint also loads with load_model / src/MLP.py:97-107), then Adam moments and step counters, the critic
+    # and its Adam state, and caller state under "extra_<name>".
+    def checkpoint_state(self) -> dict[str, np.ndarray]:
+        def host(t):
+            return t.detach().to("cpu").numpy()
+
+        st: dict[str, np.ndarray] = {"n_layers": np.array(len(self.params["W"]), dtype=np.int64),
+                                     "adam_t": np.array(self._adam_t, dtype=np.int64)}
+        for i, (W, b) in enumerate(zip(self.params["W"], self.params["b"])):
+            st[f"W_{i}"], st[f"b_{i}"] = host(W), host(b)
+            st[f"adam_mW_{i}"], st[f"adam_vW_{i}"] = host(self._adam_m_W[i]), host(self._adam_v_W[i])
+            st[f"adam_mb_{i}"], st[f"adam_vb_{i}"] = host(self._adam_m_B[i]), host(self._adam_v_B[i])
+        if self.critic_params is not None:
+            st["critic_n_layers"] = np.array(len(self.critic_params["W"]), dtype=np.int64)
+            st["critic_adam_t"] = np.array(self._adam_t_c, dtype=np.int64)
+            for i, (W, b) in enumerate(zip(self.critic_params["W"], self.critic_params["b"])):
+                st[f"critic_W_{i}"], st[f"critic_b_{i}"] = host(W), host(b)
+                st[f"critic_adam_mW_{i}"], st[f"critic_adam_vW_{i}"] = host(self._adam_m_W_c[i]), host(self._adam_v_W_c[i])
+                st[f"critic_adam_mb_{i}"], st[f"critic_adam_vb_{i}"] = host(self._adam_m_B_c[i]), host(self._adam_v_B_c[i])
+        return st
+
+    def load_checkpoint_state(self, st) -> None:
+        def dev(a):
+            return torch.as_tensor(np.asarray(a, dtype=np.float32), device=self.device).contiguous()
+
+        n = int(st["n_layers"])
+        self.params = {"W": [dev(st[f"W_{i}"]) for i in range(n)], "b": [dev(st[f"b_{i}"]) for i in range(n)]}
+        self.mlp_config.hidden_sizes = [int(W.shape[1]) for W in self.params["W"][:-1]]
+        self._adam_m_W = [dev(st[f"adam_mW_{i}"]) for i in range(n)]
+        self._adam_v_W = [dev(st[f"adam_vW_{i}"]) for i in range(n)]
+        self._adam_m_B = [dev(st[f"adam_mb_{i}"]) for i in range(n)]
+        self._adam_v_B = [dev(st[f"adam_vb_{i}"]) for i in range(n)]
+        self._adam_t = int(st["adam_t"])
+        if (self.critic_params is not None) != ("critic_n_layers" in st):
+            raise ValueError("checkpoint critic does not match agent_config.use_critic")
+        if self.critic_params is not None:
+            m = int(st["critic_n_layers"])
+            self.critic_params = {"W": [dev(st[f"critic_W_{i}"]) for i in range(m)],
+                                  "b": [dev(st[f"critic_b_{i}"]) for i in range(m)]}
+            self._adam_m_W_c = [dev(st[f"critic_adam_mW_{i}"]) for i in range(m)]
+            self._adam_v_W_c = [dev(st[f"critic_adam_vW_{i}"]) for i in range(m)]
+            self._adam_m_B_c = [dev(st[f"critic_adam_mb_{i}"]) for i in range(m)]
+            self._adam_v_B_c = [dev(st[f"critic_adam_vb_{i}"]) for i in range(m)]
+            self._adam_t_c = int(st["critic_adam_t"])
+
+    def save_checkpoint(self, file_path: str, extra: dict | None = None) -> None:
+        st = self.checkpoint_state()
+        for k, v in (extra or {}).items():
+            st[f"extra_{k}"] = np.asarray(v)
+        tmp = str(file_path) + ".tmp.npz"
+        np.savez(tmp, **st)
+        os.replace(tmp, file_path)
+
+    def load_checkpoint(self, file_path: str) -> dict:
+        """Restores what save_checkpoint wrote; returns the extra_* entries (numpy scalars / arrays)."""
+        with np.load(file_path, allow_pickle=False) as z:
+            st = {k: z[k] for k in z.files}
+        self.load_checkpoint_state(st)
+        self._logger.info(f"Checkpoint loaded from {file_path}")
+        return {k[len("extra_"):]: v for k, v in st.items() if k.startswith("extra_")}
 
     # ============================================================================================ helpers
     @property

@@ -146,6 +146,13 @@ class SeedStream:
     def take(self, n: int) -> list[int]:
         return [int(x) for x in self.rng.integers(0, self.hi, size=n, dtype=np.int64)]
 
+    def skip(self, n: int) -> None:
+        """Advance past n seeds (what take(n) consumes), a block at a time."""
+        while n > 0:
+            k = min(n, 1 << 20)
+            self.rng.integers(0, self.hi, size=k, dtype=np.int64)
+            n -= k
+
 
 # ---------------------------------------------------------------------------------------------- helpers
 def build_full_config_dict(env_config, mlp_config, agent_config, extra=None) -> Dict[str, Any]:
@@ -210,9 +217,16 @@ def build_training_components(device=None):
 
 def training_loop(agent: ReinforceAgent, env_config, mlp_config, agent_config, train_cfg: Dict[str, Any],
                   run_dir: Path, run_id: str) -> List[Dict[str, Any]]:
-    """runner.py:495-679 with batched rollouts.  Returns the CSV rows written (rank 0)."""
+    """runner.py:495-679 with batched rollouts.  Returns the CSV rows written (rank 0).
+
+    Beyond the reference: train_cfg["checkpoint_every"] = N > 0 writes
+    run_dir/checkpoint_latest.npz after every N-th update (actor, critic, Adam state, batch index, best average,
+    seed-stream positions); train_cfg["resume_from"] = path continues from such a file, so an interrupted run
+    resumed from batch b produces the same later batches as the uninterrupted run."""
     bs = int(train_cfg["batch_size"])
     nb = int(train_cfg["num_batches"])
+    ckpt_every = int(train_cfg.get("checkpoint_every") or 0)
+    resume_from = train_cfg.get("resume_from")
     rank, _ = dp.world()
     if rank == 0:
         attach_run_file_logger(run_dir / f"train_{run_id}.log")
@@ -227,8 +241,18 @@ def training_loop(agent: ReinforceAgent, env_config, mlp_config, agent_config, t
     best = float("-inf")
     rows: List[Dict[str, Any]] = []
     step = 0
+    if resume_from:
+        extra = agent.load_checkpoint(str(resume_from))
+        if int(extra["batch_size"]) != bs or int(extra["env_base_seed"]) != int(train_cfg["env_base_seed"]) or \
+                int(extra["policy_base_seed"]) != int(train_cfg["policy_base_seed"]):
+            raise ValueError("resume_from: batch_size / base seeds differ from the checkpoint's run")
+        step = int(extra["batch"])
+        best = float(extra["best_avg_reward"])
+        env_stream.skip(int(extra["env_seeds_drawn"]))
+        pol_stream.skip(int(extra["policy_seeds_drawn"]))
+        logger.info("Resumed from %s at batch %d", resume_from, step)
     lo, hi = _shard(bs)
-    while True:
+    while nb <= 0 or step < nb:
         env_seeds, pol_seeds = env_stream.take(bs), pol_stream.take(bs)
         batch = agent.rollout_batch(env_seeds[lo:hi], pol_seeds[lo:hi])
         step += 1
@@ -258,8 +282,11 @@ def training_loop(agent: ReinforceAgent, env_config, mlp_config, agent_config, t
         if rank == 0:
             safe_append_csv_row(csv_path, fields, row)
         rows.append(row)
-        if nb > 0 and step >= nb:
-            break
+        if ckpt_every > 0 and step % ckpt_every == 0 and rank == 0:
+            agent.save_checkpoint(str(run_dir / "checkpoint_latest.npz"), extra={
+                "batch": step, "best_avg_reward": best, "batch_size": bs, "env_seeds_drawn": step * bs,
+                "policy_seeds_drawn": step * bs, "env_base_seed": int(train_cfg["env_base_seed"]),
+                "policy_base_seed": int(train_cfg["policy_base_seed"])})
     logger.info("Training finished.")
     return rows
 

@@ -69,3 +69,34 @@ def test_cli_training_run(tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     runs = list((tmp_path / "training_history").iterdir())
     assert len(runs) == 1 and (runs[0] / "training_stats.csv").exists()
+
+
+def test_resume_reproduces_uninterrupted_run(R, tmp_path):
+    """checkpoint_every / resume_from: batches 3-4 of a run resumed from its batch-2 checkpoint equal those of the
+    uninterrupted 4-batch run, and so do the final actor / critic parameters and Adam state."""
+    tc = dict(R.DEFAULT_TRAIN_CONFIG, num_batches=4)
+    agent, ec, mc, ac, _ = R.build_training_components(DEV)
+    (tmp_path / "full_run").mkdir()
+    full = R.training_loop(agent, ec, mc, ac, tc, tmp_path / "full_run", "f")
+    a1, *_ = R.build_training_components(DEV)
+    (tmp_path / "part1").mkdir()
+    R.training_loop(a1, ec, mc, ac, dict(tc, num_batches=2, checkpoint_every=2), tmp_path / "part1", "p1")
+    ck = tmp_path / "part1" / "checkpoint_latest.npz"
+    assert ck.exists()
+    a2, *_ = R.build_training_components(DEV)
+    (tmp_path / "part2").mkdir()
+    rest = R.training_loop(a2, ec, mc, ac, dict(tc, resume_from=str(ck)), tmp_path / "part2", "p2")
+    assert [r["batch"] for r in rest] == [3, 4]
+    for got, ref in zip(rest, full[2:]):
+        assert got["max_tile_counts"] == ref["max_tile_counts"]
+        for k in ("avg_reward", "max_reward", "min_reward"):
+            assert got[k] == pytest.approx(ref[k], rel=1e-5, abs=1e-5)
+    sa, sb = agent.checkpoint_state(), a2.checkpoint_state()
+    assert sorted(sa) == sorted(sb)
+    for k in sa:
+        np.testing.assert_allclose(sb[k], sa[k], rtol=1e-5, atol=1e-6, err_msg=k)
+    # the checkpoint's actor loads as a reference model file (src/MLP.py:97-107 keys)
+    from rl2048_amd.mlp import load_model_params
+
+    p = load_model_params(str(ck))
+    assert len(p["W"]) == len(agent.params["W"])

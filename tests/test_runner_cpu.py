@@ -68,3 +68,13 @@ def test_csv_schema(R, tmp_path):
                                       "max_tile_counts": json.dumps([1] + [0] * 8)})
     lines = p.read_text().strip().splitlines()
     assert lines[0] == ",".join(fields) and len(lines) == 3
+
+
+def test_seed_stream_skip(R):
+    """SeedStream.skip(n) consumes exactly what take(n) does (resume support)."""
+    for base, n in ((3, 0), (7, 1), (12345, 700), (54321, (1 << 20) + 17)):
+        ref = R.SeedStream(base)
+        ref.take(n)
+        s = R.SeedStream(base)
+        s.skip(n)
+        assert s.take(40) == ref.take(40)
