@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env steps/sec (whole node) + achieved HBM GB/s, batch=1M 4x4 boards"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+POLICY_FLOP_PER_BOARD = 2 * (16 * 256 + 256 * 256 + 256 * 4)  # 141,312: the runner-default MLP forward
 
 # Algorithmic bytes one g2048_step moves per board in steady state (no reset), by mode.  Reads / writes:
 #   board 8/8, action 1/-, status 1/-, step_count 4/4, max_tile 1/1, score 4/4, reward -/4, flags -/1, mask -/4
@@ -166,9 +167,10 @@ def cpu_baseline(args, seconds: float) -> dict:
 
 
 # ---------------------------------------------------------------------------------------------- policy loop
-def policy_rollout_rate(torch, B: int, device, steps: int = 20, warmup: int = 5) -> dict:
-    """Env steps/s with the runner-default policy in the loop: MLP [256,256] ReLU HeNormal (fp32, hipBLASLt) on
-    log2 obs -> fused masked-softmax + numpy-PCG64 choice kernel -> fused env step (auto-reset)."""
+def policy_rollout_rate(torch, B: int, device, steps: int = 20, warmup: int = 5, fused: bool = True) -> dict:
+    """Env steps/s with the runner-default policy in the loop: MLP [256,256] ReLU HeNormal fp32 on log2 obs.
+    fused: g2048_policy (fp32 MFMA forward + numpy-PCG64 choice straight from the bitboards) -> env step without
+    the obs buffer; else hipBLASLt GEMMs (bias + ReLU epilogue) on the env's obs -> g2048_sample -> env step."""
     from rl2048_amd import Game2048EnvConfig, VecGame2048Env
     from rl2048_amd import _lib as L
     from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
@@ -187,12 +189,20 @@ def policy_rollout_rate(torch, B: int, device, steps: int = 20, warmup: int = 5)
     stream = L.stream_handle(device)
     L.check(lib.g2048_seed_pcg64(L.ptr(seeds), L.ptr(st), L.ptr(inc), L.ptr(buf), B, stream))
     acts = torch.empty(B, dtype=torch.uint8, device=device)
+    spec = agent._fused_policy_spec()
+    packed = agent._packed_policy(spec)
 
     def one():
-        logits = agent._policy_logits(env.obs)
-        L.check(lib.g2048_sample(L.ptr(logits), L.ptr(env.mask), None, 0, 0, L.ptr(st), L.ptr(inc), L.ptr(buf), 0,
-                                 None, None, None, L.ptr(acts), B, stream))
-        env.step_into(acts)
+        if fused:
+            L.check(lib.g2048_policy(L.ptr(packed), spec[0], spec[1], spec[2], L.ptr(env.board), L.ptr(env.status),
+                                     L.OBS_LOG2, 0.0625, 1, 0, L.RNG_PCG64, L.ptr(st), L.ptr(inc), L.ptr(buf), 0,
+                                     None, None, None, None, L.ptr(acts), B, stream))
+            env.step_into(acts, write_obs=False)
+        else:
+            logits = agent._policy_logits(env.obs)
+            L.check(lib.g2048_sample(L.ptr(logits), L.ptr(env.mask), None, 0, 0, L.ptr(st), L.ptr(inc), L.ptr(buf),
+                                     0, None, None, None, L.ptr(acts), B, stream))
+            env.step_into(acts)
 
     with torch.no_grad():
         for _ in range(warmup):
@@ -203,8 +213,11 @@ def policy_rollout_rate(torch, B: int, device, steps: int = 20, warmup: int = 5)
             one()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+    path = ("fused g2048_policy (fp32 MFMA) + step without obs" if fused else
+            "hipBLASLt GEMMs + g2048_sample + step with obs")
     return {"value": steps * B / dt, "unit": "env steps/s", "boards": B, "steps": steps,
-            "ms_per_step": dt / steps * 1e3, "model": "MLP 16-256-256-4 ReLU fp32 (runner.py defaults)"}
+            "ms_per_step": dt / steps * 1e3, "model": "MLP 16-256-256-4 ReLU fp32 (runner.py defaults)",
+            "path": path, "policy_tflops": steps * B * POLICY_FLOP_PER_BOARD / dt / 1e12}
 
 
 # ---------------------------------------------------------------------------------------------- main
@@ -285,6 +298,7 @@ def main():
             del actions
             torch.cuda.empty_cache()
             policy = policy_rollout_rate(torch, B, device)
+            policy["gemm_path"] = policy_rollout_rate(torch, B, device, fused=False)
         except Exception as e:  # noqa: BLE001 -- an extra, never the headline
             policy = {"error": repr(e)}
     if world > 1:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 1
+#define G2048_ABI_VERSION 2
 
 /* status codes */
 #define G2048_OK 0
@@ -166,6 +166,33 @@ int g2048_returns(const float* rewards, const int32_t* lengths, double gamma, fl
  * masks are recomputed from the transformed boards by g2048_obs. */
 int g2048_symmetries(const uint64_t* boards, const uint8_t* actions, uint64_t* out_boards, uint8_t* out_actions,
                      int64_t n, void* stream);
+
+/* ---- fused policy (rollout / evaluation forward) ----------------------------------------------------------
+ * One kernel for forward_logits (src/MLP.py:159-196) + logits_to_probs (:139-156) + the action choice of
+ * select_action (src/reinforce_agent.py:178-190), for the reference's MLP with two hidden layers of 1..256 units
+ * (MLPConfig.hidden_sizes, src/MLP.py:45-94), obs width 16 ("log2" / "raw" obs built from the bitboards in the
+ * kernel), ReLU or Sigmoid, 4 actions.  fp32 throughout (MFMA f32: a k-ordered fmaf chain), so it agrees with the
+ * GEMM path up to fp32 summation order; the choice is the g2048_sample code on the resulting probabilities. */
+#define G2048_ACT_RELU 0
+#define G2048_ACT_SIGMOID 1
+
+/* floats of the packed net for hidden sizes (h1, h2); -1 if unsupported */
+int64_t g2048_policy_packed_size(int h1, int h2);
+
+/* Pack W1 [in_dim x h1], b1 [h1], W2 [h1 x h2], b2 [h2], W3 [h2 x 4], b3 [4] (row-major, x @ W layout of
+ * src/MLP.py) into `packed` (g2048_policy_packed_size floats, device memory).  Re-pack after every update. */
+int g2048_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                      const float* b3, int in_dim, int h1, int h2, float* packed, int64_t packed_len, void* stream);
+
+/* boards [n]; active [n] status bytes (bit 0 = active; NULL = all) -- inactive lanes are left untouched;
+ * use_mask: mask the logits with the boards' action masks (Game2048.get_action_mask, src/game2048.py:95-99);
+ * greedy / rng_mode / rng_* / philox_key / lane_seed / counter / probs_out / actions as in g2048_sample;
+ * logits_out [n*4] may be NULL. */
+int g2048_policy(const float* packed, int h1, int h2, int activation, const uint64_t* boards, const uint8_t* active,
+                 int obs_mode, float obs_scale, int use_mask, int greedy, int rng_mode, uint64_t* rng_state,
+                 const uint64_t* rng_inc, const uint64_t* rng_buf, uint64_t philox_key, const uint64_t* lane_seed,
+                 const uint32_t* counter, float* probs_out, float* logits_out, uint8_t* actions, int64_t n,
+                 void* stream);
 
 #ifdef __cplusplus
 }

@@ -21,11 +21,13 @@ LIB_PATH = SHIPPED_LIB
 if os.environ.get("G2048_DIAG_LIB"):
     LIB_PATH = os.environ["G2048_DIAG_LIB"]
 SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
+SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # include/g2048.h constants
 OBS_NONE, OBS_RAW, OBS_LOG2, OBS_ONEHOT = -1, 0, 1, 2
+ACT_RELU, ACT_SIGMOID = 0, 1
 RNG_PCG64, RNG_PHILOX = 0, 1
 F_CHANGED, F_TERMINATED, F_TRUNCATED, F_INVALID = 0x01, 0x02, 0x04, 0x08
 F_OVERFLOW, F_RESET, F_INACTIVE, F_BADACTION = 0x10, 0x20, 0x40, 0x80
@@ -37,7 +39,7 @@ def build(verbose: bool = False) -> str:
     """Compile libg2048.so for gfx950 in-tree (hipcc cross-compiles; no GPU needed)."""
     # -ffp-contract=off: the fp64 reward keeps the reference's separately rounded multiply and add (no FMA)
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", "-I" + INCLUDE,
-           "-I" + os.path.dirname(SRC), "-o", SHIPPED_LIB, SRC]
+           "-I" + os.path.dirname(SRC), "-o", SHIPPED_LIB] + SOURCES
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
@@ -83,13 +85,19 @@ def _declare(L):
     L.g2048_sample.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp, u64, vp, vp, vp, vp, i64, vp]
     L.g2048_returns.argtypes = [vp, vp, d, vp, i64, i64, vp]
     L.g2048_symmetries.argtypes = [vp, vp, vp, vp, i64, vp]
+    L.g2048_policy_packed_size.argtypes = [i32, i32]
+    L.g2048_policy_packed_size.restype = i64
+    L.g2048_policy_pack.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i64, vp]
+    L.g2048_policy.argtypes = [vp, i32, i32, i32, vp, vp, i32, f, i32, i32, i32, vp, vp, vp, u64, vp, vp, vp, vp, vp,
+                               i64, vp]
     for name in ("g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step", "g2048_obs", "g2048_move",
-                 "g2048_sample", "g2048_returns", "g2048_symmetries"):
+                 "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy"):
         getattr(L, name).restype = ctypes.c_int
 
 
 EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g2048_seed_pcg64", "g2048_reset",
-                    "g2048_step", "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries")
+                    "g2048_step", "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries",
+                    "g2048_policy_packed_size", "g2048_policy_pack", "g2048_policy")
 
 
 def lib():

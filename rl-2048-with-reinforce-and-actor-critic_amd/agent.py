@@ -188,6 +188,11 @@ class ReinforceAgent:
             self._init_adam(self.critic_params, prefix="critic")
             self._adam_t_c = 0
         self.chunk_steps = int(chunk_steps)
+        # rollout / evaluation forward through the fused g2048_policy kernel when the net fits it
+        self.use_fused_policy = True
+        self._params_version = 0
+        self._packed: torch.Tensor | None = None
+        self._pack_key = None
         self._vec_cache: dict = {}
         self._lib = L.lib()
         self.last_stats: dict = {}
@@ -197,6 +202,7 @@ class ReinforceAgent:
         """src/reinforce_agent.py:108-116"""
         self.params = load_model_params(file_path, device=self.device)
         self.mlp_config.hidden_sizes = [int(W.shape[1]) for W in self.params["W"][:-1]]
+        self._params_version += 1
         self._logger.info(f"Model parameters loaded from {file_path}")
 
     def save_model(self, file_path: str = "params.npz") -> None:
@@ -234,6 +240,7 @@ class ReinforceAgent:
         n = int(st["n_layers"])
         self.params = {"W": [dev(st[f"W_{i}"]) for i in range(n)], "b": [dev(st[f"b_{i}"]) for i in range(n)]}
         self.mlp_config.hidden_sizes = [int(W.shape[1]) for W in self.params["W"][:-1]]
+        self._params_version += 1
         self._adam_m_W = [dev(st[f"adam_mW_{i}"]) for i in range(n)]
         self._adam_v_W = [dev(st[f"adam_vW_{i}"]) for i in range(n)]
         self._adam_m_B = [dev(st[f"adam_mb_{i}"]) for i in range(n)]
@@ -310,6 +317,39 @@ class ReinforceAgent:
     def _policy_logits(self, x: torch.Tensor) -> torch.Tensor:
         return forward_logits(self.params, x, self.mlp_config.activation, keep_cache=False)[0]
 
+    def _fused_policy_spec(self):
+        """(h1, h2, activation code) when g2048_policy covers the actor (obs width 16, two hidden layers of
+        1..256 units, ReLU / Sigmoid, fp32), else None (the GEMM path + g2048_sample then runs)."""
+        if not self.use_fused_policy or self.env_config.obs_mode not in ("log2", "raw"):
+            return None
+        Ws, bs = self.params["W"], self.params["b"]
+        if len(Ws) != 3 or len(bs) != 3 or tuple(Ws[0].shape)[0] != 16 or tuple(Ws[2].shape)[1] != 4:
+            return None
+        h1, h2 = int(Ws[0].shape[1]), int(Ws[1].shape[1])
+        act = {"ReLU": L.ACT_RELU, "Sigmoid": L.ACT_SIGMOID}.get(self.mlp_config.activation)
+        if act is None or not (1 <= h1 <= 256 and 1 <= h2 <= 256) or tuple(Ws[1].shape)[0] != h1 or \
+                tuple(Ws[2].shape)[0] != h2:
+            return None
+        if any(t.dtype != torch.float32 or t.device != self.device for t in Ws + bs):
+            return None
+        return h1, h2, act
+
+    def _packed_policy(self, spec) -> torch.Tensor:
+        """The actor packed in MFMA fragment order (g2048_policy_pack), re-packed whenever a parameter tensor is
+        replaced or modified in place (or after an update / load)."""
+        Ws, bs = self.params["W"], self.params["b"]
+        key = (self._params_version,) + tuple((t.data_ptr(), t._version) for t in Ws + bs)
+        if key != self._pack_key:
+            h1, h2, _ = spec
+            size = int(self._lib.g2048_policy_packed_size(h1, h2))
+            if self._packed is None or self._packed.numel() < size:
+                self._packed = torch.empty(size, dtype=torch.float32, device=self.device)
+            w = [t.contiguous() for t in (Ws[0], bs[0], Ws[1], bs[1], Ws[2], bs[2])]
+            L.check(self._lib.g2048_policy_pack(*[L.ptr(t) for t in w], 16, h1, h2, L.ptr(self._packed), size,
+                                                self._stream))
+            self._pack_key = key
+        return self._packed
+
     # ============================================================================================ acting
     def select_action(self, obs, rng: np.random.Generator, action_fn: Callable | None = None,
                       use_greedy: bool = False):
@@ -371,6 +411,11 @@ class ReinforceAgent:
         rewards = torch.empty(cap, n, dtype=torch.float32, device=dev)
         flags = torch.empty(cap, n, dtype=torch.uint8, device=dev)
         probs = torch.zeros(cap, n, 4, dtype=torch.float32, device=dev) if record_probs else None
+        # the reference masks the logits only when the obs carries an action mask (encode_observation,
+        # src/MLP.py:22-43 -> select_action src/reinforce_agent.py:138-145)
+        use_mask = bool(self.env_config.use_action_mask)
+        spec = self._fused_policy_spec()
+        packed = self._packed_policy(spec) if spec is not None else None
         t = 0
         while True:
             if t == cap:
@@ -382,13 +427,24 @@ class ReinforceAgent:
                 if probs is not None:
                     probs = torch.cat([probs, torch.zeros(grow, n, 4, dtype=torch.float32, device=dev)])
                 cap += grow
-            logits = self._policy_logits(env.obs)
-            L.check(self._lib.g2048_sample(L.ptr(logits), L.ptr(env.mask), L.ptr(env.status), int(use_greedy),
-                                           rng_mode, L.ptr(pst), L.ptr(pinc), L.ptr(pbuf), env.philox_key ^ 0x5A5A,
-                                           L.ptr(pseeds), L.ptr(env.step_count),
-                                           L.ptr(probs[t]) if probs is not None else None, L.ptr(actions[t]), n,
-                                           self._stream))
-            env.step_into(actions[t], reward=rewards[t], flags=flags[t], prev_board=boards[t])
+            if spec is not None:
+                # fused forward + choice straight from the boards; the step then skips the obs buffer
+                L.check(self._lib.g2048_policy(L.ptr(packed), spec[0], spec[1], spec[2], L.ptr(env.board),
+                                               L.ptr(env.status), _OBS_CODE[self.env_config.obs_mode],
+                                               float(self.env_config.obs_log2_scale), int(use_mask),
+                                               int(use_greedy), rng_mode, L.ptr(pst), L.ptr(pinc), L.ptr(pbuf),
+                                               env.philox_key ^ 0x5A5A, L.ptr(pseeds), L.ptr(env.step_count),
+                                               L.ptr(probs[t]) if probs is not None else None, None,
+                                               L.ptr(actions[t]), n, self._stream))
+                env.step_into(actions[t], reward=rewards[t], flags=flags[t], prev_board=boards[t], write_obs=False)
+            else:
+                logits = self._policy_logits(env.obs)
+                L.check(self._lib.g2048_sample(L.ptr(logits), L.ptr(env.mask) if use_mask else None,
+                                               L.ptr(env.status), int(use_greedy), rng_mode, L.ptr(pst),
+                                               L.ptr(pinc), L.ptr(pbuf), env.philox_key ^ 0x5A5A, L.ptr(pseeds),
+                                               L.ptr(env.step_count), L.ptr(probs[t]) if probs is not None else None,
+                                               L.ptr(actions[t]), n, self._stream))
+                env.step_into(actions[t], reward=rewards[t], flags=flags[t], prev_board=boards[t])
             t += 1
             if t % check_every == 0 and not bool(env.status.any()):
                 break
@@ -686,6 +742,7 @@ class ReinforceAgent:
                 self._adam_update(gWc, gbc, prefix="critic")
         else:
             raise ValueError(f"Unknown optimizer: {c.optimizer}")
+        self._params_version += 1
         if self._logger.isEnabledFor(logging.INFO):
             self._logger.info(f"Global Grad Norms: Actor: {stats['actor_grad_norm']:.4f}")
             if c.use_critic:

@@ -603,31 +603,11 @@ template <int RNG>
 __global__ void __launch_bounds__(256) sample_kernel(SampleArgs a) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
         if (a.active && !ld(a.active, i)) continue;
-        const float4 lg = ld(reinterpret_cast<const float4*>(a.logits), i);
-        uint32_t mw = 0x01010101u;
-        if (a.mask) mw = ld(reinterpret_cast<const uint32_t*>(a.mask), i);
-        const bool m0 = mw & 0xFFu, m1 = (mw >> 8) & 0xFFu, m2 = (mw >> 16) & 0xFFu, m3 = mw >> 24;
-        const float l0 = m0 ? lg.x : -1e9f, l1 = m1 ? lg.y : -1e9f, l2 = m2 ? lg.z : -1e9f, l3 = m3 ? lg.w : -1e9f;
-        const float mx = fmaxf(fmaxf(l0, l1), fmaxf(l2, l3));
-        const float e0 = expf(l0 - mx), e1 = expf(l1 - mx), e2 = expf(l2 - mx), e3 = expf(l3 - mx);
-        const float s = ((e0 + e1) + e2) + e3;
-        const float p[4] = {e0 / s, e1 / s, e2 / s, e3 / s};
-        if (a.probs_out) st(reinterpret_cast<float4*>(a.probs_out), i, make_float4(p[0], p[1], p[2], p[3]));
-        uint32_t act = 0;
-        if (a.greedy) {
-            // probs = probs * action_mask; argmax (first maximum)
-            const float q[4] = {a.mask ? p[0] * (float)m0 : p[0], a.mask ? p[1] * (float)m1 : p[1],
-                                a.mask ? p[2] * (float)m2 : p[2], a.mask ? p[3] * (float)m3 : p[3]};
-            float best = q[0];
-#pragma unroll
-            for (int k = 1; k < 4; k++)
-                if (q[k] > best) { best = q[k]; act = k; }
-        } else {
-            // Generator.choice(4, p): fp64 cdf, normalised by its last entry, searchsorted(side='right')
-            double cdf[4], acc = 0.0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) { acc += (double)p[k]; cdf[k] = acc; }
-            double u;
+        const float4 lg4 = ld(reinterpret_cast<const float4*>(a.logits), i);
+        const float lg[4] = {lg4.x, lg4.y, lg4.z, lg4.w};
+        const uint32_t mw = a.mask ? ld(reinterpret_cast<const uint32_t*>(a.mask), i) : 0x01010101u;
+        double u = 0.0;
+        if (!a.greedy) {
             if constexpr (RNG == G2048_RNG_PCG64) {
                 Pcg64 g;
                 const ulonglong2 sv = ld(reinterpret_cast<const ulonglong2*>(a.rs), i);
@@ -643,9 +623,10 @@ __global__ void __launch_bounds__(256) sample_kernel(SampleArgs a) {
                 const uint64_t x = ((uint64_t)r.x << 32) | r.y;
                 u = (double)(x >> 11) * (1.0 / 9007199254740992.0);
             }
-#pragma unroll
-            for (int k = 0; k < 4; k++) act += (cdf[k] / cdf[3] <= u) ? 1u : 0u;
         }
+        float p[4];
+        const uint32_t act = softmax_select(lg, mw, a.mask != nullptr, a.greedy != 0, u, p);
+        if (a.probs_out) st(reinterpret_cast<float4*>(a.probs_out), i, make_float4(p[0], p[1], p[2], p[3]));
         st(a.actions, i, (uint8_t)act);
     }
 }
@@ -811,6 +792,11 @@ int device_cus(int dev) {
 }
 
 }  // namespace
+
+// error string shared with the other translation unit of the library (g2048_policy.hip)
+namespace g2048_internal {
+int set_error(int code, const char* msg) { return fail(code, msg); }
+}  // namespace g2048_internal
 
 extern "C" {
 

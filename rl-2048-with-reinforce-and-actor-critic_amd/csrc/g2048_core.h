@@ -6,6 +6,7 @@
 //
 // Every function names the reference semantics it implements (paths relative to the reference repo root).
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #ifdef __HIPCC__
@@ -490,6 +491,40 @@ G2048_HD uint64_t spawn_pcg(uint64_t b, Pcg64& g) {
     uint32_t cell = kth_empty_cell(z, k);
     uint64_t e = pcg_random(g) < 0.9 ? 1u : 2u;
     return b | (e << (4u * cell));
+}
+
+// logits_to_probs (src/MLP.py:139-156) + the action choice of select_action (src/reinforce_agent.py:178-190) for
+// one board: where(mask, logits, -1e9), max-shifted softmax in fp32; greedy = argmax of probs*mask (first
+// maximum); else Generator.choice(4, p): fp64 cdf normalised by its last entry, searchsorted(side='right') of the
+// uniform draw u.  mw: int8[4] mask as one word (byte a = action a); has_mask false = no mask.
+G2048_HD uint32_t softmax_select(const float lg[4], uint32_t mw, bool has_mask, bool greedy, double u, float p[4]) {
+    const bool m[4] = {(mw & 0xFFu) != 0u, ((mw >> 8) & 0xFFu) != 0u, ((mw >> 16) & 0xFFu) != 0u, (mw >> 24) != 0u};
+    float l[4];
+    for (int k = 0; k < 4; k++) l[k] = (!has_mask || m[k]) ? lg[k] : -1e9f;
+    const float mx = fmaxf(fmaxf(l[0], l[1]), fmaxf(l[2], l[3]));
+    float e[4];
+    for (int k = 0; k < 4; k++) e[k] = expf(l[k] - mx);
+    const float s = ((e[0] + e[1]) + e[2]) + e[3];
+    for (int k = 0; k < 4; k++) p[k] = e[k] / s;
+    uint32_t act = 0;
+    if (greedy) {
+        float best = has_mask ? p[0] * (float)m[0] : p[0];
+        for (int k = 1; k < 4; k++) {
+            const float q = has_mask ? p[k] * (float)m[k] : p[k];
+            if (q > best) {
+                best = q;
+                act = (uint32_t)k;
+            }
+        }
+    } else {
+        double cdf[4], acc = 0.0;
+        for (int k = 0; k < 4; k++) {
+            acc += (double)p[k];
+            cdf[k] = acc;
+        }
+        for (int k = 0; k < 4; k++) act += (cdf[k] / cdf[3] <= u) ? 1u : 0u;
+    }
+    return act;
 }
 
 // Philox spawn: r.x picks the cell (Lemire, no rejection), r.y < 0.9 * 2**32 picks the 2

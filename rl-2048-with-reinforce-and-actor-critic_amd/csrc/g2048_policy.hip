@@ -1,0 +1,383 @@
+// g2048_policy.hip -- fused policy forward + action selection for the rollout (part of libg2048.so).
+//
+// Replaces, for the batched rollout, the chain forward_logits (src/MLP.py:159-196) -> logits_to_probs
+// (:139-156) -> select_action's choice (src/reinforce_agent.py:178-190) for the reference's 2-hidden-layer MLP
+// (obs width 16: "log2" / "raw"; hidden sizes <= 256; ReLU or Sigmoid; 4 actions).  One wave takes 32 boards:
+//   * the obs are built in registers from the bitboards (no obs buffer round trip through HBM);
+//   * layer 1 (H1^T = W1^T X^T) and layer 2 (H2^T = W2^T H1^T) run on v_mfma_f32_32x32x2_f32 -- exact fp32,
+//     a k-ordered fmaf chain (cdna_hip_programming.md "FP32-input MFMA") -- with hidden units on the MFMA rows
+//     and boards on its columns, so each layer-1 accumulator tile is, register for register, the B operand of a
+//     layer-2 k-step (k order permuted consistently on both operands; no LDS round trip);
+//   * bias + activation are applied to the accumulators in registers; layer 3 (4 outputs) is VALU fmaf over each
+//     layer-2 tile as it completes, the two lane halves' partial sums are added by a cross-lane swap;
+//   * the action is chosen by the same device code as g2048_sample (softmax_select in g2048_core.h).
+// Weights are pre-packed (g2048_policy_pack) in MFMA fragment order, so every A fragment is one coalesced load
+// (the packed net, <= 290 KB, stays L2-resident).  Hidden sizes are zero-padded to whole 32-unit tiles, which is
+// exact: a padded unit's outgoing weights are zero.
+#include <hip/hip_runtime.h>
+
+
+#include "g2048.h"
+#include "g2048_core.h"
+
+using namespace g2048;
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kPolBlock = 256;   // 4 waves; two workgroups per CU (2 waves per SIMD)
+
+// packed layout (floats), nt1 / nt2 = hidden tiles of 32:
+//   w1f [nt1][8][64]         lane l of k-step s: W1[2s + (l>>5)][32t + (l&31)]
+//   b1p [nt1][2][16]         half h, register r: b1[32t + row(r, h)]
+//   w2f [nt2][nt1][4][64][4] lane l, k-step (t, r = 4q + u) at [o][t][q][l][u]: W2[32t + row(r, l>>5)][32o + (l&31)]
+//                            (one 16-B load per lane fetches four consecutive k-steps)
+//   b2p [nt2][2][16]
+//   w3p [nt2][2][16][4]      W3[32o + row(r, h)][a]
+//   b3  [4]
+// row(r, h) = (r & 3) + 8 (r >> 2) + 4 h: the hidden unit held by accumulator register r in lane half h.
+__host__ __device__ inline int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+struct PolLayout {
+    int64_t w1f, b1p, w2f, b2p, w3p, b3, total;
+};
+
+__host__ __device__ constexpr PolLayout pol_layout(int nt1, int nt2) {
+    PolLayout L{};
+    L.w1f = 0;
+    L.b1p = L.w1f + (int64_t)nt1 * 8 * 64;
+    L.w2f = L.b1p + (int64_t)nt1 * 32;
+    L.b2p = L.w2f + (int64_t)nt2 * nt1 * 16 * 64;
+    L.w3p = L.b2p + (int64_t)nt2 * 32;
+    L.b3 = L.w3p + (int64_t)nt2 * 32 * 4;
+    L.total = L.b3 + 4;
+    return L;
+}
+
+struct PackArgs {
+    const float *W1, *b1, *W2, *b2, *W3, *b3;
+    int h1, h2, nt1, nt2;
+    float* out;
+    int64_t total;
+};
+
+// one thread per packed float
+__global__ void __launch_bounds__(256) pack_kernel(PackArgs a) {
+    const PolLayout L = pol_layout(a.nt1, a.nt2);
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.total; q += (int64_t)gridDim.x * blockDim.x) {
+        float v = 0.0f;
+        if (q < L.b1p) {
+            const int64_t x = q - L.w1f;
+            const int lane = (int)(x & 63), s = (int)((x >> 6) & 7), t = (int)(x >> 9);
+            const int k = 2 * s + (lane >> 5), j = 32 * t + (lane & 31);
+            v = j < a.h1 ? a.W1[k * a.h1 + j] : 0.0f;
+        } else if (q < L.w2f) {
+            const int64_t x = q - L.b1p;
+            const int r = (int)(x & 15), h = (int)((x >> 4) & 1), t = (int)(x >> 5);
+            const int j = 32 * t + acc_row(r, h);
+            v = j < a.h1 ? a.b1[j] : 0.0f;
+        } else if (q < L.b2p) {
+            const int64_t x = q - L.w2f;
+            const int u = (int)(x & 3), lane = (int)((x >> 2) & 63), r = 4 * (int)((x >> 8) & 3) + u;
+            const int64_t tt = x >> 10;
+            const int t = (int)(tt % a.nt1), o = (int)(tt / a.nt1);
+            const int k = 32 * t + acc_row(r, lane >> 5), j = 32 * o + (lane & 31);
+            v = (k < a.h1 && j < a.h2) ? a.W2[(int64_t)k * a.h2 + j] : 0.0f;
+        } else if (q < L.w3p) {
+            const int64_t x = q - L.b2p;
+            const int r = (int)(x & 15), h = (int)((x >> 4) & 1), o = (int)(x >> 5);
+            const int j = 32 * o + acc_row(r, h);
+            v = j < a.h2 ? a.b2[j] : 0.0f;
+        } else if (q < L.b3) {
+            const int64_t x = q - L.w3p;
+            const int act = (int)(x & 3), r = (int)((x >> 2) & 15), h = (int)((x >> 6) & 1), o = (int)(x >> 7);
+            const int j = 32 * o + acc_row(r, h);
+            v = j < a.h2 ? a.W3[j * 4 + act] : 0.0f;
+        } else {
+            v = a.b3[q - L.b3];
+        }
+        a.out[q] = v;
+    }
+}
+
+struct PolArgs {
+    const float* net;
+    const uint64_t* boards;
+    const uint8_t* active;   // status (bit 0) or NULL
+    uint64_t *rs, *inc, *buf;
+    uint64_t key;
+    const uint64_t* lane_seed;
+    const uint32_t* counter;
+    float* probs_out;
+    float* logits_out;
+    uint8_t* actions;
+    float obs_scale;
+    uint32_t n;
+    int use_mask, greedy;
+};
+
+template <int ACT>
+__device__ __forceinline__ float activate(float z) {
+    if constexpr (ACT == 0) return fmaxf(z, 0.0f);
+    else return 1.0f / (1.0f + expf(-z));
+}
+
+template <int OBS>
+__device__ __forceinline__ float obs_value(uint64_t b, int cell, float scale) {
+    const uint32_t e = (uint32_t)(b >> (4 * cell)) & 15u;
+    if constexpr (OBS == G2048_OBS_LOG2) return (float)e * scale;
+    else return e ? (float)(1u << e) : 0.0f;
+}
+
+// Waves per SIMD: 2 while the layer-1 activations (16 x NT1 registers) leave room; the 256-unit first layer
+// (128 registers of activations + the layer-2 A fragments in flight) takes the whole 512-register file.
+template <int NT1>
+constexpr int pol_waves_per_simd() { return NT1 >= 8 ? 1 : 2; }
+
+template <int NT1, int NT2, int ACT, int OBS, int RNG>
+__global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) policy_kernel(PolArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    constexpr PolLayout L = pol_layout(NT1, NT2);
+    // the small tensors (layer-1 fragments, biases, layer 3: <= 22.5 KB) are staged in LDS once per workgroup;
+    // the layer-2 fragments (the bulk, up to 256 KB) stream from L2 with an explicit one-k-tile-ahead prefetch
+    constexpr int kSmall = (int)(L.w2f - L.w1f) + (int)(L.total - L.b2p);
+    __shared__ float sm[kSmall];
+    for (int k = threadIdx.x; k < kSmall; k += kPolBlock)
+        sm[k] = k < (int)L.w2f ? a.net[k] : a.net[L.b2p + (k - (int)L.w2f)];
+    __syncthreads();
+    const float* w1f = sm;
+    const float* b1p = sm + L.b1p;
+    const float* b2p = sm + L.w2f;
+    const float* w3p = sm + L.w2f + (L.w3p - L.b2p);
+    const float* b3 = sm + L.w2f + (L.b3 - L.b2p);
+    const float4* __restrict__ w2q = reinterpret_cast<const float4*>(a.net + L.w2f) + lane;   // [o][t][q][64]
+    const uint32_t waves = gridDim.x * (kPolBlock / 64);
+    const uint32_t groups = (a.n + 31u) >> 5;
+    for (uint32_t gi = blockIdx.x * (kPolBlock / 64) + (threadIdx.x >> 6); gi < groups; gi += waves) {
+        const uint32_t i = gi * 32u + (uint32_t)col;            // this lane's board (both halves)
+        const uint32_t ic = i < a.n ? i : a.n - 1u;
+        const uint64_t b = a.boards[ic];
+        // first layer-2 fragments in flight while layer 1 runs
+        float4 fa[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) fa[q] = w2q[q * 64];
+        // X^T k-step s: row k = 2s + h (obs feature), column = board
+        float x[8];
+#pragma unroll
+        for (int s = 0; s < 8; s++) x[s] = obs_value<OBS>(b, 2 * s + h, a.obs_scale);
+        // layer 1: H1^T tile t (32 hidden x 32 boards), bias + activation in registers
+        float h1[NT1][16];
+#pragma unroll
+        for (int t = 0; t < NT1; t++) {
+            floatx16 acc = {};
+#pragma unroll
+            for (int s = 0; s < 8; s++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1f[(t * 8 + s) * 64 + lane], x[s], acc, 0, 0, 0);
+            const float4* bb = reinterpret_cast<const float4*>(b1p + (t * 2 + h) * 16);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 bv = bb[q];
+                h1[t][4 * q + 0] = activate<ACT>(acc[4 * q + 0] + bv.x);
+                h1[t][4 * q + 1] = activate<ACT>(acc[4 * q + 1] + bv.y);
+                h1[t][4 * q + 2] = activate<ACT>(acc[4 * q + 2] + bv.z);
+                h1[t][4 * q + 3] = activate<ACT>(acc[4 * q + 3] + bv.w);
+            }
+        }
+        // layer 2 tile by tile (A fragments of k-tile t+1 loaded while tile t's 16 MFMAs run, across tiles),
+        // each output tile folded into the 4 logits as soon as it is done
+        float lg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 1
+        for (int o = 0; o < NT2; o++) {
+            floatx16 acc = {};
+            const float4* wo = w2q + o * NT1 * 4 * 64;
+#pragma unroll
+            for (int t = 0; t < NT1; t++) {
+                float4 fb[4];
+                const float4* nx = (t + 1 < NT1) ? wo + (t + 1) * 4 * 64 : (o + 1 < NT2 ? wo + NT1 * 4 * 64 : w2q);
+#pragma unroll
+                for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, h1[t][4 * q + 0], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, h1[t][4 * q + 1], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, h1[t][4 * q + 2], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, h1[t][4 * q + 3], acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) fa[q] = fb[q];
+            }
+            const float4* bb = reinterpret_cast<const float4*>(b2p + (o * 2 + h) * 16);
+            const float4* w3 = reinterpret_cast<const float4*>(w3p + (o * 2 + h) * 64);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 bv = bb[q];
+                const float hv[4] = {activate<ACT>(acc[4 * q + 0] + bv.x), activate<ACT>(acc[4 * q + 1] + bv.y),
+                                     activate<ACT>(acc[4 * q + 2] + bv.z), activate<ACT>(acc[4 * q + 3] + bv.w)};
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const float4 wv = w3[4 * q + u];
+                    lg[0] = fmaf(hv[u], wv.x, lg[0]);
+                    lg[1] = fmaf(hv[u], wv.y, lg[1]);
+                    lg[2] = fmaf(hv[u], wv.z, lg[2]);
+                    lg[3] = fmaf(hv[u], wv.w, lg[3]);
+                }
+            }
+        }
+        // the two lane halves hold different hidden units of the same board
+#pragma unroll
+        for (int k = 0; k < 4; k++) lg[k] = (lg[k] + __shfl_xor(lg[k], 32, 64)) + b3[k];
+        if (h == 0 && i < a.n && (!a.active || (a.active[i] & 1u))) {
+            if (a.logits_out) reinterpret_cast<float4*>(a.logits_out)[i] = make_float4(lg[0], lg[1], lg[2], lg[3]);
+            const uint32_t mw = a.use_mask ? ((action_mask(b) & 1u) | ((action_mask(b) & 2u) << 7) |
+                                              ((action_mask(b) & 4u) << 14) | ((action_mask(b) & 8u) << 21))
+                                           : 0x01010101u;
+            double u = 0.0;
+            if (!a.greedy) {
+                if constexpr (RNG == G2048_RNG_PCG64) {
+                    Pcg64 g;
+                    const ulonglong2 sv = reinterpret_cast<const ulonglong2*>(a.rs)[i];
+                    const ulonglong2 iv = reinterpret_cast<const ulonglong2*>(a.inc)[i];
+                    const uint64_t bf = a.buf[i];
+                    g.s_lo = sv.x; g.s_hi = sv.y; g.i_lo = iv.x; g.i_hi = iv.y;
+                    g.has_uint32 = (uint32_t)(bf >> 32); g.uinteger = (uint32_t)bf;
+                    u = pcg_random(g);
+                    reinterpret_cast<ulonglong2*>(a.rs)[i] = make_ulonglong2(g.s_lo, g.s_hi);
+                } else {
+                    const uint64_t sd = a.lane_seed ? a.lane_seed[i] : (uint64_t)i;
+                    U4 c{(uint32_t)sd, (uint32_t)(sd >> 32), a.counter ? a.counter[i] : 0u, 3u};
+                    const U4 r = philox4x32(c, (uint32_t)a.key, (uint32_t)(a.key >> 32));
+                    const uint64_t xx = ((uint64_t)r.x << 32) | r.y;
+                    u = (double)(xx >> 11) * (1.0 / 9007199254740992.0);
+                }
+            }
+            float p[4];
+            const uint32_t act = softmax_select(lg, mw, a.use_mask != 0, a.greedy != 0, u, p);
+            if (a.probs_out) reinterpret_cast<float4*>(a.probs_out)[i] = make_float4(p[0], p[1], p[2], p[3]);
+            a.actions[i] = (uint8_t)act;
+        }
+    }
+}
+
+template <int NT1, int NT2, int ACT, int OBS>
+void launch_pol_rng(const PolArgs& a, int rng, int grid, hipStream_t s) {
+    if (rng == G2048_RNG_PCG64)
+        hipLaunchKernelGGL((policy_kernel<NT1, NT2, ACT, OBS, G2048_RNG_PCG64>), dim3(grid), dim3(kPolBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL((policy_kernel<NT1, NT2, ACT, OBS, G2048_RNG_PHILOX>), dim3(grid), dim3(kPolBlock), 0, s, a);
+}
+
+template <int NT1, int NT2, int ACT>
+void launch_pol_obs(const PolArgs& a, int obs, int rng, int grid, hipStream_t s) {
+    if (obs == G2048_OBS_LOG2) launch_pol_rng<NT1, NT2, ACT, G2048_OBS_LOG2>(a, rng, grid, s);
+    else launch_pol_rng<NT1, NT2, ACT, G2048_OBS_RAW>(a, rng, grid, s);
+}
+
+template <int NT1, int NT2>
+void launch_pol_act(const PolArgs& a, int act, int obs, int rng, int grid, hipStream_t s) {
+    if (act == G2048_ACT_RELU) launch_pol_obs<NT1, NT2, 0>(a, obs, rng, grid, s);
+    else launch_pol_obs<NT1, NT2, 1>(a, obs, rng, grid, s);
+}
+
+template <int NT1>
+void launch_pol_nt2(const PolArgs& a, int nt2, int act, int obs, int rng, int grid, hipStream_t s) {
+    switch (nt2) {
+        case 1: launch_pol_act<NT1, 1>(a, act, obs, rng, grid, s); break;
+        case 2: launch_pol_act<NT1, 2>(a, act, obs, rng, grid, s); break;
+        case 4: launch_pol_act<NT1, 4>(a, act, obs, rng, grid, s); break;
+        default: launch_pol_act<NT1, 8>(a, act, obs, rng, grid, s); break;
+    }
+}
+
+int tiles_for(int hsize) {   // hidden units -> 32-unit tiles, rounded up to 1, 2, 4 or 8
+    const int t = (hsize + 31) / 32;
+    return t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : 8;
+}
+
+}  // namespace
+
+namespace g2048_internal {
+int set_error(int code, const char* msg);   // g2048.hip: the g2048_last_error() string
+}  // namespace g2048_internal
+
+namespace {
+int pfail(int code, const char* msg) { return g2048_internal::set_error(code, msg); }
+}  // namespace
+
+extern "C" {
+
+int64_t g2048_policy_packed_size(int h1, int h2) {
+    if (h1 < 1 || h1 > 256 || h2 < 1 || h2 > 256) return -1;
+    return pol_layout(tiles_for(h1), tiles_for(h2)).total;
+}
+
+int g2048_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                      const float* b3, int in_dim, int h1, int h2, float* packed, int64_t packed_len, void* stream) {
+    if (in_dim != 16) return pfail(G2048_EINVAL, "fused policy: obs width must be 16 (log2 / raw obs)");
+    const int64_t need = g2048_policy_packed_size(h1, h2);
+    if (need < 0) return pfail(G2048_EINVAL, "fused policy: hidden sizes must be in 1..256");
+    if (!W1 || !b1 || !W2 || !b2 || !W3 || !b3 || !packed) return pfail(G2048_EINVAL, "fused policy: NULL weight");
+    if (packed_len < need) return pfail(G2048_EINVAL, "fused policy: packed buffer too small");
+    PackArgs a{W1, b1, W2, b2, W3, b3, h1, h2, tiles_for(h1), tiles_for(h2), packed, need};
+    const int grid = (int)((need + 255) / 256 < 4096 ? (need + 255) / 256 : 4096);
+    hipLaunchKernelGGL(pack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return pfail(G2048_EHIP, hipGetErrorString(e));
+    return G2048_OK;
+}
+
+int g2048_policy(const float* packed, int h1, int h2, int activation, const uint64_t* boards, const uint8_t* active,
+                 int obs_mode, float obs_scale, int use_mask, int greedy, int rng_mode, uint64_t* rng_state,
+                 const uint64_t* rng_inc, const uint64_t* rng_buf, uint64_t philox_key, const uint64_t* lane_seed,
+                 const uint32_t* counter, float* probs_out, float* logits_out, uint8_t* actions, int64_t n,
+                 void* stream) {
+    if (n < 0 || n > (int64_t)0xFFFFFFE0) return pfail(G2048_EINVAL, "n out of range");
+    if (n == 0) return G2048_OK;
+    if (!packed || !boards || !actions) return pfail(G2048_EINVAL, "packed / boards / actions is NULL");
+    if (g2048_policy_packed_size(h1, h2) < 0) return pfail(G2048_EINVAL, "fused policy: hidden sizes must be in 1..256");
+    if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
+        return pfail(G2048_EINVAL, "Unsupported activation");
+    if (obs_mode != G2048_OBS_LOG2 && obs_mode != G2048_OBS_RAW)
+        return pfail(G2048_EINVAL, "fused policy: obs_mode must be log2 or raw");
+    if (rng_mode != G2048_RNG_PCG64 && rng_mode != G2048_RNG_PHILOX) return pfail(G2048_EINVAL, "Unsupported rng_mode");
+    if (!greedy && rng_mode == G2048_RNG_PCG64 && (!rng_state || !rng_inc || !rng_buf))
+        return pfail(G2048_EINVAL, "PCG64 sampling needs rng_state / rng_inc / rng_buf");
+    PolArgs a;
+    a.net = packed;
+    a.boards = boards;
+    a.active = active;
+    a.rs = rng_state;
+    a.inc = const_cast<uint64_t*>(rng_inc);
+    a.buf = const_cast<uint64_t*>(rng_buf);
+    a.key = philox_key;
+    a.lane_seed = lane_seed;
+    a.counter = counter;
+    a.probs_out = probs_out;
+    a.logits_out = logits_out;
+    a.actions = actions;
+    a.obs_scale = obs_scale;
+    a.n = (uint32_t)n;
+    a.use_mask = use_mask;
+    a.greedy = greedy;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0) cus = c;
+    }
+    const int64_t groups = (n + 31) / 32, waves_per_block = kPolBlock / 64;
+    int64_t grid = (groups + waves_per_block - 1) / waves_per_block;
+    const int nt1 = tiles_for(h1), nt2 = tiles_for(h2);
+    const int per_cu = nt1 >= 8 ? 1 : 2;   // pol_waves_per_simd
+    if (grid > per_cu * cus) grid = per_cu * cus;   // persistent
+    hipStream_t s = (hipStream_t)stream;
+    switch (nt1) {
+        case 1: launch_pol_nt2<1>(a, nt2, activation, obs_mode, rng_mode, (int)grid, s); break;
+        case 2: launch_pol_nt2<2>(a, nt2, activation, obs_mode, rng_mode, (int)grid, s); break;
+        case 4: launch_pol_nt2<4>(a, nt2, activation, obs_mode, rng_mode, (int)grid, s); break;
+        default: launch_pol_nt2<8>(a, nt2, activation, obs_mode, rng_mode, (int)grid, s); break;
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return pfail(G2048_EHIP, hipGetErrorString(e));
+    return G2048_OK;
+}
+
+}  // extern "C"

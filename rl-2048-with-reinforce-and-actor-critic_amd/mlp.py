@@ -104,9 +104,10 @@ def forward_logits(params: dict[str, list[torch.Tensor]], x: torch.Tensor, activ
     act = x.to(torch.float32)
     acts, pres = ([act], []) if keep_cache else (None, None)
     for i, (W, b) in enumerate(zip(Ws, bs)):
-        if not keep_cache and activation_mode == "ReLU" and act.dim() == 2 and i < len(Ws) - 1:
+        if not keep_cache and activation_mode == "ReLU" and act.dim() == 2 and i < len(Ws) - 1 and \
+                not (torch.is_grad_enabled() and (act.requires_grad or W.requires_grad or b.requires_grad)):
             # rollout / inference: bias + ReLU in the hipBLASLt epilogue (no separate pass over the [n, 256]
-            # activations; same fp32 values as relu(addmm))
+            # activations; same fp32 values as relu(addmm)); it has no autograd formula, so not under grad
             act = torch._addmm_activation(b, act, W, use_gelu=False)
             continue
         z = torch.addmm(b, act, W) if act.dim() == 2 else act @ W + b

@@ -125,18 +125,20 @@ class VecGame2048Env:
         return self._obs_view(), {"score": self.score, "board": self.board}
 
     def step_into(self, actions: torch.Tensor, reward: torch.Tensor | None = None, flags: torch.Tensor | None = None,
-                  prev_board: torch.Tensor | None = None) -> None:
-        """Launch one step writing reward/flags (and the pre-step board) into caller tensors (trajectory rows)."""
+                  prev_board: torch.Tensor | None = None, write_obs: bool = True) -> None:
+        """Launch one step writing reward/flags (and the pre-step board) into caller tensors (trajectory rows).
+        write_obs=False skips the obs buffer (its consumer reads the boards itself, e.g. g2048_policy)."""
         if actions.dtype != torch.uint8 or actions.device != self.device or actions.numel() != self.n:
             raise ValueError("actions must be a uint8 tensor of num_envs elements on the env device")
         out = self._out
-        if reward is not None or flags is not None or prev_board is not None:
+        if reward is not None or flags is not None or prev_board is not None or not write_obs:
             out = L.StepOut(L.ptr(reward if reward is not None else self.reward),
-                            L.ptr(flags if flags is not None else self.flags), L.ptr(self.mask), L.ptr(self.obs),
+                            L.ptr(flags if flags is not None else self.flags), L.ptr(self.mask),
+                            L.ptr(self.obs) if write_obs else None,
                             L.ptr(self.merged), L.ptr(prev_board if prev_board is not None else self.prev_board))
         if torch.cuda.current_device() != self.device.index:
             with torch.cuda.device(self.device):
-                return self.step_into(actions, reward, flags, prev_board)
+                return self.step_into(actions, reward, flags, prev_board, write_obs)
         L.check(self._lib.g2048_step(ctypes.byref(self._lanes), L.ptr(actions), ctypes.byref(self._cfg),
                                      ctypes.byref(out), self.rng_mode, self.philox_key, int(self.auto_reset),
                                      self.reset_stride, self.n, L.stream_handle(self.device)))

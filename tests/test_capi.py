@@ -22,13 +22,14 @@ def L():
 
 def _declared_functions():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(g2048_\w+)\s*\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(g2048_\w+)\s*\(", text, flags=re.M)))
 
 
 def test_header_declares_expected_api():
     assert _declared_functions() == sorted([
         "g2048_abi_version", "g2048_last_error", "g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step",
-        "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries"])
+        "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_packed_size",
+        "g2048_policy_pack", "g2048_policy"])
 
 
 def test_library_exports_every_declared_symbol(L):
@@ -79,6 +80,20 @@ def test_argument_validation_without_gpu(L):
     assert rc == L.G2048_EINVAL and b"reward mode" in lib.g2048_last_error()
     with pytest.raises(ValueError):
         L.check(L.G2048_EINVAL)
+    # fused policy: shape / mode validation (no launch)
+    assert lib.g2048_policy_packed_size(256, 256) == 8 * 8 * 64 + 8 * 32 + 8 * 8 * 16 * 64 + 8 * 32 + 8 * 128 + 4
+    assert lib.g2048_policy_packed_size(0, 16) == -1 and lib.g2048_policy_packed_size(16, 300) == -1
+    p = ctypes.c_void_p(8)
+    assert lib.g2048_policy_pack(p, p, p, p, p, p, 272, 32, 32, p, 1 << 20, None) == L.G2048_EINVAL
+    assert b"obs width" in lib.g2048_last_error()
+    assert lib.g2048_policy_pack(p, p, p, p, p, p, 16, 32, 32, p, 10, None) == L.G2048_EINVAL
+    args = [p, 32, 32, L.ACT_RELU, p, None, L.OBS_ONEHOT, 1.0, 1, 0, L.RNG_PHILOX, None, None, None, 0, None, None,
+            None, None, p, 4, None]
+    assert lib.g2048_policy(*args) == L.G2048_EINVAL and b"obs_mode" in lib.g2048_last_error()
+    args[6], args[3] = L.OBS_LOG2, 7
+    assert lib.g2048_policy(*args) == L.G2048_EINVAL and b"activation" in lib.g2048_last_error()
+    args[3], args[10] = L.ACT_RELU, L.RNG_PCG64
+    assert lib.g2048_policy(*args) == L.G2048_EINVAL and b"PCG64" in lib.g2048_last_error()
 
 
 def test_config_validation_messages():

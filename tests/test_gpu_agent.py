@@ -39,13 +39,13 @@ def test_forward_matches_reference_mlp(golden_dir):
             np.testing.assert_allclose(pr, d[f"{name}__probs"], rtol=1e-5, atol=1e-7)
 
 
-def _agent(obs_mode="log2", hidden=(32, 16), act="ReLU", **acfg):
+def _agent(obs_mode="log2", hidden=(32, 16), act="ReLU", use_action_mask=True, **acfg):
     from rl2048_amd import Game2048EnvConfig
     from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
     from rl2048_amd.mlp import MLPConfig
 
     env_cfg = Game2048EnvConfig(obs_mode=obs_mode, obs_log2_scale=0.0625, reward_mode="log2", base_reward_scale=0.5,
-                                max_steps=300)
+                                max_steps=300, use_action_mask=use_action_mask)
     return ReinforceAgent(env_cfg, MLPConfig(hidden_sizes=list(hidden), activation=act, init_distribution="HeNormal"),
                           ReinforceAgentConfig(**acfg), device=DEV)
 
@@ -54,10 +54,15 @@ def _np_params(p):
     return {k: [t.detach().cpu().numpy().copy() for t in v] for k, v in p.items()}
 
 
-def test_rollout_transitions_and_sampling_bit_exact():
+@pytest.mark.parametrize("fused,mask", [(True, True), (False, True), (True, False), (False, False)])
+def test_rollout_transitions_and_sampling_bit_exact(fused, mask):
     """rollout_batch == the reference's run_episode: same env stream (transitions replayed in the oracle env) and
-    the same policy stream (Generator.choice on the probabilities the device used)."""
-    agent = _agent()
+    the same policy stream (Generator.choice on the probabilities the device used).  fused: the g2048_policy
+    kernel (else the GEMM path + g2048_sample); mask: use_action_mask (without it the logits are not masked,
+    src/reinforce_agent.py:138-145)."""
+    agent = _agent(use_action_mask=mask)
+    agent.use_fused_policy = fused
+    assert (agent._fused_policy_spec() is not None) == fused
     n = 48
     env_seeds = [int(s) for s in np.random.default_rng(3).integers(0, 2**62, size=n)]
     pol_seeds = [int(s) for s in np.random.default_rng(4).integers(0, 2**62, size=n)]
@@ -68,7 +73,8 @@ def test_rollout_transitions_and_sampling_bit_exact():
     probs = batch.probs.cpu().numpy()
     boards = batch.boards.cpu().numpy().view(np.uint64)
     for i in range(n):
-        env = O.Env(obs_mode="log2", obs_log2_scale=0.0625, reward_mode="log2", base_reward_scale=0.5, max_steps=300)
+        env = O.Env(obs_mode="log2", obs_log2_scale=0.0625, reward_mode="log2", base_reward_scale=0.5, max_steps=300,
+                    use_action_mask=mask)
         env.reset(env_seeds[i])
         pr = O.PCG64(pol_seeds[i])
         total = 0.0
@@ -84,8 +90,10 @@ def test_rollout_transitions_and_sampling_bit_exact():
         assert int(batch.max_tile[i]) == env.max_tile_seen
 
 
-def test_rollout_probs_match_numpy_softmax():
+@pytest.mark.parametrize("fused", [True, False])
+def test_rollout_probs_match_numpy_softmax(fused):
     agent = _agent()
+    agent.use_fused_policy = fused
     batch = agent.rollout_batch(list(range(16)), list(range(100, 116)), record_probs=True)
     from rl2048_amd.mlp import forward_logits
 

@@ -1,0 +1,150 @@
+"""GPU: the fused policy kernel (g2048_policy) against the GEMM path it replaces in the rollout.
+
+* logits: g2048_policy's fp32 MFMA forward vs forward_logits (hipBLASLt GEMMs) on the same boards and weights,
+  within fp32 summation-order error (1e-5 relative to the logits' scale), for hidden sizes that fill, pad and
+  under-fill the 32-unit tiles, both activations and both 16-wide obs modes;
+* choice: the fused kernel's probabilities and actions equal g2048_sample run on the fused kernel's own logits with
+  the same RNG state (bit-exact), for PCG64 / Philox / greedy, with and without the action mask;
+* inactive lanes (status bit 0 clear) are left untouched; n not a multiple of the 32-board group.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _boards(n, seed):
+    g = np.random.default_rng(seed)
+    e = g.integers(1, 13, size=(n, 16))
+    e[g.random((n, 16)) < 0.4] = 0
+    b = np.zeros(n, dtype=np.uint64)
+    for c in range(16):
+        b |= e[:, c].astype(np.uint64) << np.uint64(4 * c)
+    return torch.from_numpy(b.view(np.int64)).to(DEV)
+
+
+def _params(h1, h2, seed):
+    g = torch.Generator().manual_seed(seed)
+    shapes = [(16, h1), (h1, h2), (h2, 4)]
+    W = [(torch.randn(*s, generator=g) * (2.0 / s[0]) ** 0.5).to(DEV) for s in shapes]
+    b = [(torch.randn(s[1], generator=g) * 0.1).to(DEV) for s in shapes]
+    return {"W": W, "b": b}
+
+
+def _pack(L, lib, p, h1, h2):
+    size = int(lib.g2048_policy_packed_size(h1, h2))
+    packed = torch.empty(size, dtype=torch.float32, device=DEV)
+    w = [p["W"][0], p["b"][0], p["W"][1], p["b"][1], p["W"][2], p["b"][2]]
+    L.check(lib.g2048_policy_pack(*[L.ptr(t.contiguous()) for t in w], 16, h1, h2, L.ptr(packed), size,
+                                  L.stream_handle(DEV)))
+    return packed
+
+
+def _pcg(L, lib, n, seed):
+    seeds = torch.arange(n, dtype=torch.int64, device=DEV) + seed
+    st = torch.empty(2 * n, dtype=torch.int64, device=DEV)
+    inc = torch.empty(2 * n, dtype=torch.int64, device=DEV)
+    buf = torch.empty(n, dtype=torch.int64, device=DEV)
+    L.check(lib.g2048_seed_pcg64(L.ptr(seeds), L.ptr(st), L.ptr(inc), L.ptr(buf), n, L.stream_handle(DEV)))
+    return seeds, st, inc, buf
+
+
+@pytest.mark.parametrize("h1,h2,act,obs", [(256, 256, "ReLU", "log2"), (32, 16, "Sigmoid", "raw"),
+                                           (100, 60, "ReLU", "log2"), (256, 32, "ReLU", "raw"),
+                                           (64, 256, "Sigmoid", "log2"), (1, 1, "ReLU", "log2"),
+                                           (128, 128, "Sigmoid", "log2")])
+def test_fused_logits_match_gemm_path(h1, h2, act, obs):
+    from rl2048_amd import _lib as L
+    from rl2048_amd.mlp import forward_logits
+
+    lib = L.lib()
+    L.ensure_device(DEV)
+    n = 1000                                  # not a multiple of 32
+    boards = _boards(n, h1 * 7 + h2)
+    p = _params(h1, h2, h1 + 31 * h2)
+    packed = _pack(L, lib, p, h1, h2)
+    code = {"log2": L.OBS_LOG2, "raw": L.OBS_RAW}[obs]
+    x = torch.empty(n, 16, dtype=torch.float32, device=DEV)
+    L.check(lib.g2048_obs(L.ptr(boards), code, 0.0625, L.ptr(x), None, n, L.stream_handle(DEV)))
+    ref = forward_logits(p, x, act, keep_cache=False)[0]
+    logits = torch.full((n, 4), float("nan"), device=DEV)
+    actions = torch.empty(n, dtype=torch.uint8, device=DEV)
+    a = {"ReLU": L.ACT_RELU, "Sigmoid": L.ACT_SIGMOID}[act]
+    L.check(lib.g2048_policy(L.ptr(packed), h1, h2, a, L.ptr(boards), None, code, 0.0625, 1, 1, L.RNG_PHILOX, None,
+                             None, None, 0, None, None, None, L.ptr(logits), L.ptr(actions), n,
+                             L.stream_handle(DEV)))
+    torch.cuda.synchronize()
+    scale = float(ref.abs().max()) + 1e-30
+    err = float((logits - ref).abs().max()) / scale
+    assert err < 1e-5, (h1, h2, act, obs, err)
+
+
+@pytest.mark.parametrize("rng,greedy,mask", [("pcg64", 0, 1), ("pcg64", 0, 0), ("philox", 0, 1), ("pcg64", 1, 1),
+                                             ("philox", 1, 0)])
+def test_fused_choice_equals_sample_kernel(rng, greedy, mask):
+    from rl2048_amd import _lib as L
+
+    lib = L.lib()
+    L.ensure_device(DEV)
+    n, h1, h2 = 777, 256, 256
+    boards = _boards(n, 5)
+    p = _params(h1, h2, 9)
+    packed = _pack(L, lib, p, h1, h2)
+    seeds, st, inc, buf = _pcg(L, lib, n, 1234)
+    counter = torch.arange(n, dtype=torch.int32, device=DEV) * 3
+    status = torch.ones(n, dtype=torch.uint8, device=DEV)
+    status[::7] = 0                            # inactive lanes are left untouched
+    rmode = L.RNG_PCG64 if rng == "pcg64" else L.RNG_PHILOX
+    key = 0x1234ABCD5678
+    st2 = st.clone()
+    logits = torch.empty(n, 4, device=DEV)
+    probs = torch.full((n, 4), -1.0, device=DEV)
+    actions = torch.full((n,), 9, dtype=torch.uint8, device=DEV)
+    L.check(lib.g2048_policy(L.ptr(packed), h1, h2, L.ACT_RELU, L.ptr(boards), L.ptr(status), L.OBS_LOG2, 0.0625,
+                             mask, greedy, rmode, L.ptr(st), L.ptr(inc), L.ptr(buf), key, L.ptr(seeds),
+                             L.ptr(counter), L.ptr(probs), L.ptr(logits), L.ptr(actions), n, L.stream_handle(DEV)))
+    # the same choice on the fused kernel's own logits through g2048_sample
+    mk = torch.empty(n, 4, dtype=torch.int8, device=DEV)
+    x = torch.empty(n, 16, dtype=torch.float32, device=DEV)
+    L.check(lib.g2048_obs(L.ptr(boards), L.OBS_LOG2, 0.0625, L.ptr(x), L.ptr(mk), n, L.stream_handle(DEV)))
+    probs2 = torch.full((n, 4), -1.0, device=DEV)
+    actions2 = torch.full((n,), 9, dtype=torch.uint8, device=DEV)
+    L.check(lib.g2048_sample(L.ptr(logits), L.ptr(mk) if mask else None, L.ptr(status), greedy, rmode, L.ptr(st2),
+                             L.ptr(inc), L.ptr(buf), key, L.ptr(seeds), L.ptr(counter), L.ptr(probs2),
+                             L.ptr(actions2), n, L.stream_handle(DEV)))
+    torch.cuda.synchronize()
+    act = status.bool()
+    assert torch.equal(actions, actions2)
+    assert torch.equal(probs, probs2)
+    assert torch.equal(st, st2)                # the PCG64 streams advanced identically
+    assert bool((actions[~act] == 9).all()) and bool((probs[~act] == -1.0).all())
+    assert bool((actions[act] < 4).all())
+    if mask:                                   # a masked action is never chosen (when any action is valid)
+        m = mk.bool()
+        chosen = m[torch.arange(n, device=DEV), actions.long().clamp(max=3)]
+        assert bool((chosen | ~m.any(1) | ~act).all())
+
+
+def test_agent_packed_cache_follows_updates():
+    """The agent re-packs after an update / in-place edit, so the fused rollout always uses the current actor."""
+    from rl2048_amd import Game2048EnvConfig
+    from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
+    from rl2048_amd.mlp import MLPConfig
+
+    agent = ReinforceAgent(Game2048EnvConfig(max_steps=50), MLPConfig(hidden_sizes=[64, 32]),
+                           ReinforceAgentConfig(optimizer="adam", learning_rate=1e-2), device=DEV)
+    spec = agent._fused_policy_spec()
+    assert spec == (64, 32, 1 if agent.mlp_config.activation == "Sigmoid" else 0)
+    p0 = agent._packed_policy(spec).clone()
+    batch = agent.rollout_batch(list(range(8)), list(range(8)))
+    agent.update_from_batch(batch)
+    p1 = agent._packed_policy(spec).clone()
+    assert not torch.equal(p0, p1)
+    with torch.no_grad():
+        agent.params["b"][2].add_(1.0)         # in-place edit of the actor
+    p2 = agent._packed_policy(spec)
+    assert not torch.equal(p1, p2)

@@ -5,4 +5,4 @@ set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG="$ROOT/rl-2048-with-reinforce-and-actor-critic_amd"
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DG2048_DIAG=1 -shared -fPIC -I"$ROOT/include" \
-  -I"$PKG/csrc" -o "$ROOT/tools/libg2048_diag.so" "$PKG/csrc/g2048.hip"
+  -I"$PKG/csrc" -o "$ROOT/tools/libg2048_diag.so" "$PKG/csrc/g2048.hip" "$PKG/csrc/g2048_policy.hip"
