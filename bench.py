@@ -35,6 +35,8 @@ sys.path.insert(0, ROOT)
 METRIC = "env steps/sec (whole node) + achieved HBM GB/s, batch=1M 4x4 boards"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 POLICY_FLOP_PER_BOARD = 2 * (16 * 256 + 256 * 256 + 256 * 4)  # 141,312: the runner-default MLP forward
+# update per sample: forward + weight / input gradients of layers 2 and 3, weight gradient of layer 1
+UPDATE_FLOP_PER_SAMPLE = POLICY_FLOP_PER_BOARD + 2 * (256 * 256 * 2 + 256 * 4 * 2 + 16 * 256)
 
 # Algorithmic bytes one g2048_step moves per board in steady state (no reset), by mode.  Reads / writes:
 #   board 8/8, action 1/-, status 1/-, step_count 4/4, max_tile 1/1, score 4/4, reward -/4, flags -/1, mask -/4
@@ -195,7 +197,7 @@ def policy_rollout_rate(torch, B: int, device, steps: int = 20, warmup: int = 5,
     def one():
         if fused:
             L.check(lib.g2048_policy(L.ptr(packed), spec[0], spec[1], spec[2], L.ptr(env.board), L.ptr(env.status),
-                                     L.OBS_LOG2, 0.0625, 1, 0, L.RNG_PCG64, L.ptr(st), L.ptr(inc), L.ptr(buf), 0,
+                                     None, L.OBS_LOG2, 0.0625, 1, 0, L.RNG_PCG64, L.ptr(st), L.ptr(inc), L.ptr(buf), 0,
                                      None, None, None, None, L.ptr(acts), B, stream))
             env.step_into(acts, write_obs=False)
         else:
@@ -218,6 +220,37 @@ def policy_rollout_rate(torch, B: int, device, steps: int = 20, warmup: int = 5,
     return {"value": steps * B / dt, "unit": "env steps/s", "boards": B, "steps": steps,
             "ms_per_step": dt / steps * 1e3, "model": "MLP 16-256-256-4 ReLU fp32 (runner.py defaults)",
             "path": path, "policy_tflops": steps * B * POLICY_FLOP_PER_BOARD / dt / 1e12}
+
+
+def train_iteration_rate(torch, device, episodes: int = 65536, repeats: int = 2) -> dict:
+    """One training iteration of configs[1] (65,536 parallel boards, REINFORCE + the runner-default MLP): the
+    batched rollout of one episode per lane (fused policy kernel + env step) and update_from_batch (batched manual
+    backprop of update_batch, fp32), timed separately; the last of `repeats` iterations after one warm-up."""
+    from rl2048_amd import Game2048EnvConfig
+    from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
+    from rl2048_amd.mlp import MLPConfig
+
+    agent = ReinforceAgent(Game2048EnvConfig(), MLPConfig(hidden_sizes=[256, 256], activation="ReLU",
+                                                          init_distribution="HeNormal"),
+                           ReinforceAgentConfig(baseline_mode="batch"), device=device)
+    out = {}
+    for rep in range(repeats + 1):
+        base = 1000 + rep * episodes
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        batch = agent.rollout_batch(list(range(base, base + episodes)), list(range(base + 7 * episodes,
+                                                                                 base + 8 * episodes)))
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        agent.update_from_batch(batch)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        samples = int(batch.lengths.sum())
+        out = {"episodes": episodes, "env_steps": samples, "longest_episode": batch.T, "rollout_s": t1 - t0,
+               "update_s": t2 - t1, "iteration_s": t2 - t0, "env_steps_per_s": samples / (t2 - t0),
+               "update_tflops": samples * UPDATE_FLOP_PER_SAMPLE / (t2 - t1) / 1e12,
+               "model": "REINFORCE, MLP 16-256-256-4 ReLU fp32, batch baseline (runner.py defaults)"}
+    return out
 
 
 # ---------------------------------------------------------------------------------------------- main
@@ -299,6 +332,7 @@ def main():
             torch.cuda.empty_cache()
             policy = policy_rollout_rate(torch, B, device)
             policy["gemm_path"] = policy_rollout_rate(torch, B, device, fused=False)
+            policy["train_iteration_configs1"] = train_iteration_rate(torch, device)
         except Exception as e:  # noqa: BLE001 -- an extra, never the headline
             policy = {"error": repr(e)}
     if world > 1:

@@ -184,12 +184,14 @@ int64_t g2048_policy_packed_size(int h1, int h2);
 int g2048_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                       const float* b3, int in_dim, int h1, int h2, float* packed, int64_t packed_len, void* stream);
 
-/* boards [n]; active [n] status bytes (bit 0 = active; NULL = all) -- inactive lanes are left untouched;
+/* boards / active / rng / counters / outputs are per lane; the call covers n entries: entry j is lane
+ * lane_index[j] (int32, NULL = lane j), so a rollout can run the net on its still-active lanes only;
+ * active: status bytes (bit 0 = active; NULL = all) -- inactive lanes are left untouched;
  * use_mask: mask the logits with the boards' action masks (Game2048.get_action_mask, src/game2048.py:95-99);
  * greedy / rng_mode / rng_* / philox_key / lane_seed / counter / probs_out / actions as in g2048_sample;
  * logits_out [n*4] may be NULL. */
 int g2048_policy(const float* packed, int h1, int h2, int activation, const uint64_t* boards, const uint8_t* active,
-                 int obs_mode, float obs_scale, int use_mask, int greedy, int rng_mode, uint64_t* rng_state,
+                 const int32_t* lane_index, int obs_mode, float obs_scale, int use_mask, int greedy, int rng_mode, uint64_t* rng_state,
                  const uint64_t* rng_inc, const uint64_t* rng_buf, uint64_t philox_key, const uint64_t* lane_seed,
                  const uint32_t* counter, float* probs_out, float* logits_out, uint8_t* actions, int64_t n,
                  void* stream);

@@ -88,8 +88,8 @@ def _declare(L):
     L.g2048_policy_packed_size.argtypes = [i32, i32]
     L.g2048_policy_packed_size.restype = i64
     L.g2048_policy_pack.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i64, vp]
-    L.g2048_policy.argtypes = [vp, i32, i32, i32, vp, vp, i32, f, i32, i32, i32, vp, vp, vp, u64, vp, vp, vp, vp, vp,
-                               i64, vp]
+    L.g2048_policy.argtypes = [vp, i32, i32, i32, vp, vp, vp, i32, f, i32, i32, i32, vp, vp, vp, u64, vp, vp, vp, vp,
+                               vp, i64, vp]
     for name in ("g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step", "g2048_obs", "g2048_move",
                  "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy"):
         getattr(L, name).restype = ctypes.c_int

@@ -10,9 +10,10 @@ Two faces over one implementation:
   trajectory buffer; ``update_from_batch(batch)`` applies exactly the update of ``update_batch`` to it.
 
 The update is the reference's per-timestep manual backprop (src/reinforce_agent.py:502-555, :639-678) restated
-as batched autograd over all valid steps: the actor's logit gradient is A_t * (onehot(a_t) - pi(.|s_t)) scaled by
-rank_w / (T_i * n) and back-propagated through the MLP (identical to summing the reference's per-step outer
-products); the critic's is the (MSE or Huber) TD gradient with the same weights.  Gradient clipping, SGD ascent /
+as one batched manual backprop over all valid steps (mlp.mlp_backward_): the actor's logit gradient is
+A_t * (onehot(a_t) - pi(.|s_t)) scaled by rank_w / (T_i * n) and back-propagated through the MLP (identical to
+summing the reference's per-step outer products; the weight gradients are split-K batched GEMMs); the critic's is
+the (MSE or Huber) TD gradient with the same weights.  Gradient clipping, SGD ascent /
 descent and Adam follow :558-582, :719-770, :835-861.
 
 Data parallel: when torch.distributed is initialised each rank holds a shard of the batch's episodes; rank
@@ -33,7 +34,8 @@ import torch
 from . import _lib as L
 from . import dp
 from .config import Game2048EnvConfig, obs_width
-from .mlp import (MLPConfig, encode_observation, forward_logits, init_model_params, load_model_params,
+from .mlp import (MLPConfig, encode_observation, forward_logits, init_model_params, load_model_params, mlp_backward_,
+                  mlp_forward_kept,
                   logits_to_probs, save_model_params)
 from .vec_env import VecGame2048Env
 
@@ -416,6 +418,7 @@ class ReinforceAgent:
         use_mask = bool(self.env_config.use_action_mask)
         spec = self._fused_policy_spec()
         packed = self._packed_policy(spec) if spec is not None else None
+        active_idx = None
         t = 0
         while True:
             if t == cap:
@@ -428,14 +431,19 @@ class ReinforceAgent:
                     probs = torch.cat([probs, torch.zeros(grow, n, 4, dtype=torch.float32, device=dev)])
                 cap += grow
             if spec is not None:
-                # fused forward + choice straight from the boards; the step then skips the obs buffer
+                # fused forward + choice straight from the boards, on the lanes still active at the last check
+                # (compacted every check_every steps); the step then skips the obs buffer
+                if active_idx is None or t % check_every == 0:
+                    active_idx = torch.nonzero(env.status & 1).view(-1).to(torch.int32)
+                m = int(active_idx.numel())
                 L.check(self._lib.g2048_policy(L.ptr(packed), spec[0], spec[1], spec[2], L.ptr(env.board),
-                                               L.ptr(env.status), _OBS_CODE[self.env_config.obs_mode],
+                                               L.ptr(env.status), L.ptr(active_idx) if m < n else None,
+                                               _OBS_CODE[self.env_config.obs_mode],
                                                float(self.env_config.obs_log2_scale), int(use_mask),
                                                int(use_greedy), rng_mode, L.ptr(pst), L.ptr(pinc), L.ptr(pbuf),
                                                env.philox_key ^ 0x5A5A, L.ptr(pseeds), L.ptr(env.step_count),
                                                L.ptr(probs[t]) if probs is not None else None, None,
-                                               L.ptr(actions[t]), n, self._stream))
+                                               L.ptr(actions[t]), m if m < n else n, self._stream))
                 env.step_into(actions[t], reward=rewards[t], flags=flags[t], prev_board=boards[t], write_obs=False)
             else:
                 logits = self._policy_logits(env.obs)
@@ -663,14 +671,13 @@ class ReinforceAgent:
         if c.use_critic:
             critic_g = [torch.zeros_like(p) for p in self.critic_params["W"] + self.critic_params["b"]]
             deltas = torch.empty(K, steps.N, dtype=torch.float32, device=self.device)
-            cparams = [p.detach().requires_grad_(True) for p in self.critic_params["W"] + self.critic_params["b"]]
-            nW = len(self.critic_params["W"])
-            cp = {"W": cparams[:nW], "b": cparams[nW:]}
+            ncW = len(self.critic_params["W"])
             for k in range(K):
                 for sel in self._chunks(steps.N):
                     x, _ = steps.features(sel, k)
-                    v = forward_logits(cp, x, self.mlp_config.activation, keep_cache=False)[0].view(-1)
                     with torch.no_grad():
+                        v, kept = mlp_forward_kept(self.critic_params, x, self.mlp_config.activation)
+                        v = v.view(-1)
                         hn = steps.has_next[sel]
                         vn = torch.zeros_like(v)
                         if bool(hn.any()):
@@ -689,9 +696,8 @@ class ReinforceAgent:
                         else:
                             raise ValueError(f"Unknown critic loss type: {c.critic_loss_type}")
                         g = g * step_w[sel]
-                    grads = torch.autograd.grad(v, cparams, grad_outputs=g)
-                    for acc, gr in zip(critic_g, grads):
-                        acc.add_(gr)
+                        mlp_backward_(self.critic_params, kept, self.mlp_config.activation, g.unsqueeze(1),
+                                      critic_g[:ncW], critic_g[ncW:])
             # advantages from TD errors, over all K x n "episodes"
             lane_k = (torch.arange(K, device=self.device).unsqueeze(1) * n_local + lane.unsqueeze(0)).reshape(-1)
             adv = self._advantages(deltas.reshape(-1), lane_k, K * n_local,
@@ -703,20 +709,16 @@ class ReinforceAgent:
         stats["adv_mean"] = float(adv.mean()) if adv.numel() else 0.0
         stats["adv_std"] = float(adv.std(unbiased=False)) if adv.numel() else 0.0
 
-        aparams = [p.detach().requires_grad_(True) for p in self.params["W"] + self.params["b"]]
         nW = len(self.params["W"])
-        ap = {"W": aparams[:nW], "b": aparams[nW:]}
-        for k in range(K):
-            for sel in self._chunks(steps.N):
-                x, mk = steps.features(sel, k)
-                logits = forward_logits(ap, x, self.mlp_config.activation, keep_cache=False)[0]
-                with torch.no_grad():
+        with torch.no_grad():
+            for k in range(K):
+                for sel in self._chunks(steps.N):
+                    x, mk = steps.features(sel, k)
+                    logits, kept = mlp_forward_kept(self.params, x, self.mlp_config.activation)
                     p = logits_to_probs(logits, mk)
                     onehot = torch.nn.functional.one_hot(steps.actions_k(sel, k), 4).to(torch.float32)
                     g = (onehot - p) * (adv[k, sel] * step_w[sel]).unsqueeze(1)
-                grads = torch.autograd.grad(logits, aparams, grad_outputs=g)
-                for acc, gr in zip(actor_g, grads):
-                    acc.add_(gr)
+                    mlp_backward_(self.params, kept, self.mlp_config.activation, g, actor_g[:nW], actor_g[nW:])
 
         # one fused all-reduce of actor (+ critic) gradients across ranks, before clipping
         dp.fused_all_reduce_(actor_g + (critic_g or []))

@@ -105,6 +105,7 @@ struct PolArgs {
     const float* net;
     const uint64_t* boards;
     const uint8_t* active;   // status (bit 0) or NULL
+    const int32_t* lane_index;   // entry j -> lane lane_index[j] (NULL: lane j)
     uint64_t *rs, *inc, *buf;
     uint64_t key;
     const uint64_t* lane_seed;
@@ -155,9 +156,10 @@ __global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) policy_k
     const uint32_t waves = gridDim.x * (kPolBlock / 64);
     const uint32_t groups = (a.n + 31u) >> 5;
     for (uint32_t gi = blockIdx.x * (kPolBlock / 64) + (threadIdx.x >> 6); gi < groups; gi += waves) {
-        const uint32_t i = gi * 32u + (uint32_t)col;            // this lane's board (both halves)
-        const uint32_t ic = i < a.n ? i : a.n - 1u;
-        const uint64_t b = a.boards[ic];
+        const uint32_t j = gi * 32u + (uint32_t)col;            // this lane's entry (both halves)
+        const uint32_t jc = j < a.n ? j : a.n - 1u;
+        const uint32_t i = a.lane_index ? (uint32_t)a.lane_index[jc] : jc;   // its board / lane
+        const uint64_t b = a.boards[i];
         // first layer-2 fragments in flight while layer 1 runs
         float4 fa[4];
 #pragma unroll
@@ -226,7 +228,7 @@ __global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) policy_k
         // the two lane halves hold different hidden units of the same board
 #pragma unroll
         for (int k = 0; k < 4; k++) lg[k] = (lg[k] + __shfl_xor(lg[k], 32, 64)) + b3[k];
-        if (h == 0 && i < a.n && (!a.active || (a.active[i] & 1u))) {
+        if (h == 0 && j < a.n && (!a.active || (a.active[i] & 1u))) {
             if (a.logits_out) reinterpret_cast<float4*>(a.logits_out)[i] = make_float4(lg[0], lg[1], lg[2], lg[3]);
             const uint32_t mw = a.use_mask ? ((action_mask(b) & 1u) | ((action_mask(b) & 2u) << 7) |
                                               ((action_mask(b) & 4u) << 14) | ((action_mask(b) & 8u) << 21))
@@ -326,7 +328,7 @@ int g2048_policy_pack(const float* W1, const float* b1, const float* W2, const f
 }
 
 int g2048_policy(const float* packed, int h1, int h2, int activation, const uint64_t* boards, const uint8_t* active,
-                 int obs_mode, float obs_scale, int use_mask, int greedy, int rng_mode, uint64_t* rng_state,
+                 const int32_t* lane_index, int obs_mode, float obs_scale, int use_mask, int greedy, int rng_mode, uint64_t* rng_state,
                  const uint64_t* rng_inc, const uint64_t* rng_buf, uint64_t philox_key, const uint64_t* lane_seed,
                  const uint32_t* counter, float* probs_out, float* logits_out, uint8_t* actions, int64_t n,
                  void* stream) {
@@ -345,6 +347,7 @@ int g2048_policy(const float* packed, int h1, int h2, int activation, const uint
     a.net = packed;
     a.boards = boards;
     a.active = active;
+    a.lane_index = lane_index;
     a.rs = rng_state;
     a.inc = const_cast<uint64_t*>(rng_inc);
     a.buf = const_cast<uint64_t*>(rng_buf);

@@ -119,6 +119,61 @@ def forward_logits(params: dict[str, list[torch.Tensor]], x: torch.Tensor, activ
     return act, acts, pres
 
 
+def _wgrad_(out: torch.Tensor, a: torch.Tensor, d: torch.Tensor) -> None:
+    """out += a^T d for a [m, p], d [m, q] with m >> p, q (the weight gradient of a batch): split-K as a batched
+    GEMM over row blocks plus one reduction, so the few output tiles are spread over the whole chip instead of
+    each walking all m rows (a plain addmm of these shapes gets a handful of workgroups)."""
+    m = a.shape[0]
+    P = min(128, m // 2048)
+    if P >= 2:
+        q = m // P
+        mm = P * q
+        part = torch.bmm(a[:mm].view(P, q, -1).transpose(1, 2), d[:mm].view(P, q, -1))
+        out.add_(part.sum(0))
+        if mm < m:
+            out.addmm_(a[mm:].t(), d[mm:])
+    else:
+        out.addmm_(a.t(), d)
+
+
+def mlp_forward_kept(params: dict[str, list[torch.Tensor]], x: torch.Tensor, activation_mode: str):
+    """forward_logits (src/MLP.py:159-196) keeping the layer inputs a_0..a_{L-1} for mlp_backward_."""
+    Ws, bs = params["W"], params["b"]
+    acts = [x.to(torch.float32)]
+    a = acts[0]
+    for i in range(len(Ws)):
+        z = torch.addmm(bs[i], a, Ws[i])
+        if i < len(Ws) - 1:
+            a = apply_activation(z, activation_mode)
+            acts.append(a)
+        else:
+            a = z
+    return a, acts
+
+
+def mlp_backward_(params: dict[str, list[torch.Tensor]], acts: list[torch.Tensor], activation_mode: str,
+                  grad_out: torch.Tensor, grad_W: list[torch.Tensor], grad_b: list[torch.Tensor]) -> None:
+    """The manual backprop of src/reinforce_agent.py:_backpropagation (:639-678) and _activation_derivative
+    (:624-636) for a whole batch at once: given the kept layer inputs (mlp_forward_kept) and dL/d(output) =
+    grad_out [m, out], ACCUMULATE dL/dW_i = a_i^T d_i and dL/db_i = sum_rows d_i into grad_W / grad_b (tensors
+    shaped like the params), with d_{i-1} = (d_i W_i^T) * act'(a_i); act' = 1[a > 0] (ReLU) or a (1 - a)
+    (Sigmoid), computed from the kept activation."""
+    Ws = params["W"]
+    d = grad_out
+    for i in range(len(Ws) - 1, -1, -1):
+        _wgrad_(grad_W[i], acts[i], d)
+        grad_b[i].add_(d.sum(0))
+        if i > 0:
+            h = acts[i]
+            dh = d @ Ws[i].t()
+            if activation_mode == "ReLU":
+                d = torch.ops.aten.threshold_backward(dh, h, 0.0)   # dh * 1[h > 0] in one pass
+            elif activation_mode == "Sigmoid":
+                d = dh.mul_(h * (1.0 - h))
+            else:
+                raise ValueError(f"Unsupported activation: {activation_mode}")
+
+
 def masked_logits(logits: torch.Tensor, action_mask: torch.Tensor | None) -> torch.Tensor:
     if action_mask is None:
         return logits

@@ -87,12 +87,12 @@ def test_argument_validation_without_gpu(L):
     assert lib.g2048_policy_pack(p, p, p, p, p, p, 272, 32, 32, p, 1 << 20, None) == L.G2048_EINVAL
     assert b"obs width" in lib.g2048_last_error()
     assert lib.g2048_policy_pack(p, p, p, p, p, p, 16, 32, 32, p, 10, None) == L.G2048_EINVAL
-    args = [p, 32, 32, L.ACT_RELU, p, None, L.OBS_ONEHOT, 1.0, 1, 0, L.RNG_PHILOX, None, None, None, 0, None, None,
-            None, None, p, 4, None]
+    args = [p, 32, 32, L.ACT_RELU, p, None, None, L.OBS_ONEHOT, 1.0, 1, 0, L.RNG_PHILOX, None, None, None, 0, None,
+            None, None, None, p, 4, None]
     assert lib.g2048_policy(*args) == L.G2048_EINVAL and b"obs_mode" in lib.g2048_last_error()
-    args[6], args[3] = L.OBS_LOG2, 7
+    args[7], args[3] = L.OBS_LOG2, 7
     assert lib.g2048_policy(*args) == L.G2048_EINVAL and b"activation" in lib.g2048_last_error()
-    args[3], args[10] = L.ACT_RELU, L.RNG_PCG64
+    args[3], args[11] = L.ACT_RELU, L.RNG_PCG64
     assert lib.g2048_policy(*args) == L.G2048_EINVAL and b"PCG64" in lib.g2048_last_error()
 
 

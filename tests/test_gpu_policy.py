@@ -74,8 +74,8 @@ def test_fused_logits_match_gemm_path(h1, h2, act, obs):
     logits = torch.full((n, 4), float("nan"), device=DEV)
     actions = torch.empty(n, dtype=torch.uint8, device=DEV)
     a = {"ReLU": L.ACT_RELU, "Sigmoid": L.ACT_SIGMOID}[act]
-    L.check(lib.g2048_policy(L.ptr(packed), h1, h2, a, L.ptr(boards), None, code, 0.0625, 1, 1, L.RNG_PHILOX, None,
-                             None, None, 0, None, None, None, L.ptr(logits), L.ptr(actions), n,
+    L.check(lib.g2048_policy(L.ptr(packed), h1, h2, a, L.ptr(boards), None, None, code, 0.0625, 1, 1,
+                             L.RNG_PHILOX, None, None, None, 0, None, None, None, L.ptr(logits), L.ptr(actions), n,
                              L.stream_handle(DEV)))
     torch.cuda.synchronize()
     scale = float(ref.abs().max()) + 1e-30
@@ -104,8 +104,8 @@ def test_fused_choice_equals_sample_kernel(rng, greedy, mask):
     logits = torch.empty(n, 4, device=DEV)
     probs = torch.full((n, 4), -1.0, device=DEV)
     actions = torch.full((n,), 9, dtype=torch.uint8, device=DEV)
-    L.check(lib.g2048_policy(L.ptr(packed), h1, h2, L.ACT_RELU, L.ptr(boards), L.ptr(status), L.OBS_LOG2, 0.0625,
-                             mask, greedy, rmode, L.ptr(st), L.ptr(inc), L.ptr(buf), key, L.ptr(seeds),
+    L.check(lib.g2048_policy(L.ptr(packed), h1, h2, L.ACT_RELU, L.ptr(boards), L.ptr(status), None, L.OBS_LOG2,
+                             0.0625, mask, greedy, rmode, L.ptr(st), L.ptr(inc), L.ptr(buf), key, L.ptr(seeds),
                              L.ptr(counter), L.ptr(probs), L.ptr(logits), L.ptr(actions), n, L.stream_handle(DEV)))
     # the same choice on the fused kernel's own logits through g2048_sample
     mk = torch.empty(n, 4, dtype=torch.int8, device=DEV)
@@ -148,3 +148,39 @@ def test_agent_packed_cache_follows_updates():
         agent.params["b"][2].add_(1.0)         # in-place edit of the actor
     p2 = agent._packed_policy(spec)
     assert not torch.equal(p1, p2)
+
+
+def test_lane_index_subset_equals_full_call():
+    """g2048_policy over lane_index (a compacted active-lane list) == the full call on those lanes; the other lanes'
+    actions, probabilities and RNG streams are untouched."""
+    from rl2048_amd import _lib as L
+
+    lib = L.lib()
+    L.ensure_device(DEV)
+    n, h1, h2 = 3000, 256, 256
+    boards = _boards(n, 11)
+    p = _params(h1, h2, 13)
+    packed = _pack(L, lib, p, h1, h2)
+    seeds, st, inc, buf = _pcg(L, lib, n, 77)
+    st_full = st.clone()
+    sel = torch.from_numpy(np.sort(np.random.default_rng(5).choice(n, size=701, replace=False))).to(DEV)
+    idx = sel.to(torch.int32)
+    probs = torch.full((n, 4), -1.0, device=DEV)
+    actions = torch.full((n,), 9, dtype=torch.uint8, device=DEV)
+    L.check(lib.g2048_policy(L.ptr(packed), h1, h2, L.ACT_RELU, L.ptr(boards), None, L.ptr(idx), L.OBS_LOG2, 0.0625,
+                             1, 0, L.RNG_PCG64, L.ptr(st), L.ptr(inc), L.ptr(buf), 0, None, None, L.ptr(probs), None,
+                             L.ptr(actions), idx.numel(), L.stream_handle(DEV)))
+    probs_f = torch.empty(n, 4, device=DEV)
+    actions_f = torch.empty(n, dtype=torch.uint8, device=DEV)
+    L.check(lib.g2048_policy(L.ptr(packed), h1, h2, L.ACT_RELU, L.ptr(boards), None, None, L.OBS_LOG2, 0.0625, 1, 0,
+                             L.RNG_PCG64, L.ptr(st_full), L.ptr(inc), L.ptr(buf), 0, None, None, L.ptr(probs_f), None,
+                             L.ptr(actions_f), n, L.stream_handle(DEV)))
+    torch.cuda.synchronize()
+    m = torch.zeros(n, dtype=torch.bool, device=DEV)
+    m[sel] = True
+    assert torch.equal(actions[m], actions_f[m]) and torch.equal(probs[m], probs_f[m])
+    assert bool((actions[~m] == 9).all()) and bool((probs[~m] == -1.0).all())
+    st2, sf2 = st.view(n, 2), st_full.view(n, 2)
+    assert torch.equal(st2[m], sf2[m])
+    _, st0, _, _ = _pcg(L, lib, n, 77)
+    assert torch.equal(st2[~m], st0.view(n, 2)[~m])

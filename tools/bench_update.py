@@ -1,0 +1,60 @@
+"""TOOL: training-loop throughput on the GPU box -- rollout_batch and update_from_batch timed separately for the
+runner-default agent (MLP 16-256-256-4 ReLU, log2 obs, batch baseline), REINFORCE and actor-critic, at several
+batch sizes (episodes per update).  One JSON line per configuration.
+
+    python tools/bench_update.py [--episodes 256 4096 65536] [--critic]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+FLOP_FWD = 2 * (16 * 256 + 256 * 256 + 256 * 4)      # per sample, actor forward
+FLOP_BWD = 2 * (256 * 256 + 256 * 256 + 16 * 256 + 2 * 256 * 4)   # dW2, dH1, dW1, dW3 + dH2
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--episodes", type=int, nargs="+", default=[256, 4096, 65536])
+    ap.add_argument("--critic", action="store_true")
+    ap.add_argument("--max-steps", type=int, default=1024)
+    ap.add_argument("--repeats", type=int, default=2)
+    args = ap.parse_args()
+    import torch
+
+    from rl2048_amd import Game2048EnvConfig
+    from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
+    from rl2048_amd.mlp import MLPConfig
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    for n in args.episodes:
+        agent = ReinforceAgent(Game2048EnvConfig(max_steps=args.max_steps),
+                               MLPConfig(hidden_sizes=[256, 256], activation="ReLU", init_distribution="HeNormal"),
+                               ReinforceAgentConfig(baseline_mode="batch", use_critic=args.critic), device=dev)
+        for rep in range(args.repeats + 1):
+            base = 1000 + rep * n
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            batch = agent.rollout_batch(list(range(base, base + n)), list(range(base + 7 * n, base + 8 * n)))
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            agent.update_from_batch(batch)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            if rep == 0:
+                continue                       # warm-up (allocator, kernels)
+            samples = int(batch.lengths.sum())
+            flop = samples * (FLOP_FWD + FLOP_BWD) * (2 if args.critic else 1)
+            print(json.dumps({"episodes": n, "critic": args.critic, "T": batch.T, "samples": samples,
+                              "rollout_s": round(t1 - t0, 4), "update_s": round(t2 - t1, 4),
+                              "rollout_steps_per_s": samples / (t1 - t0), "update_samples_per_s": samples / (t2 - t1),
+                              "update_tflops": flop / (t2 - t1) / 1e12}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
