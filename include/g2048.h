@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 2
+#define G2048_ABI_VERSION 3
 
 /* status codes */
 #define G2048_OK 0
@@ -195,6 +195,20 @@ int g2048_policy(const float* packed, int h1, int h2, int activation, const uint
                  const uint64_t* rng_inc, const uint64_t* rng_buf, uint64_t philox_key, const uint64_t* lane_seed,
                  const uint32_t* counter, float* probs_out, float* logits_out, uint8_t* actions, int64_t n,
                  void* stream);
+
+/* The whole batched rollout in one launch: ReinforceAgent.run_episode (src/reinforce_agent.py:195-252) for n
+ * (env_seed, policy_seed) pairs -- select_action (the fused policy above) + Game2048Env.step until terminated or
+ * truncated, per episode.  env_* / pol_*: the PCG64 streams of default_rng(env_seed) / default_rng(policy_seed)
+ * per episode (g2048_seed_pcg64); queue: one uint32, zero before the call (episode work queue).
+ * Trajectory rows are time-major [cap, n]: boards (pre-step), actions, rewards (fp32), flags (G2048_F_*),
+ * probs [cap, n, 4] (NULL ok); rows at or past an episode's length are not written.  Per episode: lengths,
+ * totals (fp64 sum of the fp32 rewards), max_tile (log2 of max_tile_seen), final_board.
+ * Requires obs_mode log2 / raw, cfg->max_steps >= 0 and cap >= max(max_steps, 1) (episodes end by then). */
+int g2048_rollout(const float* packed, int h1, int h2, int activation, const g2048_env_cfg* cfg, int greedy,
+                  const uint64_t* env_state, const uint64_t* env_inc, const uint64_t* env_buf, const uint64_t* pol_state,
+                  const uint64_t* pol_inc, const uint64_t* pol_buf, uint32_t* queue, int64_t n, int64_t cap,
+                  uint64_t* boards, uint8_t* actions, float* rewards, uint8_t* flags, float* probs, int32_t* lengths,
+                  double* totals, uint8_t* max_tile, uint64_t* final_board, void* stream);
 
 #ifdef __cplusplus
 }

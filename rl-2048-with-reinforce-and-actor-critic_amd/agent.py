@@ -192,6 +192,8 @@ class ReinforceAgent:
         self.chunk_steps = int(chunk_steps)
         # rollout / evaluation forward through the fused g2048_policy kernel when the net fits it
         self.use_fused_policy = True
+        # ... and the whole rollout in one launch (g2048_rollout) when the episodes are bounded (max_steps set)
+        self.use_fused_rollout = True
         self._params_version = 0
         self._packed: torch.Tensor | None = None
         self._pack_key = None
@@ -392,6 +394,9 @@ class ReinforceAgent:
         n = len(env_seeds)
         if len(policy_seeds) != n:
             raise ValueError("env_seeds and policy_seeds must have the same length")
+        spec = self._fused_policy_spec()
+        if spec is not None and rng == "pcg64" and self.env_config.max_steps is not None and self.use_fused_rollout:
+            return self._rollout_fused(env_seeds, policy_seeds, spec, use_greedy, record_probs)
         env = self._vec_env(n, rng)
         env.reset(seed=list(env_seeds) if not isinstance(env_seeds, torch.Tensor) else env_seeds)
         dev = self.device
@@ -416,7 +421,6 @@ class ReinforceAgent:
         # the reference masks the logits only when the obs carries an action mask (encode_observation,
         # src/MLP.py:22-43 -> select_action src/reinforce_agent.py:138-145)
         use_mask = bool(self.env_config.use_action_mask)
-        spec = self._fused_policy_spec()
         packed = self._packed_policy(spec) if spec is not None else None
         active_idx = None
         t = 0
@@ -466,6 +470,48 @@ class ReinforceAgent:
                                flags=fl[:T], lengths=lengths, total_reward=total,
                                max_tile=env.max_tile_seen.clone(), final_boards=env.board.clone(),
                                probs=probs[:T] if probs is not None else None)
+
+    def _rollout_fused(self, env_seeds, policy_seeds, spec, use_greedy: bool, record_probs: bool) -> TrajectoryBatch:
+        """rollout_batch in ONE launch (g2048_rollout): every episode runs to its end inside a persistent kernel
+        (fused policy + env step per step, episode slots refilled from a work queue)."""
+        from .config import env_cfg_struct
+        from .vec_env import _as_u64_seeds
+
+        n = len(env_seeds)
+        dev = self.device
+        es = _as_u64_seeds(list(env_seeds) if not isinstance(env_seeds, torch.Tensor) else env_seeds, n, 0, dev)
+        ps = _as_u64_seeds(list(policy_seeds) if not isinstance(policy_seeds, torch.Tensor) else policy_seeds, n, 0,
+                           dev)
+        streams = []
+        for seeds in (es, ps):
+            st = torch.empty(2 * n, dtype=torch.int64, device=dev)
+            inc = torch.empty(2 * n, dtype=torch.int64, device=dev)
+            buf = torch.empty(n, dtype=torch.int64, device=dev)
+            L.check(self._lib.g2048_seed_pcg64(L.ptr(seeds), L.ptr(st), L.ptr(inc), L.ptr(buf), n, self._stream))
+            streams += [st, inc, buf]
+        cap = max(int(self.env_config.max_steps), 1)
+        boards = torch.empty(cap, n, dtype=torch.int64, device=dev)
+        actions = torch.zeros(cap, n, dtype=torch.uint8, device=dev)
+        rewards = torch.zeros(cap, n, dtype=torch.float32, device=dev)
+        flags = torch.full((cap, n), L.F_INACTIVE, dtype=torch.uint8, device=dev)
+        probs = torch.zeros(cap, n, 4, dtype=torch.float32, device=dev) if record_probs else None
+        lengths = torch.empty(n, dtype=torch.int32, device=dev)
+        totals = torch.empty(n, dtype=torch.float64, device=dev)
+        max_e = torch.empty(n, dtype=torch.uint8, device=dev)
+        final = torch.empty(n, dtype=torch.int64, device=dev)
+        queue = torch.zeros(1, dtype=torch.int32, device=dev)
+        cfg = env_cfg_struct(self.env_config)
+        packed = self._packed_policy(spec)
+        L.check(self._lib.g2048_rollout(L.ptr(packed), spec[0], spec[1], spec[2], ctypes.byref(cfg), int(use_greedy),
+                                        *[L.ptr(t) for t in streams], L.ptr(queue), n, cap, L.ptr(boards),
+                                        L.ptr(actions), L.ptr(rewards), L.ptr(flags),
+                                        L.ptr(probs) if probs is not None else None, L.ptr(lengths), L.ptr(totals),
+                                        L.ptr(max_e), L.ptr(final), self._stream))
+        T = int(lengths.max().item()) if n else 0
+        return TrajectoryBatch(boards=boards[:T], actions=actions[:T], rewards=rewards[:T], flags=flags[:T],
+                               lengths=lengths, total_reward=totals,
+                               max_tile=torch.ones(n, dtype=torch.int64, device=dev) << max_e.to(torch.int64),
+                               final_boards=final, probs=probs[:T] if probs is not None else None)
 
     def trajectories_from_batch(self, batch: TrajectoryBatch, with_states: bool = True) -> list[dict[str, Any]]:
         """Convert a device batch to the reference's trajectory dicts (src/reinforce_agent.py:240-247)."""

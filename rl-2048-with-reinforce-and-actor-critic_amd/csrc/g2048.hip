@@ -26,6 +26,10 @@
 
 using namespace g2048;
 
+static_assert(G2048_F_CHANGED == kFChanged && G2048_F_TERMINATED == kFTerminated && G2048_F_TRUNCATED == kFTruncated &&
+                  G2048_F_INVALID == kFInvalid && G2048_F_OVERFLOW == kFOverflow,
+              "g2048_core.h step flag bits == include/g2048.h");
+
 namespace {
 
 thread_local std::string g_err;
@@ -793,9 +797,13 @@ int device_cus(int dev) {
 
 }  // namespace
 
-// error string shared with the other translation unit of the library (g2048_policy.hip)
+// shared with the other translation unit of the library (g2048_policy.hip): the error string, the current
+// device's row tables, env-config validation / reward config
 namespace g2048_internal {
 int set_error(int code, const char* msg) { return fail(code, msg); }
+int device_tables(const uint8_t*& tab, int& cus) { return tab_for_current(tab, cus); }
+int check_env_cfg(const g2048_env_cfg* c) { return check_cfg(c); }
+RewardCfg reward_cfg_of(const g2048_env_cfg& c) { return reward_cfg(c); }
 }  // namespace g2048_internal
 
 extern "C" {

@@ -571,6 +571,40 @@ G2048_HD double env_reward(const RewardCfg& c, const MoveSummary& s, uint64_t fi
     return r;
 }
 
+// Flag bits of a step (the G2048_F_* of include/g2048.h; g2048.hip static_asserts they agree).
+constexpr uint32_t kFChanged = 1u, kFTerminated = 2u, kFTruncated = 4u, kFInvalid = 8u, kFOverflow = 16u;
+
+// One Game2048Env.step (src/env.py:264-302) on a lane held in values, PCG64 parity stream: move, score, spawn
+// only if the board changed (src/game2048.py:40-70), done of the final board, reward (fp64, stored fp32 by the
+// caller), truncation at max_steps (< 0 = None).  Updates step_count / max_tile_e / g; returns the new board.
+struct StepValues {
+    uint64_t board;
+    double reward;
+    uint32_t flags, score_add;
+};
+
+template <class Lut, class Code>
+G2048_HD StepValues env_step_pcg(uint64_t b, uint32_t a, uint32_t& step_count, uint32_t& max_tile_e, Pcg64& g,
+                                 const RewardCfg& rc, int64_t max_steps, const Lut& lut, const Code& code) {
+    const uint32_t sc = step_count + 1u;
+    MoveSummary s;
+    uint64_t m = board_move_coded<false>(b, a, lut, code, s);
+    const bool changed = m != b;
+    if (changed) m = spawn_pcg(m, g);
+    const BoardBits bits = board_bits(m);
+    const bool done = bits_done(bits);
+    const bool invalid = !changed && !done;
+    StepValues o;
+    o.reward = env_reward(rc, s, m, done, invalid, max_tile_e);
+    const bool trunc = max_steps >= 0 && (int64_t)sc >= max_steps && !done;
+    o.flags = (changed ? kFChanged : 0u) | (done ? kFTerminated : 0u) | (trunc ? kFTruncated : 0u) |
+              (invalid ? kFInvalid : 0u) | (s.overflow ? kFOverflow : 0u);
+    o.board = m;
+    o.score_add = s.score;
+    step_count = sc;
+    return o;
+}
+
 // Dihedral symmetry k of a board (Game2048Env.get_symmetries order, src/env.py:355-396):
 // k = 0..3: k counter-clockwise quarter turns (np.rot90 k=1 per step); k = 4..7: fliplr, then (k-4) turns.
 G2048_HD uint64_t rot_ccw(uint64_t b) { return transpose(reverse_rows(b)); }  // out[i][j] = b[j][3-i]

@@ -136,23 +136,114 @@ __device__ __forceinline__ float obs_value(uint64_t b, int cell, float scale) {
 template <int NT1>
 constexpr int pol_waves_per_simd() { return NT1 >= 8 ? 1 : 2; }
 
+// Small tensors of the packed net staged in LDS (layer-1 fragments, biases, layer 3: <= 22.5 KB); the
+// layer-2 fragments (the bulk, up to 256 KB) stay in L2 and are streamed by mlp_logits.
+template <int NT1, int NT2>
+struct NetSmem {
+    static constexpr PolLayout L = pol_layout(NT1, NT2);
+    static constexpr int kFloats = (int)(L.w2f - L.w1f) + (int)(L.total - L.b2p);
+    float v[kFloats];
+    __device__ void load(const float* net) {   // whole workgroup; caller syncs
+        for (int k = threadIdx.x; k < kFloats; k += blockDim.x) v[k] = k < (int)L.w2f ? net[k] : net[L.b2p + (k - (int)L.w2f)];
+    }
+    __device__ const float* w1f() const { return v; }
+    __device__ const float* b1p() const { return v + L.b1p; }
+    __device__ const float* b2p() const { return v + L.w2f; }
+    __device__ const float* w3p() const { return v + L.w2f + (L.w3p - L.b2p); }
+    __device__ const float* b3() const { return v + L.w2f + (L.b3 - L.b2p); }
+};
+
+// The 4 logits of board b (this lane's column; both lane halves return the same values) for one wave of 32
+// boards: layer 1 and 2 on fp32 MFMA, layer 3 on VALU (see the file comment).  w2q: the layer-2 fragments
+// (float4) offset by this lane.
+template <int NT1, int NT2, int ACT, int OBS>
+__device__ __forceinline__ void mlp_logits(const NetSmem<NT1, NT2>& sm, const float4* __restrict__ w2q, uint64_t b,
+                                           float obs_scale, int lane, float lg[4]) {
+    const int h = lane >> 5;
+    // first layer-2 fragments in flight while layer 1 runs
+    float4 fa[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) fa[q] = w2q[q * 64];
+    // X^T k-step s: row k = 2s + h (obs feature), column = board
+    float x[8];
+#pragma unroll
+    for (int s = 0; s < 8; s++) x[s] = obs_value<OBS>(b, 2 * s + h, obs_scale);
+    // layer 1: H1^T tile t (32 hidden x 32 boards), bias + activation in registers
+    float h1[NT1][16];
+    const float* w1f = sm.w1f();
+#pragma unroll
+    for (int t = 0; t < NT1; t++) {
+        floatx16 acc = {};
+#pragma unroll
+        for (int s = 0; s < 8; s++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1f[(t * 8 + s) * 64 + lane], x[s], acc, 0, 0, 0);
+        const float4* bb = reinterpret_cast<const float4*>(sm.b1p() + (t * 2 + h) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float4 bv = bb[q];
+            h1[t][4 * q + 0] = activate<ACT>(acc[4 * q + 0] + bv.x);
+            h1[t][4 * q + 1] = activate<ACT>(acc[4 * q + 1] + bv.y);
+            h1[t][4 * q + 2] = activate<ACT>(acc[4 * q + 2] + bv.z);
+            h1[t][4 * q + 3] = activate<ACT>(acc[4 * q + 3] + bv.w);
+        }
+    }
+    // layer 2 tile by tile (A fragments of k-tile t+1 loaded while tile t's 16 MFMAs run, across tiles),
+    // each output tile folded into the 4 logits as soon as it is done
+    lg[0] = lg[1] = lg[2] = lg[3] = 0.0f;
+#pragma unroll 1
+    for (int o = 0; o < NT2; o++) {
+        floatx16 acc = {};
+        const float4* wo = w2q + o * NT1 * 4 * 64;
+#pragma unroll
+        for (int t = 0; t < NT1; t++) {
+            float4 fb[4];
+            const float4* nx = (t + 1 < NT1) ? wo + (t + 1) * 4 * 64 : (o + 1 < NT2 ? wo + NT1 * 4 * 64 : w2q);
+#pragma unroll
+            for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, h1[t][4 * q + 0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, h1[t][4 * q + 1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, h1[t][4 * q + 2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, h1[t][4 * q + 3], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) fa[q] = fb[q];
+        }
+        const float4* bb = reinterpret_cast<const float4*>(sm.b2p() + (o * 2 + h) * 16);
+        const float4* w3 = reinterpret_cast<const float4*>(sm.w3p() + (o * 2 + h) * 64);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float4 bv = bb[q];
+            const float hv[4] = {activate<ACT>(acc[4 * q + 0] + bv.x), activate<ACT>(acc[4 * q + 1] + bv.y),
+                                 activate<ACT>(acc[4 * q + 2] + bv.z), activate<ACT>(acc[4 * q + 3] + bv.w)};
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const float4 wv = w3[4 * q + u];
+                lg[0] = fmaf(hv[u], wv.x, lg[0]);
+                lg[1] = fmaf(hv[u], wv.y, lg[1]);
+                lg[2] = fmaf(hv[u], wv.z, lg[2]);
+                lg[3] = fmaf(hv[u], wv.w, lg[3]);
+            }
+        }
+    }
+    // the two lane halves hold different hidden units of the same board
+    const float* b3 = sm.b3();
+#pragma unroll
+    for (int k = 0; k < 4; k++) lg[k] = (lg[k] + __shfl_xor(lg[k], 32, 64)) + b3[k];
+}
+
+__device__ __forceinline__ uint32_t mask_word_of(uint64_t b) {
+    const uint32_t m = action_mask(b);   // int8[4] as one word: byte a = bit a
+    return (m & 1u) | ((m & 2u) << 7) | ((m & 4u) << 14) | ((m & 8u) << 21);
+}
+
 template <int NT1, int NT2, int ACT, int OBS, int RNG>
 __global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) policy_kernel(PolArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
-    constexpr PolLayout L = pol_layout(NT1, NT2);
-    // the small tensors (layer-1 fragments, biases, layer 3: <= 22.5 KB) are staged in LDS once per workgroup;
-    // the layer-2 fragments (the bulk, up to 256 KB) stream from L2 with an explicit one-k-tile-ahead prefetch
-    constexpr int kSmall = (int)(L.w2f - L.w1f) + (int)(L.total - L.b2p);
-    __shared__ float sm[kSmall];
-    for (int k = threadIdx.x; k < kSmall; k += kPolBlock)
-        sm[k] = k < (int)L.w2f ? a.net[k] : a.net[L.b2p + (k - (int)L.w2f)];
+    __shared__ NetSmem<NT1, NT2> sm;
+    sm.load(a.net);
     __syncthreads();
-    const float* w1f = sm;
-    const float* b1p = sm + L.b1p;
-    const float* b2p = sm + L.w2f;
-    const float* w3p = sm + L.w2f + (L.w3p - L.b2p);
-    const float* b3 = sm + L.w2f + (L.b3 - L.b2p);
-    const float4* __restrict__ w2q = reinterpret_cast<const float4*>(a.net + L.w2f) + lane;   // [o][t][q][64]
+    const float4* __restrict__ w2q = reinterpret_cast<const float4*>(a.net + NetSmem<NT1, NT2>::L.w2f) + lane;
     const uint32_t waves = gridDim.x * (kPolBlock / 64);
     const uint32_t groups = (a.n + 31u) >> 5;
     for (uint32_t gi = blockIdx.x * (kPolBlock / 64) + (threadIdx.x >> 6); gi < groups; gi += waves) {
@@ -160,79 +251,11 @@ __global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) policy_k
         const uint32_t jc = j < a.n ? j : a.n - 1u;
         const uint32_t i = a.lane_index ? (uint32_t)a.lane_index[jc] : jc;   // its board / lane
         const uint64_t b = a.boards[i];
-        // first layer-2 fragments in flight while layer 1 runs
-        float4 fa[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) fa[q] = w2q[q * 64];
-        // X^T k-step s: row k = 2s + h (obs feature), column = board
-        float x[8];
-#pragma unroll
-        for (int s = 0; s < 8; s++) x[s] = obs_value<OBS>(b, 2 * s + h, a.obs_scale);
-        // layer 1: H1^T tile t (32 hidden x 32 boards), bias + activation in registers
-        float h1[NT1][16];
-#pragma unroll
-        for (int t = 0; t < NT1; t++) {
-            floatx16 acc = {};
-#pragma unroll
-            for (int s = 0; s < 8; s++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1f[(t * 8 + s) * 64 + lane], x[s], acc, 0, 0, 0);
-            const float4* bb = reinterpret_cast<const float4*>(b1p + (t * 2 + h) * 16);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float4 bv = bb[q];
-                h1[t][4 * q + 0] = activate<ACT>(acc[4 * q + 0] + bv.x);
-                h1[t][4 * q + 1] = activate<ACT>(acc[4 * q + 1] + bv.y);
-                h1[t][4 * q + 2] = activate<ACT>(acc[4 * q + 2] + bv.z);
-                h1[t][4 * q + 3] = activate<ACT>(acc[4 * q + 3] + bv.w);
-            }
-        }
-        // layer 2 tile by tile (A fragments of k-tile t+1 loaded while tile t's 16 MFMAs run, across tiles),
-        // each output tile folded into the 4 logits as soon as it is done
-        float lg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 1
-        for (int o = 0; o < NT2; o++) {
-            floatx16 acc = {};
-            const float4* wo = w2q + o * NT1 * 4 * 64;
-#pragma unroll
-            for (int t = 0; t < NT1; t++) {
-                float4 fb[4];
-                const float4* nx = (t + 1 < NT1) ? wo + (t + 1) * 4 * 64 : (o + 1 < NT2 ? wo + NT1 * 4 * 64 : w2q);
-#pragma unroll
-                for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, h1[t][4 * q + 0], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, h1[t][4 * q + 1], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, h1[t][4 * q + 2], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, h1[t][4 * q + 3], acc, 0, 0, 0);
-                }
-#pragma unroll
-                for (int q = 0; q < 4; q++) fa[q] = fb[q];
-            }
-            const float4* bb = reinterpret_cast<const float4*>(b2p + (o * 2 + h) * 16);
-            const float4* w3 = reinterpret_cast<const float4*>(w3p + (o * 2 + h) * 64);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float4 bv = bb[q];
-                const float hv[4] = {activate<ACT>(acc[4 * q + 0] + bv.x), activate<ACT>(acc[4 * q + 1] + bv.y),
-                                     activate<ACT>(acc[4 * q + 2] + bv.z), activate<ACT>(acc[4 * q + 3] + bv.w)};
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const float4 wv = w3[4 * q + u];
-                    lg[0] = fmaf(hv[u], wv.x, lg[0]);
-                    lg[1] = fmaf(hv[u], wv.y, lg[1]);
-                    lg[2] = fmaf(hv[u], wv.z, lg[2]);
-                    lg[3] = fmaf(hv[u], wv.w, lg[3]);
-                }
-            }
-        }
-        // the two lane halves hold different hidden units of the same board
-#pragma unroll
-        for (int k = 0; k < 4; k++) lg[k] = (lg[k] + __shfl_xor(lg[k], 32, 64)) + b3[k];
+        float lg[4];
+        mlp_logits<NT1, NT2, ACT, OBS>(sm, w2q, b, a.obs_scale, lane, lg);
         if (h == 0 && j < a.n && (!a.active || (a.active[i] & 1u))) {
             if (a.logits_out) reinterpret_cast<float4*>(a.logits_out)[i] = make_float4(lg[0], lg[1], lg[2], lg[3]);
-            const uint32_t mw = a.use_mask ? ((action_mask(b) & 1u) | ((action_mask(b) & 2u) << 7) |
-                                              ((action_mask(b) & 4u) << 14) | ((action_mask(b) & 8u) << 21))
-                                           : 0x01010101u;
+            const uint32_t mw = a.use_mask ? mask_word_of(b) : 0x01010101u;
             double u = 0.0;
             if (!a.greedy) {
                 if constexpr (RNG == G2048_RNG_PCG64) {
@@ -256,6 +279,144 @@ __global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) policy_k
             const uint32_t act = softmax_select(lg, mw, a.use_mask != 0, a.greedy != 0, u, p);
             if (a.probs_out) reinterpret_cast<float4*>(a.probs_out)[i] = make_float4(p[0], p[1], p[2], p[3]);
             a.actions[i] = (uint8_t)act;
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------------- rollout
+// The whole batched rollout (ReinforceAgent.run_episode, src/reinforce_agent.py:195-252, for n (env_seed,
+// policy_seed) pairs) in one persistent launch: each wave runs 32 episode slots; per step the MLP above picks
+// every slot's action (Generator.choice on the slot's policy stream, or greedy), Game2048Env.step runs in
+// registers (env_step_pcg, row tables read through L1/L2), and the step's trajectory row is written.  A slot
+// whose episode ends writes the episode's results and takes the next episode from a.next (one atomic per
+// episode), so no work is spent on finished episodes and there is no per-step host round trip.  Both lane halves
+// carry every slot (the MFMA layout); the lower half writes.
+struct RolloutArgs {
+    const float* net;
+    const uint8_t* tab;
+    RewardCfg rc;
+    int64_t max_steps;
+    float obs_scale;
+    int use_mask, greedy;
+    const uint64_t *env_rs, *env_inc, *env_buf;   // default_rng(env_seed) per episode (g2048_seed_pcg64)
+    const uint64_t *pol_rs, *pol_inc, *pol_buf;   // default_rng(policy_seed) per episode
+    uint32_t* next;                               // episode queue (zero before the launch)
+    uint64_t* boards;                             // [cap, n] time-major trajectory rows
+    uint8_t* actions;
+    float* rewards;
+    uint8_t* flags;
+    float* probs;                                 // [cap, n, 4] or NULL
+    int32_t* lengths;                             // per episode
+    double* totals;
+    uint8_t* max_tile;
+    uint64_t* final_board;
+    uint32_t n, cap;
+};
+
+__device__ __forceinline__ Pcg64 load_stream(const uint64_t* rs, const uint64_t* inc, const uint64_t* buf, uint32_t e) {
+    Pcg64 g;
+    const ulonglong2 s = reinterpret_cast<const ulonglong2*>(rs)[e];
+    const ulonglong2 c = reinterpret_cast<const ulonglong2*>(inc)[e];
+    const uint64_t bf = buf[e];
+    g.s_lo = s.x;
+    g.s_hi = s.y;
+    g.i_lo = c.x;
+    g.i_hi = c.y;
+    g.has_uint32 = (uint32_t)(bf >> 32);
+    g.uinteger = (uint32_t)bf;
+    return g;
+}
+
+struct GLine {
+    const uint16_t* p;
+    __device__ uint32_t operator()(uint32_t o) const { return p[o]; }
+};
+struct GCode {
+    const uint8_t* p;
+    __device__ uint32_t operator()(uint32_t o) const { return (p[o >> 1] >> ((o & 1u) << 2)) & 15u; }
+};
+
+template <int NT1, int NT2, int ACT, int OBS>
+__global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) rollout_kernel(RolloutArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    __shared__ NetSmem<NT1, NT2> sm;
+    sm.load(a.net);
+    __syncthreads();
+    const float4* __restrict__ w2q = reinterpret_cast<const float4*>(a.net + NetSmem<NT1, NT2>::L.w2f) + lane;
+    const GLine lut{reinterpret_cast<const uint16_t*>(a.tab)};
+    const GCode code{a.tab + 2 * 65536};
+    // claim episodes for the slots that need one: wave-aggregated atomic on the lower half, broadcast to the upper
+    const auto claim = [&](bool need) -> uint32_t {
+        const uint64_t bal = __ballot(need && h == 0);
+        uint32_t base = 0;
+        if (bal) {
+            const int leader = __builtin_ctzll(bal);
+            if (lane == leader) base = atomicAdd(a.next, (uint32_t)__popcll(bal));
+            base = (uint32_t)__shfl((int)base, leader, 64);
+        }
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        const uint32_t mine = base + rank;                                   // valid on the lower half
+        return (uint32_t)__shfl((int)mine, col, 64);                         // the upper half copies its slot
+    };
+    uint32_t ep = claim(true);
+    bool drained = __ballot(ep >= a.n) != 0ull;          // wave-uniform: the queue is empty (claims only grow)
+    uint32_t t = 0, sc = 0, mt = 2;
+    uint64_t b = 0;
+    double total = 0.0;
+    Pcg64 ge{}, gp{};
+    const auto start = [&]() {
+        if (ep < a.n) {
+            ge = load_stream(a.env_rs, a.env_inc, a.env_buf, ep);
+            gp = load_stream(a.pol_rs, a.pol_inc, a.pol_buf, ep);
+            b = spawn_pcg(spawn_pcg(0ull, ge), ge);       // Game2048.reset (src/game2048.py:26-34)
+            t = 0;
+            sc = 0;
+            mt = 2;                                       // max_tile_seen = 4 (src/env.py:188)
+            total = 0.0;
+        }
+    };
+    start();
+    while (__ballot(ep < a.n)) {                         // wave-uniform
+        float lg[4];
+        mlp_logits<NT1, NT2, ACT, OBS>(sm, w2q, b, a.obs_scale, lane, lg);
+        if (ep < a.n) {
+            const uint32_t mw = a.use_mask ? mask_word_of(b) : 0x01010101u;
+            const double u = a.greedy ? 0.0 : pcg_random(gp);
+            float p[4];
+            const uint32_t act = softmax_select(lg, mw, a.use_mask != 0, a.greedy != 0, u, p);
+            const StepValues o = env_step_pcg(b, act, sc, mt, ge, a.rc, a.max_steps, lut, code);
+            const float r = (float)o.reward;
+            total += (double)r;
+            if (h == 0) {
+                const size_t row = (size_t)t * a.n + ep;
+                a.boards[row] = b;
+                a.actions[row] = (uint8_t)act;
+                a.rewards[row] = r;
+                a.flags[row] = (uint8_t)o.flags;
+                if (a.probs) reinterpret_cast<float4*>(a.probs)[row] = make_float4(p[0], p[1], p[2], p[3]);
+            }
+            b = o.board;
+            t += 1;
+            const bool end = (o.flags & (kFTerminated | kFTruncated)) != 0u || t >= a.cap;
+            if (end) {
+                if (h == 0) {
+                    a.lengths[ep] = (int32_t)t;
+                    a.totals[ep] = total;
+                    a.max_tile[ep] = (uint8_t)mt;
+                    a.final_board[ep] = b;
+                }
+                ep = a.n;                                 // claimed below
+            }
+        }
+        const bool need = ep >= a.n;
+        if (!drained && __ballot(need)) {                // wave-uniform
+            const uint32_t fresh = claim(need);
+            if (need && fresh < a.n) {
+                ep = fresh;
+                start();
+            }
+            drained = __ballot(need && fresh >= a.n) != 0ull;
         }
     }
 }
@@ -290,6 +451,28 @@ void launch_pol_nt2(const PolArgs& a, int nt2, int act, int obs, int rng, int gr
     }
 }
 
+template <int NT1, int NT2, int ACT>
+void launch_roll_obs(const RolloutArgs& a, int obs, int grid, hipStream_t s) {
+    if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((rollout_kernel<NT1, NT2, ACT, G2048_OBS_LOG2>), dim3(grid), dim3(kPolBlock), 0, s, a);
+    else hipLaunchKernelGGL((rollout_kernel<NT1, NT2, ACT, G2048_OBS_RAW>), dim3(grid), dim3(kPolBlock), 0, s, a);
+}
+
+template <int NT1, int NT2>
+void launch_roll_act(const RolloutArgs& a, int act, int obs, int grid, hipStream_t s) {
+    if (act == G2048_ACT_RELU) launch_roll_obs<NT1, NT2, 0>(a, obs, grid, s);
+    else launch_roll_obs<NT1, NT2, 1>(a, obs, grid, s);
+}
+
+template <int NT1>
+void launch_roll_nt2(const RolloutArgs& a, int nt2, int act, int obs, int grid, hipStream_t s) {
+    switch (nt2) {
+        case 1: launch_roll_act<NT1, 1>(a, act, obs, grid, s); break;
+        case 2: launch_roll_act<NT1, 2>(a, act, obs, grid, s); break;
+        case 4: launch_roll_act<NT1, 4>(a, act, obs, grid, s); break;
+        default: launch_roll_act<NT1, 8>(a, act, obs, grid, s); break;
+    }
+}
+
 int tiles_for(int hsize) {   // hidden units -> 32-unit tiles, rounded up to 1, 2, 4 or 8
     const int t = (hsize + 31) / 32;
     return t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : 8;
@@ -297,8 +480,11 @@ int tiles_for(int hsize) {   // hidden units -> 32-unit tiles, rounded up to 1, 
 
 }  // namespace
 
-namespace g2048_internal {
-int set_error(int code, const char* msg);   // g2048.hip: the g2048_last_error() string
+namespace g2048_internal {   // g2048.hip
+int set_error(int code, const char* msg);   // the g2048_last_error() string
+int device_tables(const uint8_t*& tab, int& cus);
+int check_env_cfg(const g2048_env_cfg* c);
+g2048::RewardCfg reward_cfg_of(const g2048_env_cfg& c);
 }  // namespace g2048_internal
 
 namespace {
@@ -377,6 +563,72 @@ int g2048_policy(const float* packed, int h1, int h2, int activation, const uint
         case 2: launch_pol_nt2<2>(a, nt2, activation, obs_mode, rng_mode, (int)grid, s); break;
         case 4: launch_pol_nt2<4>(a, nt2, activation, obs_mode, rng_mode, (int)grid, s); break;
         default: launch_pol_nt2<8>(a, nt2, activation, obs_mode, rng_mode, (int)grid, s); break;
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return pfail(G2048_EHIP, hipGetErrorString(e));
+    return G2048_OK;
+}
+
+int g2048_rollout(const float* packed, int h1, int h2, int activation, const g2048_env_cfg* cfg, int greedy,
+                  const uint64_t* env_state, const uint64_t* env_inc, const uint64_t* env_buf, const uint64_t* pol_state,
+                  const uint64_t* pol_inc, const uint64_t* pol_buf, uint32_t* queue, int64_t n, int64_t cap,
+                  uint64_t* boards, uint8_t* actions, float* rewards, uint8_t* flags, float* probs, int32_t* lengths,
+                  double* totals, uint8_t* max_tile, uint64_t* final_board, void* stream) {
+    int rc = g2048_internal::check_env_cfg(cfg);
+    if (rc) return rc;
+    if (n < 0 || n > (int64_t)0x7FFFFFFF) return pfail(G2048_EINVAL, "n out of range");
+    if (n == 0) return G2048_OK;
+    if (cfg->obs_mode != G2048_OBS_LOG2 && cfg->obs_mode != G2048_OBS_RAW)
+        return pfail(G2048_EINVAL, "fused rollout: obs_mode must be log2 or raw");
+    if (cfg->max_steps < 0) return pfail(G2048_EINVAL, "fused rollout: max_steps must be set (>= 0)");
+    if (cap < (cfg->max_steps > 1 ? cfg->max_steps : 1) || cap > (int64_t)0x7FFFFFFF)
+        return pfail(G2048_EINVAL, "fused rollout: cap must be >= max(max_steps, 1)");
+    if (g2048_policy_packed_size(h1, h2) < 0) return pfail(G2048_EINVAL, "fused policy: hidden sizes must be in 1..256");
+    if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
+        return pfail(G2048_EINVAL, "Unsupported activation");
+    if (!packed || !env_state || !env_inc || !env_buf || !pol_state || !pol_inc || !pol_buf || !queue || !boards ||
+        !actions || !rewards || !flags || !lengths || !totals || !max_tile || !final_board)
+        return pfail(G2048_EINVAL, "fused rollout: a required buffer is NULL");
+    const uint8_t* tab = nullptr;
+    int cus = 256;
+    if ((rc = g2048_internal::device_tables(tab, cus))) return rc;
+    RolloutArgs a;
+    a.net = packed;
+    a.tab = tab;
+    a.rc = g2048_internal::reward_cfg_of(*cfg);
+    a.max_steps = cfg->max_steps;
+    a.obs_scale = cfg->obs_log2_scale;
+    a.use_mask = cfg->use_action_mask;
+    a.greedy = greedy;
+    a.env_rs = env_state;
+    a.env_inc = env_inc;
+    a.env_buf = env_buf;
+    a.pol_rs = pol_state;
+    a.pol_inc = pol_inc;
+    a.pol_buf = pol_buf;
+    a.next = queue;
+    a.boards = boards;
+    a.actions = actions;
+    a.rewards = rewards;
+    a.flags = flags;
+    a.probs = probs;
+    a.lengths = lengths;
+    a.totals = totals;
+    a.max_tile = max_tile;
+    a.final_board = final_board;
+    a.n = (uint32_t)n;
+    a.cap = (uint32_t)cap;
+    const int nt1 = tiles_for(h1), nt2 = tiles_for(h2);
+    const int per_cu = nt1 >= 8 ? 1 : 2;   // pol_waves_per_simd
+    const int64_t waves_needed = (n + 31) / 32, per_block = kPolBlock / 64;
+    int64_t grid = (waves_needed + per_block - 1) / per_block;
+    if (grid > per_cu * cus) grid = per_cu * cus;   // persistent; the slots refill from the episode queue
+    hipStream_t s = (hipStream_t)stream;
+    switch (nt1) {
+        case 1: launch_roll_nt2<1>(a, nt2, activation, cfg->obs_mode, (int)grid, s); break;
+        case 2: launch_roll_nt2<2>(a, nt2, activation, cfg->obs_mode, (int)grid, s); break;
+        case 4: launch_roll_nt2<4>(a, nt2, activation, cfg->obs_mode, (int)grid, s); break;
+        default: launch_roll_nt2<8>(a, nt2, activation, cfg->obs_mode, (int)grid, s); break;
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return pfail(G2048_EHIP, hipGetErrorString(e));

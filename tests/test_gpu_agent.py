@@ -54,15 +54,18 @@ def _np_params(p):
     return {k: [t.detach().cpu().numpy().copy() for t in v] for k, v in p.items()}
 
 
-@pytest.mark.parametrize("fused,mask", [(True, True), (False, True), (True, False), (False, False)])
-def test_rollout_transitions_and_sampling_bit_exact(fused, mask):
+@pytest.mark.parametrize("path,mask", [("rollout", True), ("policy", True), ("gemm", True), ("rollout", False),
+                                       ("gemm", False)])
+def test_rollout_transitions_and_sampling_bit_exact(path, mask):
     """rollout_batch == the reference's run_episode: same env stream (transitions replayed in the oracle env) and
-    the same policy stream (Generator.choice on the probabilities the device used).  fused: the g2048_policy
-    kernel (else the GEMM path + g2048_sample); mask: use_action_mask (without it the logits are not masked,
-    src/reinforce_agent.py:138-145)."""
+    the same policy stream (Generator.choice on the probabilities the device used).  path: "rollout" = the whole
+    rollout in one launch (g2048_rollout); "policy" = per-step loop with the fused g2048_policy kernel; "gemm" =
+    per-step loop with the GEMM forward + g2048_sample.  mask: use_action_mask (without it the logits are not
+    masked, src/reinforce_agent.py:138-145)."""
     agent = _agent(use_action_mask=mask)
-    agent.use_fused_policy = fused
-    assert (agent._fused_policy_spec() is not None) == fused
+    agent.use_fused_policy = path != "gemm"
+    agent.use_fused_rollout = path == "rollout"
+    assert (agent._fused_policy_spec() is not None) == (path != "gemm")
     n = 48
     env_seeds = [int(s) for s in np.random.default_rng(3).integers(0, 2**62, size=n)]
     pol_seeds = [int(s) for s in np.random.default_rng(4).integers(0, 2**62, size=n)]
@@ -90,10 +93,11 @@ def test_rollout_transitions_and_sampling_bit_exact(fused, mask):
         assert int(batch.max_tile[i]) == env.max_tile_seen
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_rollout_probs_match_numpy_softmax(fused):
+@pytest.mark.parametrize("path", ["rollout", "policy", "gemm"])
+def test_rollout_probs_match_numpy_softmax(path):
     agent = _agent()
-    agent.use_fused_policy = fused
+    agent.use_fused_policy = path != "gemm"
+    agent.use_fused_rollout = path == "rollout"
     batch = agent.rollout_batch(list(range(16)), list(range(100, 116)), record_probs=True)
     from rl2048_amd.mlp import forward_logits
 
