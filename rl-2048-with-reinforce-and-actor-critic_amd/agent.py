@@ -87,6 +87,11 @@ class TrajectoryBatch:
         return int(self.boards.shape[0])
 
 
+def _seed_seq(seeds):
+    """A batch of episode seeds as a tensor / numpy array (kept: the fast conversion path) or a list."""
+    return seeds if isinstance(seeds, (torch.Tensor, np.ndarray)) else list(seeds)
+
+
 def _render_values(vals: np.ndarray) -> str:
     from .env import _render
 
@@ -398,12 +403,11 @@ class ReinforceAgent:
         if spec is not None and rng == "pcg64" and self.env_config.max_steps is not None and self.use_fused_rollout:
             return self._rollout_fused(env_seeds, policy_seeds, spec, use_greedy, record_probs)
         env = self._vec_env(n, rng)
-        env.reset(seed=list(env_seeds) if not isinstance(env_seeds, torch.Tensor) else env_seeds)
+        env.reset(seed=_seed_seq(env_seeds))
         dev = self.device
         from .vec_env import _as_u64_seeds
 
-        pseeds = _as_u64_seeds(list(policy_seeds) if not isinstance(policy_seeds, torch.Tensor) else policy_seeds,
-                               n, 0, dev)
+        pseeds = _as_u64_seeds(_seed_seq(policy_seeds), n, 0, dev)
         pst = torch.empty(2 * n, dtype=torch.int64, device=dev)
         pinc = torch.empty(2 * n, dtype=torch.int64, device=dev)
         pbuf = torch.empty(n, dtype=torch.int64, device=dev)
@@ -479,9 +483,8 @@ class ReinforceAgent:
 
         n = len(env_seeds)
         dev = self.device
-        es = _as_u64_seeds(list(env_seeds) if not isinstance(env_seeds, torch.Tensor) else env_seeds, n, 0, dev)
-        ps = _as_u64_seeds(list(policy_seeds) if not isinstance(policy_seeds, torch.Tensor) else policy_seeds, n, 0,
-                           dev)
+        es = _as_u64_seeds(_seed_seq(env_seeds), n, 0, dev)
+        ps = _as_u64_seeds(_seed_seq(policy_seeds), n, 0, dev)
         streams = []
         for seeds in (es, ps):
             st = torch.empty(2 * n, dtype=torch.int64, device=dev)

@@ -26,6 +26,16 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+#ifndef G2048_DIAG
+#define G2048_DIAG 0
+#endif
+#if G2048_DIAG
+// diag build only: per-workgroup sums of rollout phase durations (s_memrealtime ticks): layer 1 + barrier,
+// layer 2 + barrier, logits + choice + env step, claims; [4] = steps
+constexpr int kRollDiagBlocks = 4096;
+__device__ unsigned long long g_roll_ph[kRollDiagBlocks * 5];
+#endif
+
 constexpr int kPolBlock = 256;   // 4 waves; two workgroups per CU (2 waves per SIMD)
 
 // packed layout (floats), nt1 / nt2 = hidden tiles of 32:
@@ -337,30 +347,65 @@ struct GCode {
     __device__ uint32_t operator()(uint32_t o) const { return (p[o >> 1] >> ((o & 1u) << 2)) & 15u; }
 };
 
+// LDS of one rollout workgroup: the small net tensors, the layer-1 activations of the current step in
+// layer-2 B-fragment order, the per-wave partial logits and the episode-claim broadcast.
+template <int NT1, int NT2>
+struct RollSmem {
+    NetSmem<NT1, NT2> net;
+    float4 h1f[NT1][4][64];      // [k-tile t][r / 4][lane]: registers 4q..4q+3 of layer-1 tile t
+    float part[4][32][4];        // [wave][slot][action]
+    uint32_t claim[32];
+};
+
+// One workgroup (one per CU) = 32 episode slots; its 4 waves split every step's MLP: wave w computes the layer-1
+// tiles and the layer-2 output tiles congruent to w mod 4 (a quarter of the MFMAs), exchanging the layer-1
+// activations and the partial logits through LDS (two barriers per step), so a step takes about a quarter of the
+// one-wave latency.  Each wave's quarter of the layer-2 weights (<= 2 output tiles x NT1 x 16 fragments = 256
+// floats per lane) is loaded ONCE into registers (the accumulator file: MFMA A operands may be AGPRs), so the
+// steady state reads no weights from memory at all.  Every wave then holds the same logits and runs the same
+// choice and env step on the same slot state (so no per-slot state is broadcast); wave 0 writes the trajectory
+// and claims episodes for the workgroup.
 template <int NT1, int NT2, int ACT, int OBS>
-__global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) rollout_kernel(RolloutArgs a) {
-    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
-    __shared__ NetSmem<NT1, NT2> sm;
-    sm.load(a.net);
-    __syncthreads();
+__global__ void __launch_bounds__(kPolBlock, 1) rollout_kernel(RolloutArgs a) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
+    __shared__ RollSmem<NT1, NT2> S;
+    S.net.load(a.net);
     const float4* __restrict__ w2q = reinterpret_cast<const float4*>(a.net + NetSmem<NT1, NT2>::L.w2f) + lane;
     const GLine lut{reinterpret_cast<const uint16_t*>(a.tab)};
     const GCode code{a.tab + 2 * 65536};
-    // claim episodes for the slots that need one: wave-aggregated atomic on the lower half, broadcast to the upper
-    const auto claim = [&](bool need) -> uint32_t {
-        const uint64_t bal = __ballot(need && h == 0);
-        uint32_t base = 0;
-        if (bal) {
-            const int leader = __builtin_ctzll(bal);
-            if (lane == leader) base = atomicAdd(a.next, (uint32_t)__popcll(bal));
-            base = (uint32_t)__shfl((int)base, leader, 64);
+    // episode claims for the slots that need one (identical `need` in all waves): wave 0 takes them with one
+    // atomic and publishes them; every wave must call this together (it contains barriers)
+    // this wave's layer-2 fragments, loaded once: output tiles o = w + 4 k2
+    constexpr int kOwn = (NT2 + 3) / 4;
+    float4 wf[kOwn][NT1][4];
+#pragma unroll
+    for (int k2 = 0; k2 < kOwn; k2++) {
+        const int o = w + 4 * k2 < NT2 ? w + 4 * k2 : 0;
+#pragma unroll
+        for (int tt = 0; tt < NT1; tt++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) wf[k2][tt][q] = w2q[((o * NT1 + tt) * 4 + q) * 64];
+    }
+    const auto claim = [&](bool need, uint32_t cur) -> uint32_t {
+        if (w == 0) {
+            const uint64_t bal = __ballot(need && h == 0);
+            uint32_t base = 0;
+            if (bal) {
+                const int leader = __builtin_ctzll(bal);
+                if (lane == leader) base = atomicAdd(a.next, (uint32_t)__popcll(bal));
+                base = (uint32_t)__shfl((int)base, leader, 64);
+            }
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            if (h == 0) S.claim[col] = need ? base + rank : cur;
         }
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        const uint32_t mine = base + rank;                                   // valid on the lower half
-        return (uint32_t)__shfl((int)mine, col, 64);                         // the upper half copies its slot
+        __syncthreads();
+        const uint32_t v = S.claim[col];
+        __syncthreads();
+        return v;
     };
-    uint32_t ep = claim(true);
-    bool drained = __ballot(ep >= a.n) != 0ull;          // wave-uniform: the queue is empty (claims only grow)
+    uint32_t ep = claim(true, 0u);
+    bool drained = __ballot(ep >= a.n) != 0ull;           // block-uniform: the queue is empty (claims only grow)
     uint32_t t = 0, sc = 0, mt = 2;
     uint64_t b = 0;
     double total = 0.0;
@@ -377,48 +422,139 @@ __global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) rollout_
         }
     };
     start();
-    while (__ballot(ep < a.n)) {                         // wave-uniform
+#if G2048_DIAG
+    unsigned long long ph[5] = {0, 0, 0, 0, 0};
+    unsigned long long tp = __builtin_amdgcn_s_memrealtime();
+#define ROLL_PH(k)                                                        \
+    do {                                                                  \
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();  \
+        ph[k] += tn - tp;                                                 \
+        tp = tn;                                                          \
+    } while (0)
+#else
+#define ROLL_PH(k) \
+    do {           \
+    } while (0)
+#endif
+    while (__ballot(ep < a.n)) {                         // block-uniform (all waves hold the same slot state)
+        // ---- layer 1: this wave's tiles -> LDS
+        float x[8];
+#pragma unroll
+        for (int s2 = 0; s2 < 8; s2++) x[s2] = obs_value<OBS>(b, 2 * s2 + h, a.obs_scale);
+        const float* w1f = S.net.w1f();
+#pragma unroll
+        for (int tt = 0; tt < NT1; tt++) {
+            if ((tt & 3) != w) continue;
+            floatx16 acc = {};
+#pragma unroll
+            for (int s2 = 0; s2 < 8; s2++)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1f[(tt * 8 + s2) * 64 + lane], x[s2], acc, 0, 0, 0);
+            const float4* bb = reinterpret_cast<const float4*>(S.net.b1p() + (tt * 2 + h) * 16);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 bv = bb[q];
+                S.h1f[tt][q][lane] = make_float4(activate<ACT>(acc[4 * q + 0] + bv.x), activate<ACT>(acc[4 * q + 1] + bv.y),
+                                                 activate<ACT>(acc[4 * q + 2] + bv.z), activate<ACT>(acc[4 * q + 3] + bv.w));
+            }
+        }
+        __syncthreads();
+        ROLL_PH(0);
+        // ---- layer 2: this wave's output tiles (B from LDS, A resident in registers), folded into partial logits
+        float lgp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k2 = 0; k2 < kOwn; k2++) {
+            const int o = w + 4 * k2;
+            if (o >= NT2) continue;                         // wave-uniform
+            floatx16 acc = {};
+#pragma unroll
+            for (int tt = 0; tt < NT1; tt++) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4 hb = S.h1f[tt][q][lane];
+                    const float4 fa = wf[k2][tt][q];
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.x, hb.x, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.y, hb.y, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.z, hb.z, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.w, hb.w, acc, 0, 0, 0);
+                }
+            }
+            const float4* bb = reinterpret_cast<const float4*>(S.net.b2p() + (o * 2 + h) * 16);
+            const float4* w3 = reinterpret_cast<const float4*>(S.net.w3p() + (o * 2 + h) * 64);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 bv = bb[q];
+                const float hv[4] = {activate<ACT>(acc[4 * q + 0] + bv.x), activate<ACT>(acc[4 * q + 1] + bv.y),
+                                     activate<ACT>(acc[4 * q + 2] + bv.z), activate<ACT>(acc[4 * q + 3] + bv.w)};
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const float4 wv = w3[4 * q + u];
+                    lgp[0] = fmaf(hv[u], wv.x, lgp[0]);
+                    lgp[1] = fmaf(hv[u], wv.y, lgp[1]);
+                    lgp[2] = fmaf(hv[u], wv.z, lgp[2]);
+                    lgp[3] = fmaf(hv[u], wv.w, lgp[3]);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) lgp[k] += __shfl_xor(lgp[k], 32, 64);
+        if (h == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) S.part[w][col][k] = lgp[k];
+        }
+        __syncthreads();
+        ROLL_PH(1);
+        // ---- every wave: the same logits, choice and env step
+        const float* b3 = S.net.b3();
         float lg[4];
-        mlp_logits<NT1, NT2, ACT, OBS>(sm, w2q, b, a.obs_scale, lane, lg);
+#pragma unroll
+        for (int k = 0; k < 4; k++) lg[k] = (((S.part[0][col][k] + S.part[1][col][k]) + S.part[2][col][k]) + S.part[3][col][k]) + b3[k];
         if (ep < a.n) {
             const uint32_t mw = a.use_mask ? mask_word_of(b) : 0x01010101u;
             const double u = a.greedy ? 0.0 : pcg_random(gp);
             float p[4];
             const uint32_t act = softmax_select(lg, mw, a.use_mask != 0, a.greedy != 0, u, p);
-            const StepValues o = env_step_pcg(b, act, sc, mt, ge, a.rc, a.max_steps, lut, code);
-            const float r = (float)o.reward;
+            const StepValues ov = env_step_pcg(b, act, sc, mt, ge, a.rc, a.max_steps, lut, code);
+            const float r = (float)ov.reward;
             total += (double)r;
-            if (h == 0) {
+            if (w == 0 && h == 0) {
                 const size_t row = (size_t)t * a.n + ep;
                 a.boards[row] = b;
                 a.actions[row] = (uint8_t)act;
                 a.rewards[row] = r;
-                a.flags[row] = (uint8_t)o.flags;
+                a.flags[row] = (uint8_t)ov.flags;
                 if (a.probs) reinterpret_cast<float4*>(a.probs)[row] = make_float4(p[0], p[1], p[2], p[3]);
             }
-            b = o.board;
+            b = ov.board;
             t += 1;
-            const bool end = (o.flags & (kFTerminated | kFTruncated)) != 0u || t >= a.cap;
-            if (end) {
-                if (h == 0) {
+            if ((ov.flags & (kFTerminated | kFTruncated)) != 0u || t >= a.cap) {
+                if (w == 0 && h == 0) {
                     a.lengths[ep] = (int32_t)t;
                     a.totals[ep] = total;
                     a.max_tile[ep] = (uint8_t)mt;
                     a.final_board[ep] = b;
                 }
-                ep = a.n;                                 // claimed below
+                ep = a.n;
             }
         }
+        ROLL_PH(2);
         const bool need = ep >= a.n;
-        if (!drained && __ballot(need)) {                // wave-uniform
-            const uint32_t fresh = claim(need);
+        if (!drained && __ballot(need)) {                // block-uniform
+            const uint32_t fresh = claim(need, ep);
             if (need && fresh < a.n) {
                 ep = fresh;
                 start();
             }
             drained = __ballot(need && fresh >= a.n) != 0ull;
         }
+        ROLL_PH(3);
+#if G2048_DIAG
+        ph[4] += 1;
+#endif
     }
+#if G2048_DIAG
+    if (threadIdx.x == 0 && blockIdx.x < kRollDiagBlocks)
+        for (int k = 0; k < 5; k++) g_roll_ph[blockIdx.x * 5 + k] = ph[k];
+#endif
 }
 
 template <int NT1, int NT2, int ACT, int OBS>
@@ -492,6 +628,17 @@ int pfail(int code, const char* msg) { return g2048_internal::set_error(code, ms
 }  // namespace
 
 extern "C" {
+
+#if G2048_DIAG
+int g2048_diag_rollout_phases(unsigned long long* out, int blocks) {
+    if (blocks > kRollDiagBlocks) blocks = kRollDiagBlocks;
+    if (hipDeviceSynchronize() != hipSuccess) return G2048_EHIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_roll_ph), sizeof(unsigned long long) * 5 * blocks, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return G2048_EHIP;
+    return blocks;
+}
+#endif
 
 int64_t g2048_policy_packed_size(int h1, int h2) {
     if (h1 < 1 || h1 > 256 || h2 < 1 || h2 > 256) return -1;
@@ -619,10 +766,8 @@ int g2048_rollout(const float* packed, int h1, int h2, int activation, const g20
     a.n = (uint32_t)n;
     a.cap = (uint32_t)cap;
     const int nt1 = tiles_for(h1), nt2 = tiles_for(h2);
-    const int per_cu = nt1 >= 8 ? 1 : 2;   // pol_waves_per_simd
-    const int64_t waves_needed = (n + 31) / 32, per_block = kPolBlock / 64;
-    int64_t grid = (waves_needed + per_block - 1) / per_block;
-    if (grid > per_cu * cus) grid = per_cu * cus;   // persistent; the slots refill from the episode queue
+    int64_t grid = (n + 31) / 32;                  // one workgroup per 32 episode slots
+    if (grid > cus) grid = cus;                    // persistent (one per CU); the slots refill from the queue
     hipStream_t s = (hipStream_t)stream;
     switch (nt1) {
         case 1: launch_roll_nt2<1>(a, nt2, activation, cfg->obs_mode, (int)grid, s); break;

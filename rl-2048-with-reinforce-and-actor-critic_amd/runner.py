@@ -146,6 +146,10 @@ class SeedStream:
     def take(self, n: int) -> list[int]:
         return [int(x) for x in self.rng.integers(0, self.hi, size=n, dtype=np.int64)]
 
+    def take_array(self, n: int) -> np.ndarray:
+        """take(n) as an int64 array (the batched rollout's fast seed path)."""
+        return self.rng.integers(0, self.hi, size=n, dtype=np.int64)
+
     def skip(self, n: int) -> None:
         """Advance past n seeds (what take(n) consumes), a block at a time."""
         while n > 0:
@@ -253,7 +257,7 @@ def training_loop(agent: ReinforceAgent, env_config, mlp_config, agent_config, t
         logger.info("Resumed from %s at batch %d", resume_from, step)
     lo, hi = _shard(bs)
     while nb <= 0 or step < nb:
-        env_seeds, pol_seeds = env_stream.take(bs), pol_stream.take(bs)
+        env_seeds, pol_seeds = env_stream.take_array(bs), pol_stream.take_array(bs)
         batch = agent.rollout_batch(env_seeds[lo:hi], pol_seeds[lo:hi])
         step += 1
         totals, max_tiles = _global_episode_stats(batch)
@@ -302,8 +306,8 @@ def evaluation_loop(agent: ReinforceAgent, eval_cfg: Dict[str, Any], chunk: int 
     """runner.py:737-828: num_episodes episodes with fixed seed streams (greedy by default), batched."""
     n = int(eval_cfg["num_episodes"])
     greedy = bool(eval_cfg.get("use_greedy", True))
-    env_seeds = SeedStream(int(eval_cfg["env_base_seed"])).take(n)
-    pol_seeds = SeedStream(int(eval_cfg["policy_base_seed"])).take(n)
+    env_seeds = SeedStream(int(eval_cfg["env_base_seed"])).take_array(n)
+    pol_seeds = SeedStream(int(eval_cfg["policy_base_seed"])).take_array(n)
     totals, tiles = [], []
     for s in range(0, n, chunk):
         e, p = env_seeds[s:s + chunk], pol_seeds[s:s + chunk]

@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 import secrets
 
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -39,6 +40,21 @@ def _as_u64_seeds(seed, n: int, offset: int, device) -> torch.Tensor:
         if seed.numel() != n:
             raise ValueError(f"expected {n} seeds, got {seed.numel()}")
         return seed.to(device=device, dtype=torch.int64).contiguous()
+    # fast path: numpy range-checks a list of python ints in C (negative or >= 2**64 raise OverflowError);
+    # integer arrays are checked for negatives here (numpy casts arrays with wraparound)
+    try:
+        if isinstance(seed, np.ndarray):
+            arr = None
+            if seed.dtype.kind in "iu" and seed.ndim == 1 and not (seed.dtype.kind == "i" and bool((seed < 0).any())):
+                arr = seed.astype(np.uint64, copy=False)
+        elif isinstance(seed, (list, tuple)) and all(type(v) is int for v in seed[:8]):
+            arr = np.array(seed, dtype=np.uint64)
+        else:
+            arr = None
+        if arr is not None and arr.ndim == 1 and arr.size == n:
+            return torch.from_numpy(np.ascontiguousarray(arr).view(np.int64)).to(device)
+    except (OverflowError, TypeError, ValueError):
+        pass   # the checks below produce the reference's error messages
     vals = [int(s) for s in seed]
     if len(vals) != n:
         raise ValueError(f"expected {n} seeds, got {len(vals)}")

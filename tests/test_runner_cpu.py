@@ -24,6 +24,8 @@ def test_seed_stream_blocks_equal_iterator(R, golden_dir):
         s = R.SeedStream(base)
         got = s.take(1) + s.take(255) + s.take(256) + s.take(188)
         assert got == ref
+        s2 = R.SeedStream(base)
+        assert [int(x) for x in s2.take_array(300)] + s2.take(400) == ref
     d = np.load(os.path.join(golden_dir, "pcg64.npz"))
     assert R.SeedStream(3).take(64) == [int(x) for x in d["fixed_seed_iter3"]]
     assert R.SeedStream(7).take(64) == [int(x) for x in d["fixed_seed_iter7"]]
