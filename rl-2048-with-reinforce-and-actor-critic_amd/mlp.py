@@ -142,6 +142,10 @@ def mlp_forward_kept(params: dict[str, list[torch.Tensor]], x: torch.Tensor, act
     acts = [x.to(torch.float32)]
     a = acts[0]
     for i in range(len(Ws)):
+        if i < len(Ws) - 1 and activation_mode == "ReLU" and a.dim() == 2:
+            a = torch._addmm_activation(bs[i], a, Ws[i], use_gelu=False)   # bias + ReLU in the GEMM epilogue
+            acts.append(a)
+            continue
         z = torch.addmm(bs[i], a, Ws[i])
         if i < len(Ws) - 1:
             a = apply_activation(z, activation_mode)
