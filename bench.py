@@ -274,10 +274,14 @@ def main():
 
     import rl2048_amd  # noqa: F401
 
-    device = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    device = torch.device("cuda", local_rank % max(ndev, 1))
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if ndev >= world:
+            dist.init_process_group("nccl", device_id=device)   # RCCL: one rank per GPU (the production layout)
+        else:
+            dist.init_process_group("gloo")   # rehearsal of the N-rank path with ranks sharing a GPU (timing only)
     B = args.boards
     env = make_env(torch, args, B, rank * B, device)
     K, W = args.steps, args.warmup

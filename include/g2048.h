@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 3
+#define G2048_ABI_VERSION 4
 
 /* status codes */
 #define G2048_OK 0
@@ -195,6 +195,28 @@ int g2048_policy(const float* packed, int h1, int h2, int activation, const uint
                  const uint64_t* rng_inc, const uint64_t* rng_buf, uint64_t philox_key, const uint64_t* lane_seed,
                  const uint32_t* counter, float* probs_out, float* logits_out, uint8_t* actions, int64_t n,
                  void* stream);
+
+/* ---- fused actor gradient (update_batch's actor branch) ---------------------------------------------------
+ * For the same nets as g2048_policy: ReinforceAgent.update_batch's actor gradient (src/reinforce_agent.py:502-555:
+ * _policy_gradient_step :328-354, _backpropagation :639-678, _activation_derivative :624-636) over n samples
+ * (valid steps): forward from the boards, masked softmax (use_mask: the boards' action masks, as
+ * logits_to_probs src/MLP.py:139-156), g = (onehot(action) - p) * coef[i] (coef = advantage * step weight),
+ * the output and input deltas and the small weight gradients, all in one kernel.  Outputs:
+ *   a1t [(H1p + 1) x ld]  columns i < n: the first hidden layer's activations a1^T, then a row of ones;
+ *   d2t [H2p x ld]        the second hidden layer's deltas d2^T (columns n..ld-1 of both are written as padding
+ *                         with coefficient 0, so a1t d2t^T over all ld columns is the layer-2 weight gradient
+ *                         [h1 x h2] in rows < h1 and the layer-2 bias gradient in row H1p);
+ *   partials [waves x g2048_grad_partial_size]  per-wave sums: dW1 [16][H1p], db1 [H1p], dW3 [H2p][4], db3 [4].
+ * H1p / H2p = hidden sizes rounded up to 32, 64, 128 or 256; ld a multiple of 32, n <= ld < 2^26;
+ * waves = g2048_actor_grad_waves() (every wave writes its row). */
+int64_t g2048_grad_packed_size(int h1, int h2);
+int64_t g2048_grad_partial_size(int h1, int h2);
+/* Pack W2 [h1 x h2] (src/MLP.py layout) for the input-delta product; re-pack after every update. */
+int g2048_grad_pack(const float* W2, int h1, int h2, float* packed, int64_t packed_len, void* stream);
+int g2048_actor_grad_waves(void);
+int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
+                     float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions, const float* coef,
+                     int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, void* stream);
 
 /* The whole batched rollout in one launch: ReinforceAgent.run_episode (src/reinforce_agent.py:195-252) for n
  * (env_seed, policy_seed) pairs -- select_action (the fused policy above) + Game2048Env.step until terminated or

@@ -23,7 +23,7 @@ if os.environ.get("G2048_DIAG_LIB"):
 SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
 SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # include/g2048.h constants
 OBS_NONE, OBS_RAW, OBS_LOG2, OBS_ONEHOT = -1, 0, 1, 2
@@ -92,15 +92,24 @@ def _declare(L):
                                vp, i64, vp]
     L.g2048_rollout.argtypes = [vp, i32, i32, i32, P(EnvCfg), i32, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp,
                                 vp, vp, vp, vp, vp, vp]
+    L.g2048_grad_packed_size.argtypes = [i32, i32]
+    L.g2048_grad_packed_size.restype = i64
+    L.g2048_grad_partial_size.argtypes = [i32, i32]
+    L.g2048_grad_partial_size.restype = i64
+    L.g2048_grad_pack.argtypes = [vp, i32, i32, vp, i64, vp]
+    L.g2048_actor_grad_waves.argtypes = []
+    L.g2048_actor_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, vp, vp, vp, i64, i64, vp, vp, vp, i64, vp]
     for name in ("g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step", "g2048_obs", "g2048_move",
                  "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy",
-                 "g2048_rollout"):
+                 "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad"):
         getattr(L, name).restype = ctypes.c_int
 
 
 EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g2048_seed_pcg64", "g2048_reset",
                     "g2048_step", "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries",
-                    "g2048_policy_packed_size", "g2048_policy_pack", "g2048_policy", "g2048_rollout")
+                    "g2048_policy_packed_size", "g2048_policy_pack", "g2048_policy", "g2048_rollout",
+                    "g2048_grad_packed_size", "g2048_grad_partial_size", "g2048_grad_pack", "g2048_actor_grad_waves",
+                    "g2048_actor_grad")
 
 
 def lib():

@@ -199,6 +199,11 @@ class ReinforceAgent:
         self.use_fused_policy = True
         # ... and the whole rollout in one launch (g2048_rollout) when the episodes are bounded (max_steps set)
         self.use_fused_rollout = True
+        # update_batch's actor gradient through the fused g2048_actor_grad kernel when the net fits it (batched path)
+        self.use_fused_grad = True
+        self.grad_chunk_steps = 1 << 20
+        self._gpacked: torch.Tensor | None = None
+        self._gpack_key = None
         self._params_version = 0
         self._packed: torch.Tensor | None = None
         self._pack_key = None
@@ -329,7 +334,14 @@ class ReinforceAgent:
     def _fused_policy_spec(self):
         """(h1, h2, activation code) when g2048_policy covers the actor (obs width 16, two hidden layers of
         1..256 units, ReLU / Sigmoid, fp32), else None (the GEMM path + g2048_sample then runs)."""
-        if not self.use_fused_policy or self.env_config.obs_mode not in ("log2", "raw"):
+        return self._net_spec() if self.use_fused_policy else None
+
+    def _fused_grad_spec(self):
+        """The same net check for g2048_actor_grad (else the batched torch backprop runs)."""
+        return self._net_spec() if self.use_fused_grad else None
+
+    def _net_spec(self):
+        if self.env_config.obs_mode not in ("log2", "raw"):
             return None
         Ws, bs = self.params["W"], self.params["b"]
         if len(Ws) != 3 or len(bs) != 3 or tuple(Ws[0].shape)[0] != 16 or tuple(Ws[2].shape)[1] != 4:
@@ -358,6 +370,61 @@ class ReinforceAgent:
                                                 self._stream))
             self._pack_key = key
         return self._packed
+
+    def _grad_packed(self, spec) -> torch.Tensor:
+        """W2 packed for the fused gradient's input-delta product (g2048_grad_pack), re-packed like the policy."""
+        W = self.params["W"][1]
+        key = (self._params_version, W.data_ptr(), W._version)
+        if key != self._gpack_key:
+            h1, h2, _ = spec
+            size = int(self._lib.g2048_grad_packed_size(h1, h2))
+            if self._gpacked is None or self._gpacked.numel() < size:
+                self._gpacked = torch.empty(size, dtype=torch.float32, device=self.device)
+            L.check(self._lib.g2048_grad_pack(L.ptr(W.contiguous()), h1, h2, L.ptr(self._gpacked), size, self._stream))
+            self._gpack_key = key
+        return self._gpacked
+
+    def _actor_grad_fused(self, steps: "_Steps", adv: torch.Tensor, step_w: torch.Tensor, K: int,
+                          gW: list[torch.Tensor], gb: list[torch.Tensor], spec) -> None:
+        """The actor branch of update_batch (src/reinforce_agent.py:502-555) for every valid step and symmetry k:
+        g2048_actor_grad (forward from the bitboards, masked softmax, deltas, dW1 / db1 / dW3 / db3 per wave)
+        plus one split-K GEMM for the layer-2 weight and bias gradient over the a1^T / d2^T columns the kernel
+        writes.  Accumulates into gW / gb like mlp_backward_."""
+        h1, h2, act = spec
+        H1p, H2p = (32 * min(8, 1 << max(0, (h - 1) // 32).bit_length()) for h in (h1, h2))
+        packed, gpacked = self._packed_policy(spec), self._grad_packed(spec)
+        waves = int(self._lib.g2048_actor_grad_waves())
+        pf = int(self._lib.g2048_grad_partial_size(h1, h2))
+        part = torch.empty(waves, pf, dtype=torch.float32, device=self.device)
+        small = torch.zeros(pf, dtype=torch.float32, device=self.device)
+        big = torch.zeros(H1p + 1, H2p, dtype=torch.float32, device=self.device)
+        obs_code, scale = _OBS_CODE[self.env_config.obs_mode], float(self.env_config.obs_log2_scale)
+        use_mask = int(bool(self.env_config.use_action_mask))
+        flat = steps.boards.reshape(-1)
+        for k in range(K):
+            for sel in self._chunks(steps.N, self.grad_chunk_steps):
+                m = int(sel.numel())
+                b = flat[steps.vidx[sel]].contiguous()
+                if k:
+                    b = self._symmetry_boards(b, k)
+                a = steps.actions_k(sel, k).to(torch.uint8).contiguous()
+                coef = (adv[k, sel] * step_w[sel]).contiguous()
+                P = max(1, min(64, m // 8192))       # split-K of the layer-2 weight gradient over P column blocks
+                ld = -(-m // (32 * P)) * 32 * P
+                q = ld // P
+                a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
+                d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
+                L.check(self._lib.g2048_actor_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, use_mask,
+                                                   L.ptr(b), L.ptr(a), L.ptr(coef), m, ld, L.ptr(a1t), L.ptr(d2t),
+                                                   L.ptr(part), waves, self._stream))
+                big += torch.bmm(a1t.view(H1p + 1, P, q).transpose(0, 1), d2t.view(H2p, P, q).permute(1, 2, 0)).sum(0)
+                small += part.sum(0)
+        gW[0] += small[:16 * H1p].view(16, H1p)[:, :h1]
+        gb[0] += small[16 * H1p:17 * H1p][:h1]
+        gW[1] += big[:h1, :h2]
+        gb[1] += big[H1p, :h2]
+        gW[2] += small[17 * H1p:17 * H1p + 4 * H2p].view(H2p, 4)[:h2]
+        gb[2] += small[17 * H1p + 4 * H2p:]
 
     # ============================================================================================ acting
     def select_action(self, obs, rng: np.random.Generator, action_fn: Callable | None = None,
@@ -699,9 +766,10 @@ class ReinforceAgent:
         steps = _Steps(self, batch.lengths, batch.actions, batch.rewards, boards=batch.boards)
         return self._update(steps, batch.total_reward)
 
-    def _chunks(self, N: int):
-        for s in range(0, N, self.chunk_steps):
-            yield torch.arange(s, min(N, s + self.chunk_steps), device=self.device)
+    def _chunks(self, N: int, size: int | None = None):
+        size = size or self.chunk_steps
+        for s in range(0, N, size):
+            yield torch.arange(s, min(N, s + size), device=self.device)
 
     def _update(self, steps: _Steps, totals: torch.Tensor) -> dict:
         c = self.agent_config
@@ -759,10 +827,15 @@ class ReinforceAgent:
         stats["adv_std"] = float(adv.std(unbiased=False)) if adv.numel() else 0.0
 
         nW = len(self.params["W"])
+        gspec = self._fused_grad_spec() if steps.boards is not None else None
         with torch.no_grad():
-            for k in range(K):
+            if gspec is not None:
+                self._actor_grad_fused(steps, adv, step_w, K, actor_g[:nW], actor_g[nW:], gspec)
+            for k in range(K if gspec is None else 0):
                 for sel in self._chunks(steps.N):
                     x, mk = steps.features(sel, k)
+                    if steps.boards is not None and not self.env_config.use_action_mask:
+                        mk = None   # bare-board obs: unmasked probabilities, as select_action used them
                     logits, kept = mlp_forward_kept(self.params, x, self.mlp_config.activation)
                     p = logits_to_probs(logits, mk)
                     onehot = torch.nn.functional.one_hot(steps.actions_k(sel, k), 4).to(torch.float32)

@@ -242,6 +242,12 @@ __device__ __forceinline__ void mlp_logits(const NetSmem<NT1, NT2>& sm, const fl
     for (int k = 0; k < 4; k++) lg[k] = (lg[k] + __shfl_xor(lg[k], 32, 64)) + b3[k];
 }
 
+__device__ __forceinline__ uint64_t shfl64_(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint32_t mask_word_of(uint64_t b) {
     const uint32_t m = action_mask(b);   // int8[4] as one word: byte a = bit a
     return (m & 1u) | ((m & 2u) << 7) | ((m & 4u) << 14) | ((m & 8u) << 21);
@@ -587,6 +593,358 @@ void launch_pol_nt2(const PolArgs& a, int nt2, int act, int obs, int rng, int gr
     }
 }
 
+// ---------------------------------------------------------------------------------------------------- gradient
+// The actor branch of update_batch (src/reinforce_agent.py:502-555: _policy_gradient_step :328-354,
+// _backpropagation :639-678, _activation_derivative :624-636) for a batch of samples (valid steps), one wave per
+// 32 samples, fused: forward (as mlp_logits, keeping both hidden layers in registers), masked softmax,
+// g = (onehot(a) - p) * coef (coef = advantage * rank_w / (T_i * n), from the host), the output-layer delta
+// d2 = act'(a2) * (W3 g) on VALU, the input delta d1 = act'(a1) * (W2 d2) on MFMA (W2 packed by g2048_grad_pack
+// in A-fragment order; d2 tiles are its B operands register for register, like layer 2 of the forward), and the
+// small weight gradients dW1 (x^T d1), db1, dW3 (a2^T g), db3 on v_mfma_f32_16x16x4f32 through a per-wave LDS
+// transpose, accumulated per wave in LDS across the wave's sample groups.  The one large weight gradient,
+// dW2 = a1^T d2 (and db2 through a ones row), is left to a split-K GEMM over the a1^T / d2^T columns this kernel
+// writes (coalesced: the accumulator layout puts 32 consecutive samples of one unit in a lane half).
+// Packed input-delta weights: w2b [nt1][nt2][4][64][4]: lane l, k-step (t2, r = 4q + u) of output tile o1 at
+// [o1][t2][q][l][u]: W2[32 o1 + (l & 31)][32 t2 + row(r, l >> 5)].
+struct GradPackArgs {
+    const float* W2;
+    int h1, h2, nt1, nt2;
+    float* out;
+    int64_t total;
+};
+
+__global__ void __launch_bounds__(256) grad_pack_kernel(GradPackArgs a) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.total; q += (int64_t)gridDim.x * blockDim.x) {
+        const int u = (int)(q & 3), lane = (int)((q >> 2) & 63), r = 4 * (int)((q >> 8) & 3) + u;
+        const int64_t tt = q >> 10;
+        const int t2 = (int)(tt % a.nt2), o1 = (int)(tt / a.nt2);
+        const int i = 32 * o1 + (lane & 31), k = 32 * t2 + acc_row(r, lane >> 5);
+        a.out[q] = (i < a.h1 && k < a.h2) ? a.W2[(int64_t)i * a.h2 + k] : 0.0f;
+    }
+}
+
+// floats of one wave's partial gradients: dW1 [16][H1p], db1 [H1p], dW3 [H2p][4], db3 [4]
+__host__ __device__ constexpr int64_t grad_part_floats(int nt1, int nt2) { return 17 * 32 * nt1 + 4 * 32 * nt2 + 4; }
+
+struct GradArgs {
+    const float* net;        // g2048_policy_pack layout
+    const float* w2b;        // g2048_grad_pack layout
+    const uint64_t* boards;  // [n] sample boards (the obs of each step)
+    const uint8_t* actions;  // [n]
+    const float* coef;       // [n] advantage * step weight
+    float* a1t;              // [H1p + 1][ld]: a1^T and a row of ones
+    float* d2t;              // [H2p][ld]
+    float* part;             // [waves][grad_part_floats]
+    uint32_t n, ld;          // samples; columns (a multiple of 32, >= n): samples n..ld-1 have coef 0
+    float obs_scale;
+    int use_mask;
+};
+
+template <int NT1, int NT2>
+struct GradSmem {
+    static constexpr int kStage = NT1 * 4 * 64 * 4 > 32 * 33 ? NT1 * 4 * 64 * 4 : 32 * 33;   // floats per wave
+    NetSmem<NT1, NT2> net;
+    float stage[4][kStage];            // per wave: the layer-1 activations in layer-2 B-fragment order, then (after
+                                       // the forward) the backward's transpose tile [unit][sample], stride 33
+    float g[4][32][4];                 // per-wave g of the group [sample][action]
+    float db1[4][32 * NT1];            // per-wave db1 partial
+};
+
+__device__ __forceinline__ void lds_fence() {   // order this wave's LDS writes / reads (a wave's LDS ops retire in order)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int ACT>
+__device__ __forceinline__ float activation_derivative(float a) {   // from the activation (src/reinforce_agent.py:624-636)
+    if constexpr (ACT == 0) return a > 0.0f ? 1.0f : 0.0f;
+    else return a * (1.0f - a);
+}
+
+// The a1^T / d2^T column buffers are addressed as buffer resources: element (row, column) at voffset = this lane's
+// column byte offset (one VGPR for every access) + soffset = row * ld * 4 (scalar), so no per-row 64-bit vector
+// address is ever formed (those kept 2 VGPRs live per row across the whole group and spilled the large nets).
+__device__ __forceinline__ void col_store(__amdgpu_buffer_rsrc_t r, uint32_t row, uint32_t ld, uint32_t voff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, (int)(row * ld * 4u), 0);
+}
+__device__ __forceinline__ float col_load(__amdgpu_buffer_rsrc_t r, uint32_t row, uint32_t ld, uint32_t voff) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)(row * ld * 4u), 0));
+}
+// packed weight fragment `idx` (64 lanes x float4) at this lane's voffset (lane * 16): the same one-VGPR addressing
+// for the fragment streams (per-fragment 64-bit pointers were hoisted out of the group loop, 2 registers each)
+__device__ __forceinline__ float4 frag_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t idx) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)(idx * 1024u), 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+template <int NT1, int NT2, int ACT, int OBS>
+__global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
+    typedef float floatx4 __attribute__((ext_vector_type(4)));
+    constexpr int H1p = 32 * NT1, H2p = 32 * NT2;
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
+    const int l16 = lane & 15, q16 = lane >> 4;
+    __shared__ GradSmem<NT1, NT2> S;
+    S.net.load(a.net);
+    for (int k = lane; k < H1p; k += 64) S.db1[w][k] = 0.0f;
+    __syncthreads();
+    const NetSmem<NT1, NT2>& sm = S.net;
+    const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.net + NetSmem<NT1, NT2>::L.w2f), 0, NT2 * NT1 * 1024 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.w2b), 0, NT1 * NT2 * 1024 * 4,
+                                                                         0x00020000);
+    const uint32_t fvo = (uint32_t)lane * 16u;
+    float4* h1f = reinterpret_cast<float4*>(S.stage[w]);             // [t][q][lane] during the forward
+    float (*T)[33] = reinterpret_cast<float (*)[33]>(S.stage[w]);     // [unit][sample] during the backward
+    float gsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // db3 partial (lanes of half 0)
+    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc(a.a1t, 0, (int)((H1p + 1) * a.ld * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd2 = __builtin_amdgcn_make_buffer_rsrc(a.d2t, 0, (int)(H2p * a.ld * 4u), 0x00020000);
+    floatx4 dw1acc[2 * NT1], dw3acc[2 * NT2];  // dW1^T / dW3^T 16x16 accumulator blocks, across the wave's groups
+#pragma unroll
+    for (int k = 0; k < 2 * NT1; k++) dw1acc[k] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < 2 * NT2; k++) dw3acc[k] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    const uint32_t waves = gridDim.x * (kPolBlock / 64);
+    const uint32_t groups = a.ld >> 5;
+    for (uint32_t gi = blockIdx.x * (kPolBlock / 64) + w; gi < groups; gi += waves) {
+        const uint32_t j = gi * 32u + (uint32_t)col;   // this lane's sample (both halves)
+        // a compiler memory barrier per group: without it the net tensors' LDS reads (loop-invariant) are hoisted
+        // out of the group loop into hundreds of registers
+        asm volatile("" ::: "memory");
+        const uint32_t off = (j + 4u * (uint32_t)h * a.ld) * 4u;   // byte offset: column j, + acc_row's 4h rows
+        const bool valid = j < a.n;
+        const uint64_t b = valid ? a.boards[j] : 0ull;
+        const uint32_t act = valid ? a.actions[j] : 0u;
+        const float cf = valid ? a.coef[j] : 0.0f;
+        // ---- forward (mlp_logits, keeping a2 = h2); each a1 tile goes to its a1^T columns when done (a1 is
+        //      re-read from there for the input delta, so it is not held across the backward)
+        float4 fa[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) fa[q] = frag_load(rw2, fvo, q);
+        lds_fence();   // the previous group's reads of the stage are done
+        {
+            float x[8];
+#pragma unroll
+            for (int s = 0; s < 8; s++) x[s] = obs_value<OBS>(b, 2 * s + h, a.obs_scale);
+#pragma unroll
+            for (int t = 0; t < NT1; t++) {
+                floatx16 acc = {};
+#pragma unroll
+                for (int s = 0; s < 8; s++)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sm.w1f()[(t * 8 + s) * 64 + lane], x[s], acc, 0, 0, 0);
+                const float4* bb = reinterpret_cast<const float4*>(sm.b1p() + (t * 2 + h) * 16);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4 bv = bb[q];
+                    const float4 hv = make_float4(activate<ACT>(acc[4 * q + 0] + bv.x), activate<ACT>(acc[4 * q + 1] + bv.y),
+                                                  activate<ACT>(acc[4 * q + 2] + bv.z), activate<ACT>(acc[4 * q + 3] + bv.w));
+                    h1f[(t * 4 + q) * 64 + lane] = hv;
+                    col_store(ra1, 32 * t + acc_row(4 * q + 0, 0), a.ld, off, hv.x);
+                    col_store(ra1, 32 * t + acc_row(4 * q + 1, 0), a.ld, off, hv.y);
+                    col_store(ra1, 32 * t + acc_row(4 * q + 2, 0), a.ld, off, hv.z);
+                    col_store(ra1, 32 * t + acc_row(4 * q + 3, 0), a.ld, off, hv.w);
+                }
+            }
+        }
+        lds_fence();
+        if (h == 0) col_store(ra1, H1p, a.ld, j * 4u, 1.0f);   // the ones row: db2 comes out of the dW2 GEMM
+        float h2[NT2][16];
+        float lg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int o = 0; o < NT2; o++) {
+            floatx16 acc = {};
+#pragma unroll
+            for (int t = 0; t < NT1; t++) {
+                float4 fb[4];   // the next k-tile's fragments (the last one prefetches the input-delta stream)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    fb[q] = (o * NT1 + t + 1 < NT2 * NT1) ? frag_load(rw2, fvo, (o * NT1 + t + 1) * 4 + q) : frag_load(rwb, fvo, q);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4 hb = h1f[(t * 4 + q) * 64 + lane];
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, hb.x, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, hb.y, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, hb.z, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, hb.w, acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) fa[q] = fb[q];
+            }
+            const float4* bb = reinterpret_cast<const float4*>(sm.b2p() + (o * 2 + h) * 16);
+            const float4* w3 = reinterpret_cast<const float4*>(sm.w3p() + (o * 2 + h) * 64);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 bv = bb[q];
+                h2[o][4 * q + 0] = activate<ACT>(acc[4 * q + 0] + bv.x);
+                h2[o][4 * q + 1] = activate<ACT>(acc[4 * q + 1] + bv.y);
+                h2[o][4 * q + 2] = activate<ACT>(acc[4 * q + 2] + bv.z);
+                h2[o][4 * q + 3] = activate<ACT>(acc[4 * q + 3] + bv.w);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const float4 wv = w3[4 * q + u];
+                    lg[0] = fmaf(h2[o][4 * q + u], wv.x, lg[0]);
+                    lg[1] = fmaf(h2[o][4 * q + u], wv.y, lg[1]);
+                    lg[2] = fmaf(h2[o][4 * q + u], wv.z, lg[2]);
+                    lg[3] = fmaf(h2[o][4 * q + u], wv.w, lg[3]);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);   // keep the scheduler from hoisting later tiles' LDS reads
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) lg[k] = (lg[k] + __shfl_xor(lg[k], 32, 64)) + sm.b3()[k];
+        // ---- logits_to_probs (src/MLP.py:139-156) and the policy-gradient logits delta (:328-354)
+        const uint32_t mw = a.use_mask ? mask_word_of(b) : 0x01010101u;
+        float l[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) l[k] = ((mw >> (8 * k)) & 0xFFu) ? lg[k] : -1e9f;
+        const float mx = fmaxf(fmaxf(l[0], l[1]), fmaxf(l[2], l[3]));
+        float e[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) e[k] = expf(l[k] - mx);
+        const float es = ((e[0] + e[1]) + e[2]) + e[3];
+        float g[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf;
+        lds_fence();   // the previous group's reads of S.g are done
+        if (h == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                gsum[k] += g[k];
+                S.g[w][col][k] = g[k];
+            }
+        }
+        // ---- dW3 += a2^T g: per h2 tile, a2 transposed through LDS, 16x16x4 MFMAs over the 32 samples
+        //      (A = g^T [action][sample], B = a2^T [sample][unit]; only the 4 action rows are kept)
+#pragma unroll
+        for (int o = 0; o < NT2; o++) {
+            lds_fence();
+#pragma unroll
+            for (int r = 0; r < 16; r++) T[acc_row(r, h)][col] = h2[o][r];
+            lds_fence();
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) {
+                const int s = 4 * kk + q16;
+                const float av = l16 < 4 ? S.g[w][s][l16 & 3] : 0.0f;
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+                    dw3acc[2 * o + c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, T[16 * c + l16][s], dw3acc[2 * o + c], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- d2 = act'(a2) * (W3 g), in place; d2^T columns
+#pragma unroll
+        for (int o = 0; o < NT2; o++) {
+            const float4* w3 = reinterpret_cast<const float4*>(sm.w3p() + (o * 2 + h) * 64);
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const float4 wv = w3[r];
+                float dh = g[0] * wv.x;
+                dh = fmaf(g[1], wv.y, dh);
+                dh = fmaf(g[2], wv.z, dh);
+                dh = fmaf(g[3], wv.w, dh);
+                h2[o][r] = dh * activation_derivative<ACT>(h2[o][r]);
+                col_store(rd2, 32 * o + acc_row(r, 0), a.ld, off, h2[o][r]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- d1 = act'(a1) * (W2 d2) per h1 tile, then db1 and dW1 += x^T d1 (16x16x4 MFMAs: A = x^T
+        //      [feature][sample] built from the group's boards, B = d1^T [sample][unit] through LDS)
+        float xa[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const uint64_t bs = shfl64_(b, 4 * kk + q16);
+            xa[kk] = obs_value<OBS>(bs, l16, a.obs_scale);
+        }
+        float4 fw[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) fw[q] = fa[q];   // prefetched at the end of the forward
+#pragma unroll
+        for (int o1 = 0; o1 < NT1; o1++) {
+            float a1v[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) a1v[r] = col_load(ra1, 32 * o1 + acc_row(r, 0), a.ld, off);
+            floatx16 acc = {};
+#pragma unroll
+            for (int t2 = 0; t2 < NT2; t2++) {
+                float4 fb[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    fb[q] = (o1 * NT2 + t2 + 1 < NT1 * NT2) ? frag_load(rwb, fvo, (o1 * NT2 + t2 + 1) * 4 + q)
+                                                             : frag_load(rw2, fvo, q);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].x, h2[t2][4 * q + 0], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].y, h2[t2][4 * q + 1], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].z, h2[t2][4 * q + 2], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].w, h2[t2][4 * q + 3], acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) fw[q] = fb[q];
+            }
+            lds_fence();
+#pragma unroll
+            for (int r = 0; r < 16; r++) T[acc_row(r, h)][col] = acc[r] * activation_derivative<ACT>(a1v[r]);
+            lds_fence();
+            float bs = 0.0f;   // db1: unit col of this tile, samples 16h .. 16h+15, then both halves
+#pragma unroll
+            for (int s = 0; s < 16; s++) bs += T[col][16 * h + s];
+            bs += __shfl_xor(bs, 32, 64);
+            if (h == 0) S.db1[w][32 * o1 + col] += bs;
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++)
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+                    dw1acc[2 * o1 + c] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[kk], T[16 * c + l16][4 * kk + q16],
+                                                                            dw1acc[2 * o1 + c], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // ---- this wave's partial gradients
+    const uint32_t wg = blockIdx.x * (kPolBlock / 64) + w;
+    float* out = a.part + (size_t)wg * grad_part_floats(NT1, NT2);
+    lds_fence();
+#pragma unroll
+    for (int k = 0; k < 2 * NT1; k++)   // block k: h1 units 16k..16k+15; row 4 q16 + r = feature
+#pragma unroll
+        for (int r = 0; r < 4; r++) out[(4 * q16 + r) * H1p + 16 * k + l16] = dw1acc[k][r];
+    for (int k = lane; k < H1p; k += 64) out[16 * H1p + k] = S.db1[w][k];
+    if (q16 == 0) {                     // rows 0..3 = actions
+#pragma unroll
+        for (int k = 0; k < 2 * NT2; k++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) out[17 * H1p + (16 * k + l16) * 4 + r] = dw3acc[k][r];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        float v = h == 0 ? gsum[k] : 0.0f;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+        if (lane == 0) out[17 * H1p + 4 * H2p + k] = v;
+    }
+}
+
+template <int NT1, int NT2>
+void launch_grad(const GradArgs& a, int act, int obs, int grid, hipStream_t s) {
+    if (act == G2048_ACT_RELU) {
+        if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_LOG2>), dim3(grid), dim3(kPolBlock), 0, s, a);
+        else hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_RAW>), dim3(grid), dim3(kPolBlock), 0, s, a);
+    } else {
+        if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((grad_kernel<NT1, NT2, 1, G2048_OBS_LOG2>), dim3(grid), dim3(kPolBlock), 0, s, a);
+        else hipLaunchKernelGGL((grad_kernel<NT1, NT2, 1, G2048_OBS_RAW>), dim3(grid), dim3(kPolBlock), 0, s, a);
+    }
+}
+
+template <int NT1>
+void launch_grad_nt2(const GradArgs& a, int nt2, int act, int obs, int grid, hipStream_t s) {
+    switch (nt2) {
+        case 1: launch_grad<NT1, 1>(a, act, obs, grid, s); break;
+        case 2: launch_grad<NT1, 2>(a, act, obs, grid, s); break;
+        case 4: launch_grad<NT1, 4>(a, act, obs, grid, s); break;
+        default: launch_grad<NT1, 8>(a, act, obs, grid, s); break;
+    }
+}
+
 template <int NT1, int NT2, int ACT>
 void launch_roll_obs(const RolloutArgs& a, int obs, int grid, hipStream_t s) {
     if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((rollout_kernel<NT1, NT2, ACT, G2048_OBS_LOG2>), dim3(grid), dim3(kPolBlock), 0, s, a);
@@ -710,6 +1068,77 @@ int g2048_policy(const float* packed, int h1, int h2, int activation, const uint
         case 2: launch_pol_nt2<2>(a, nt2, activation, obs_mode, rng_mode, (int)grid, s); break;
         case 4: launch_pol_nt2<4>(a, nt2, activation, obs_mode, rng_mode, (int)grid, s); break;
         default: launch_pol_nt2<8>(a, nt2, activation, obs_mode, rng_mode, (int)grid, s); break;
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return pfail(G2048_EHIP, hipGetErrorString(e));
+    return G2048_OK;
+}
+
+int64_t g2048_grad_packed_size(int h1, int h2) {
+    if (h1 < 1 || h1 > 256 || h2 < 1 || h2 > 256) return -1;
+    return (int64_t)tiles_for(h1) * tiles_for(h2) * 1024;
+}
+
+int64_t g2048_grad_partial_size(int h1, int h2) {
+    if (h1 < 1 || h1 > 256 || h2 < 1 || h2 > 256) return -1;
+    return grad_part_floats(tiles_for(h1), tiles_for(h2));
+}
+
+int g2048_grad_pack(const float* W2, int h1, int h2, float* packed, int64_t packed_len, void* stream) {
+    const int64_t need = g2048_grad_packed_size(h1, h2);
+    if (need < 0) return pfail(G2048_EINVAL, "fused gradient: hidden sizes must be in 1..256");
+    if (!W2 || !packed) return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
+    if (packed_len < need) return pfail(G2048_EINVAL, "fused gradient: packed buffer too small");
+    GradPackArgs a{W2, h1, h2, tiles_for(h1), tiles_for(h2), packed, need};
+    const int grid = (int)((need + 255) / 256 < 4096 ? (need + 255) / 256 : 4096);
+    hipLaunchKernelGGL(grad_pack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return pfail(G2048_EHIP, hipGetErrorString(e));
+    return G2048_OK;
+}
+
+int g2048_actor_grad_waves(void) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0) cus = c;
+    }
+    return cus * (kPolBlock / 64);
+}
+
+int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
+                     float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions, const float* coef,
+                     int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, void* stream) {
+    if (n < 0 || ld < n || (ld & 31) || ld > ((int64_t)1 << 21)) return pfail(G2048_EINVAL, "fused gradient: bad n / ld");
+    if (g2048_grad_packed_size(h1, h2) < 0) return pfail(G2048_EINVAL, "fused gradient: hidden sizes must be in 1..256");
+    if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
+        return pfail(G2048_EINVAL, "Unsupported activation");
+    if (obs_mode != G2048_OBS_LOG2 && obs_mode != G2048_OBS_RAW)
+        return pfail(G2048_EINVAL, "fused gradient: obs_mode must be log2 or raw");
+    if (!packed || !grad_packed || !a1t || !d2t || !partials || (n > 0 && (!boards || !actions || !coef)))
+        return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
+    if (waves != g2048_actor_grad_waves()) return pfail(G2048_EINVAL, "fused gradient: waves != g2048_actor_grad_waves()");
+    GradArgs a;
+    a.net = packed;
+    a.w2b = grad_packed;
+    a.boards = boards;
+    a.actions = actions;
+    a.coef = coef;
+    a.a1t = a1t;
+    a.d2t = d2t;
+    a.part = partials;
+    a.n = (uint32_t)n;
+    a.ld = (uint32_t)ld;
+    a.obs_scale = obs_scale;
+    a.use_mask = use_mask;
+    const int grid = (int)(waves / (kPolBlock / 64));   // one workgroup per CU; every wave writes its partial row
+    const int nt1 = tiles_for(h1), nt2 = tiles_for(h2);
+    hipStream_t s = (hipStream_t)stream;
+    switch (nt1) {
+        case 1: launch_grad_nt2<1>(a, nt2, activation, obs_mode, grid, s); break;
+        case 2: launch_grad_nt2<2>(a, nt2, activation, obs_mode, grid, s); break;
+        case 4: launch_grad_nt2<4>(a, nt2, activation, obs_mode, grid, s); break;
+        default: launch_grad_nt2<8>(a, nt2, activation, obs_mode, grid, s); break;
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return pfail(G2048_EHIP, hipGetErrorString(e));

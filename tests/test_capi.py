@@ -29,7 +29,8 @@ def test_header_declares_expected_api():
     assert _declared_functions() == sorted([
         "g2048_abi_version", "g2048_last_error", "g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step",
         "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_packed_size",
-        "g2048_policy_pack", "g2048_policy", "g2048_rollout"])
+        "g2048_policy_pack", "g2048_policy", "g2048_rollout", "g2048_grad_packed_size", "g2048_grad_partial_size",
+        "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad"])
 
 
 def test_library_exports_every_declared_symbol(L):
@@ -94,6 +95,17 @@ def test_argument_validation_without_gpu(L):
     assert lib.g2048_policy(*args) == L.G2048_EINVAL and b"activation" in lib.g2048_last_error()
     args[3], args[11] = L.ACT_RELU, L.RNG_PCG64
     assert lib.g2048_policy(*args) == L.G2048_EINVAL and b"PCG64" in lib.g2048_last_error()
+    # fused actor gradient: sizes and argument checks (no launch)
+    assert lib.g2048_grad_packed_size(256, 256) == 8 * 8 * 1024 and lib.g2048_grad_packed_size(0, 5) == -1
+    assert lib.g2048_grad_partial_size(256, 256) == 17 * 256 + 4 * 256 + 4
+    assert lib.g2048_grad_partial_size(20, 40) == 17 * 32 + 4 * 64 + 4
+    assert lib.g2048_grad_pack(p, 32, 32, p, 10, None) == L.G2048_EINVAL and b"too small" in lib.g2048_last_error()
+    gargs = [p, p, 32, 32, L.ACT_RELU, L.OBS_LOG2, 1.0, 1, p, p, p, 40, 48, p, p, p, 1024, None]
+    assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL and b"ld" in lib.g2048_last_error()   # ld % 32 != 0
+    gargs[12] = 32
+    assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL   # ld < n
+    gargs[12], gargs[5] = 64, L.OBS_ONEHOT
+    assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL and b"obs_mode" in lib.g2048_last_error()
 
 
 def test_config_validation_messages():
