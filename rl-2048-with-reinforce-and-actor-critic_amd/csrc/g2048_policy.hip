@@ -719,9 +719,18 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         const float cf = valid ? a.coef[j] : 0.0f;
         // ---- forward (mlp_logits, keeping a2 = h2); each a1 tile goes to its a1^T columns when done (a1 is
         //      re-read from there for the input delta, so it is not held across the backward)
-        float4 fa[4];
+        // weight fragments: two k-tiles in flight (fa = this one, fn = the next; the one after is loaded while this
+        // tile's MFMAs run).  Stream order: the forward's (o, t) tiles, then the input-delta's (o1, t2) tiles.
+        constexpr int KF = NT2 * NT1, KB = NT1 * NT2;
+        const auto stream_frag = [&](int kt, int q) -> float4 {
+            return kt < KF ? frag_load(rw2, fvo, kt * 4 + q) : frag_load(rwb, fvo, (kt - KF) * 4 + q);
+        };
+        float4 fa[4], fn[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) fa[q] = frag_load(rw2, fvo, q);
+        for (int q = 0; q < 4; q++) {
+            fa[q] = stream_frag(0, q);
+            fn[q] = stream_frag(1, q);
+        }
         lds_fence();   // the previous group's reads of the stage are done
         {
             float x[8];
@@ -756,10 +765,9 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
             floatx16 acc = {};
 #pragma unroll
             for (int t = 0; t < NT1; t++) {
-                float4 fb[4];   // the next k-tile's fragments (the last one prefetches the input-delta stream)
+                float4 fb[4];   // k-tile kt + 2 of the stream (the last ones run into the input-delta stream)
 #pragma unroll
-                for (int q = 0; q < 4; q++)
-                    fb[q] = (o * NT1 + t + 1 < NT2 * NT1) ? frag_load(rw2, fvo, (o * NT1 + t + 1) * 4 + q) : frag_load(rwb, fvo, q);
+                for (int q = 0; q < 4; q++) fb[q] = stream_frag(o * NT1 + t + 2, q);
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const float4 hb = h1f[(t * 4 + q) * 64 + lane];
@@ -769,7 +777,10 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, hb.w, acc, 0, 0, 0);
                 }
 #pragma unroll
-                for (int q = 0; q < 4; q++) fa[q] = fb[q];
+                for (int q = 0; q < 4; q++) {
+                    fa[q] = fn[q];
+                    fn[q] = fb[q];
+                }
             }
             const float4* bb = reinterpret_cast<const float4*>(sm.b2p() + (o * 2 + h) * 16);
             const float4* w3 = reinterpret_cast<const float4*>(sm.w3p() + (o * 2 + h) * 64);
@@ -814,6 +825,11 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                 S.g[w][col][k] = g[k];
             }
         }
+        // a1 of the first h1 tile for the input delta, re-read from its columns well ahead of its use (each tile's
+        // reload is issued one tile ahead: loaded at the point of use it cost a full memory latency per register)
+        float a1n[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) a1n[r] = col_load(ra1, acc_row(r, 0), a.ld, off);
         // ---- dW3 += a2^T g: per h2 tile, a2 transposed through LDS, 16x16x4 MFMAs over the 32 samples
         //      (A = g^T [action][sample], B = a2^T [sample][unit]; only the 4 action rows are kept)
 #pragma unroll
@@ -858,20 +874,22 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         }
         float4 fw[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) fw[q] = fa[q];   // prefetched at the end of the forward
+        for (int q = 0; q < 4; q++) fw[q] = fa[q];   // input-delta k-tiles 0 and 1, prefetched by the forward
 #pragma unroll
         for (int o1 = 0; o1 < NT1; o1++) {
             float a1v[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) a1v[r] = col_load(ra1, 32 * o1 + acc_row(r, 0), a.ld, off);
+            for (int r = 0; r < 16; r++) {
+                a1v[r] = a1n[r];
+                if (o1 + 1 < NT1) a1n[r] = col_load(ra1, 32 * (o1 + 1) + acc_row(r, 0), a.ld, off);
+            }
             floatx16 acc = {};
 #pragma unroll
             for (int t2 = 0; t2 < NT2; t2++) {
                 float4 fb[4];
 #pragma unroll
-                for (int q = 0; q < 4; q++)
-                    fb[q] = (o1 * NT2 + t2 + 1 < NT1 * NT2) ? frag_load(rwb, fvo, (o1 * NT2 + t2 + 1) * 4 + q)
-                                                             : frag_load(rw2, fvo, q);
+                for (int q = 0; q < 4; q++)   // k-tile + 2 (past the end: the next group's first, harmless)
+                    fb[q] = stream_frag(KF + ((o1 * NT2 + t2 + 2) < KB ? o1 * NT2 + t2 + 2 : 0), q);
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].x, h2[t2][4 * q + 0], acc, 0, 0, 0);
@@ -880,7 +898,10 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].w, h2[t2][4 * q + 3], acc, 0, 0, 0);
                 }
 #pragma unroll
-                for (int q = 0; q < 4; q++) fw[q] = fb[q];
+                for (int q = 0; q < 4; q++) {
+                    fw[q] = fn[q];
+                    fn[q] = fb[q];
+                }
             }
             lds_fence();
 #pragma unroll
