@@ -208,7 +208,7 @@ int g2048_policy(const float* packed, int h1, int h2, int activation, const uint
  *                         [h1 x h2] in rows < h1 and the layer-2 bias gradient in row H1p);
  *   partials [waves x g2048_grad_partial_size]  per-wave sums: dW1 [16][H1p], db1 [H1p], dW3 [H2p][4], db3 [4].
  * H1p / H2p = hidden sizes rounded up to 32, 64, 128 or 256; ld a multiple of 32, n <= ld < 2^26;
- * waves = g2048_actor_grad_waves() (every wave writes its row). */
+ * waves = g2048_actor_grad_waves() (every wave writes its row); ld < 2^21 (< 2 GB column buffers). */
 int64_t g2048_grad_packed_size(int h1, int h2);
 int64_t g2048_grad_partial_size(int h1, int h2);
 /* Pack W2 [h1 x h2] (src/MLP.py layout) for the input-delta product; re-pack after every update. */
@@ -217,6 +217,15 @@ int g2048_actor_grad_waves(void);
 int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
                      float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions, const float* coef,
                      int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, void* stream);
+/* The critic branch of update_batch (src/reinforce_agent.py:403-498, _get_grad_logits_critic :884-910) on the same
+ * kernel: the critic packed like the actor with its value head [h2 x 1] / [1] as output 0 of a 4-wide layer (outputs
+ * 1..3 zero); per sample the value V(s), the TD error delta_out = target - V (target = r + gamma V(s') m from the
+ * host), and dL/dV = (V - target) (loss 0, MSE) or its Huber clip at huber_delta (loss 1), times weight[i];
+ * the outputs as for g2048_actor_grad (only column / entry 0 of dW3 / db3 is the value head's). */
+int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
+                      float obs_scale, int loss, float huber_delta, const uint64_t* boards, const float* target,
+                      const float* weight, float* delta_out, int64_t n, int64_t ld, float* a1t, float* d2t,
+                      float* partials, int64_t waves, void* stream);
 
 /* The whole batched rollout in one launch: ReinforceAgent.run_episode (src/reinforce_agent.py:195-252) for n
  * (env_seed, policy_seed) pairs -- select_action (the fused policy above) + Game2048Env.step until terminated or

@@ -99,9 +99,10 @@ def _declare(L):
     L.g2048_grad_pack.argtypes = [vp, i32, i32, vp, i64, vp]
     L.g2048_actor_grad_waves.argtypes = []
     L.g2048_actor_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, vp, vp, vp, i64, i64, vp, vp, vp, i64, vp]
+    L.g2048_critic_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, f, vp, vp, vp, vp, i64, i64, vp, vp, vp, i64, vp]
     for name in ("g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step", "g2048_obs", "g2048_move",
                  "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy",
-                 "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad"):
+                 "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad"):
         getattr(L, name).restype = ctypes.c_int
 
 
@@ -109,7 +110,7 @@ EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g204
                     "g2048_step", "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries",
                     "g2048_policy_packed_size", "g2048_policy_pack", "g2048_policy", "g2048_rollout",
                     "g2048_grad_packed_size", "g2048_grad_partial_size", "g2048_grad_pack", "g2048_actor_grad_waves",
-                    "g2048_actor_grad")
+                    "g2048_actor_grad", "g2048_critic_grad")
 
 
 def lib():

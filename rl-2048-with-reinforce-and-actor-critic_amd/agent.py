@@ -202,11 +202,8 @@ class ReinforceAgent:
         # update_batch's actor gradient through the fused g2048_actor_grad kernel when the net fits it (batched path)
         self.use_fused_grad = True
         self.grad_chunk_steps = 1 << 20
-        self._gpacked: torch.Tensor | None = None
-        self._gpack_key = None
+        self._pack_cache: dict[str, list] = {}
         self._params_version = 0
-        self._packed: torch.Tensor | None = None
-        self._pack_key = None
         self._vec_cache: dict = {}
         self._lib = L.lib()
         self.last_stats: dict = {}
@@ -340,11 +337,18 @@ class ReinforceAgent:
         """The same net check for g2048_actor_grad (else the batched torch backprop runs)."""
         return self._net_spec() if self.use_fused_grad else None
 
-    def _net_spec(self):
+    def _fused_critic_spec(self):
+        """... and for the critic (value head of width 1) through g2048_critic_grad."""
+        if not self.use_fused_grad or self.critic_params is None:
+            return None
+        return self._net_spec(self.critic_params, 1)
+
+    def _net_spec(self, params=None, out_dim: int = 4):
         if self.env_config.obs_mode not in ("log2", "raw"):
             return None
-        Ws, bs = self.params["W"], self.params["b"]
-        if len(Ws) != 3 or len(bs) != 3 or tuple(Ws[0].shape)[0] != 16 or tuple(Ws[2].shape)[1] != 4:
+        params = self.params if params is None else params
+        Ws, bs = params["W"], params["b"]
+        if len(Ws) != 3 or len(bs) != 3 or tuple(Ws[0].shape)[0] != 16 or tuple(Ws[2].shape)[1] != out_dim:
             return None
         h1, h2 = int(Ws[0].shape[1]), int(Ws[1].shape[1])
         act = {"ReLU": L.ACT_RELU, "Sigmoid": L.ACT_SIGMOID}.get(self.mlp_config.activation)
@@ -358,31 +362,31 @@ class ReinforceAgent:
     def _packed_policy(self, spec) -> torch.Tensor:
         """The actor packed in MFMA fragment order (g2048_policy_pack), re-packed whenever a parameter tensor is
         replaced or modified in place (or after an update / load)."""
-        Ws, bs = self.params["W"], self.params["b"]
-        key = (self._params_version,) + tuple((t.data_ptr(), t._version) for t in Ws + bs)
-        if key != self._pack_key:
-            h1, h2, _ = spec
-            size = int(self._lib.g2048_policy_packed_size(h1, h2))
-            if self._packed is None or self._packed.numel() < size:
-                self._packed = torch.empty(size, dtype=torch.float32, device=self.device)
-            w = [t.contiguous() for t in (Ws[0], bs[0], Ws[1], bs[1], Ws[2], bs[2])]
-            L.check(self._lib.g2048_policy_pack(*[L.ptr(t) for t in w], 16, h1, h2, L.ptr(self._packed), size,
-                                                self._stream))
-            self._pack_key = key
-        return self._packed
+        return self._pack_net(self.params, spec, "actor")
 
-    def _grad_packed(self, spec) -> torch.Tensor:
-        """W2 packed for the fused gradient's input-delta product (g2048_grad_pack), re-packed like the policy."""
-        W = self.params["W"][1]
-        key = (self._params_version, W.data_ptr(), W._version)
-        if key != self._gpack_key:
+    def _pack_net(self, params, spec, slot: str, grad: bool = False) -> torch.Tensor:
+        """g2048_policy_pack (grad=False) or g2048_grad_pack of W[1] (grad=True) of a two-hidden-layer net, cached
+        per slot until a parameter tensor changes; a value head [h2, 1] / [1] is packed as output 0 of 4."""
+        Ws, bs = params["W"], params["b"]
+        key = (self._params_version,) + tuple((t.data_ptr(), t._version) for t in Ws + bs)
+        entry = self._pack_cache.setdefault(slot + ("/grad" if grad else ""), [None, None])
+        if key != entry[1]:
             h1, h2, _ = spec
-            size = int(self._lib.g2048_grad_packed_size(h1, h2))
-            if self._gpacked is None or self._gpacked.numel() < size:
-                self._gpacked = torch.empty(size, dtype=torch.float32, device=self.device)
-            L.check(self._lib.g2048_grad_pack(L.ptr(W.contiguous()), h1, h2, L.ptr(self._gpacked), size, self._stream))
-            self._gpack_key = key
-        return self._gpacked
+            size = int(self._lib.g2048_grad_packed_size(h1, h2) if grad else self._lib.g2048_policy_packed_size(h1, h2))
+            if entry[0] is None or entry[0].numel() < size:
+                entry[0] = torch.empty(size, dtype=torch.float32, device=self.device)
+            if grad:
+                L.check(self._lib.g2048_grad_pack(L.ptr(Ws[1].contiguous()), h1, h2, L.ptr(entry[0]), size, self._stream))
+            else:
+                W3, b3 = Ws[2], bs[2]
+                if W3.shape[1] != 4:
+                    W3 = torch.nn.functional.pad(W3, (0, 4 - W3.shape[1]))
+                    b3 = torch.nn.functional.pad(b3, (0, 4 - b3.shape[0]))
+                w = [t.contiguous() for t in (Ws[0], bs[0], Ws[1], bs[1], W3, b3)]
+                L.check(self._lib.g2048_policy_pack(*[L.ptr(t) for t in w], 16, h1, h2, L.ptr(entry[0]), size,
+                                                    self._stream))
+            entry[1] = key
+        return entry[0]
 
     def _actor_grad_fused(self, steps: "_Steps", adv: torch.Tensor, step_w: torch.Tensor, K: int,
                           gW: list[torch.Tensor], gb: list[torch.Tensor], spec) -> None:
@@ -390,16 +394,61 @@ class ReinforceAgent:
         g2048_actor_grad (forward from the bitboards, masked softmax, deltas, dW1 / db1 / dW3 / db3 per wave)
         plus one split-K GEMM for the layer-2 weight and bias gradient over the a1^T / d2^T columns the kernel
         writes.  Accumulates into gW / gb like mlp_backward_."""
+        use_mask = int(bool(self.env_config.use_action_mask))
+
+        def launch(k, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale):
+            a = steps.actions_k(sel, k).to(torch.uint8).contiguous()
+            coef = (adv[k, sel] * step_w[sel]).contiguous()
+            L.check(self._lib.g2048_actor_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, use_mask,
+                                               L.ptr(b), L.ptr(a), L.ptr(coef), m, ld, L.ptr(a1t), L.ptr(d2t),
+                                               L.ptr(part), waves, self._stream))
+
+        self._fused_grad(self.params, "actor", spec, steps, K, gW, gb, 4, launch)
+
+    def _critic_grad_fused(self, steps: "_Steps", step_w: torch.Tensor, K: int, gW: list[torch.Tensor],
+                           gb: list[torch.Tensor], deltas: torch.Tensor, spec) -> None:
+        """The critic branch of update_batch (src/reinforce_agent.py:403-498, _get_grad_logits_critic :884-910):
+        V(s') of every step with a successor by the fused forward (g2048_policy, logits only), the TD target
+        r + gamma V(s') m on the device, then g2048_critic_grad (value, TD error into `deltas`, loss gradient and
+        backprop) and the same split-K GEMM as the actor."""
+        c = self.agent_config
+        loss = {"mse": 0, "huber": 1}[c.critic_loss_type]
+        flat = steps.boards.reshape(-1)
+
+        def launch(k, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale):
+            fi, hn = steps.vidx[sel], steps.has_next[sel]
+            bn = flat[torch.where(hn, fi + steps.n, fi)].contiguous()
+            if k:
+                bn = self._symmetry_boards(bn, k)
+            lg = torch.empty(m, 4, dtype=torch.float32, device=self.device)
+            dummy = torch.empty(m, dtype=torch.uint8, device=self.device)
+            L.check(self._lib.g2048_policy(L.ptr(packed), h1, h2, act, L.ptr(bn), None, None, obs_code, scale, 0, 1,
+                                           L.RNG_PCG64, None, None, None, 0, None, None, None, L.ptr(lg), L.ptr(dummy),
+                                           m, self._stream))
+            tgt = (steps.rewards[sel] + (float(c.gamma) * lg[:, 0]) * hn.to(torch.float32)).contiguous()
+            w = step_w[sel].contiguous()
+            s0 = int(sel[0])
+            L.check(self._lib.g2048_critic_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, loss,
+                                                float(c.huber_delta), L.ptr(b), L.ptr(tgt), L.ptr(w),
+                                                L.ptr(deltas[k, s0:s0 + m]), m, ld, L.ptr(a1t), L.ptr(d2t), L.ptr(part),
+                                                waves, self._stream))
+
+        self._fused_grad(self.critic_params, "critic", spec, steps, K, gW, gb, 1, launch)
+
+    def _fused_grad(self, params, slot: str, spec, steps: "_Steps", K: int, gW: list[torch.Tensor],
+                    gb: list[torch.Tensor], out_dim: int, launch) -> None:
+        """Chunked driver of the fused gradient kernels: per chunk of valid steps (symmetry k) `launch` runs the
+        kernel, then the layer-2 weight + bias gradient a1^T d2 is one split-K strided-batched GEMM and the
+        per-wave partials are summed; the padded gradients are cut to the net's shapes at the end."""
         h1, h2, act = spec
         H1p, H2p = (32 * min(8, 1 << max(0, (h - 1) // 32).bit_length()) for h in (h1, h2))
-        packed, gpacked = self._packed_policy(spec), self._grad_packed(spec)
+        packed, gpacked = self._pack_net(params, spec, slot), self._pack_net(params, spec, slot, grad=True)
         waves = int(self._lib.g2048_actor_grad_waves())
         pf = int(self._lib.g2048_grad_partial_size(h1, h2))
         part = torch.empty(waves, pf, dtype=torch.float32, device=self.device)
         small = torch.zeros(pf, dtype=torch.float32, device=self.device)
         big = torch.zeros(H1p + 1, H2p, dtype=torch.float32, device=self.device)
         obs_code, scale = _OBS_CODE[self.env_config.obs_mode], float(self.env_config.obs_log2_scale)
-        use_mask = int(bool(self.env_config.use_action_mask))
         flat = steps.boards.reshape(-1)
         for k in range(K):
             for sel in self._chunks(steps.N, self.grad_chunk_steps):
@@ -407,24 +456,20 @@ class ReinforceAgent:
                 b = flat[steps.vidx[sel]].contiguous()
                 if k:
                     b = self._symmetry_boards(b, k)
-                a = steps.actions_k(sel, k).to(torch.uint8).contiguous()
-                coef = (adv[k, sel] * step_w[sel]).contiguous()
                 P = max(1, min(64, m // 8192))       # split-K of the layer-2 weight gradient over P column blocks
                 ld = -(-m // (32 * P)) * 32 * P
                 q = ld // P
                 a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
                 d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
-                L.check(self._lib.g2048_actor_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, use_mask,
-                                                   L.ptr(b), L.ptr(a), L.ptr(coef), m, ld, L.ptr(a1t), L.ptr(d2t),
-                                                   L.ptr(part), waves, self._stream))
+                launch(k, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale)
                 big += torch.bmm(a1t.view(H1p + 1, P, q).transpose(0, 1), d2t.view(H2p, P, q).permute(1, 2, 0)).sum(0)
                 small += part.sum(0)
         gW[0] += small[:16 * H1p].view(16, H1p)[:, :h1]
         gb[0] += small[16 * H1p:17 * H1p][:h1]
         gW[1] += big[:h1, :h2]
         gb[1] += big[H1p, :h2]
-        gW[2] += small[17 * H1p:17 * H1p + 4 * H2p].view(H2p, 4)[:h2]
-        gb[2] += small[17 * H1p + 4 * H2p:]
+        gW[2] += small[17 * H1p:17 * H1p + 4 * H2p].view(H2p, 4)[:h2, :out_dim]
+        gb[2] += small[17 * H1p + 4 * H2p:][:out_dim]
 
     # ============================================================================================ acting
     def select_action(self, obs, rng: np.random.Generator, action_fn: Callable | None = None,
@@ -789,7 +834,12 @@ class ReinforceAgent:
             critic_g = [torch.zeros_like(p) for p in self.critic_params["W"] + self.critic_params["b"]]
             deltas = torch.empty(K, steps.N, dtype=torch.float32, device=self.device)
             ncW = len(self.critic_params["W"])
-            for k in range(K):
+            cspec = (self._fused_critic_spec() if steps.boards is not None and c.critic_loss_type in ("mse", "huber")
+                     else None)
+            if cspec is not None:
+                with torch.no_grad():
+                    self._critic_grad_fused(steps, step_w, K, critic_g[:ncW], critic_g[ncW:], deltas, cspec)
+            for k in range(K if cspec is None else 0):
                 for sel in self._chunks(steps.N):
                     x, _ = steps.features(sel, k)
                     with torch.no_grad():

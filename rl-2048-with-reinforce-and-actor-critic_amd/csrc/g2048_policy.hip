@@ -638,6 +638,12 @@ struct GradArgs {
     uint32_t n, ld;          // samples; columns (a multiple of 32, >= n): samples n..ld-1 have coef 0
     float obs_scale;
     int use_mask;
+    // critic mode (value head = output 0 of the packed net, outputs 1..3 zero): g0 = dL/dV * coef with
+    // L = MSE or Huber on V - target; delta_out = target - V (the TD error)
+    int critic, huber;
+    float huber_delta;
+    const float* target;     // [n]
+    float* delta_out;        // [n] or NULL
 };
 
 template <int NT1, int NT2>
@@ -715,7 +721,7 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         const uint32_t off = (j + 4u * (uint32_t)h * a.ld) * 4u;   // byte offset: column j, + acc_row's 4h rows
         const bool valid = j < a.n;
         const uint64_t b = valid ? a.boards[j] : 0ull;
-        const uint32_t act = valid ? a.actions[j] : 0u;
+        const uint32_t act = (valid && !a.critic) ? a.actions[j] : 0u;   // no actions in critic mode
         const float cf = valid ? a.coef[j] : 0.0f;
         // ---- forward (mlp_logits, keeping a2 = h2); each a1 tile goes to its a1^T columns when done (a1 is
         //      re-read from there for the input delta, so it is not held across the backward)
@@ -804,19 +810,29 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) lg[k] = (lg[k] + __shfl_xor(lg[k], 32, 64)) + sm.b3()[k];
-        // ---- logits_to_probs (src/MLP.py:139-156) and the policy-gradient logits delta (:328-354)
-        const uint32_t mw = a.use_mask ? mask_word_of(b) : 0x01010101u;
-        float l[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) l[k] = ((mw >> (8 * k)) & 0xFFu) ? lg[k] : -1e9f;
-        const float mx = fmaxf(fmaxf(l[0], l[1]), fmaxf(l[2], l[3]));
-        float e[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) e[k] = expf(l[k] - mx);
-        const float es = ((e[0] + e[1]) + e[2]) + e[3];
         float g[4];
+        if (!a.critic) {
+            // ---- logits_to_probs (src/MLP.py:139-156) and the policy-gradient logits delta (:328-354)
+            const uint32_t mw = a.use_mask ? mask_word_of(b) : 0x01010101u;
+            float l[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf;
+            for (int k = 0; k < 4; k++) l[k] = ((mw >> (8 * k)) & 0xFFu) ? lg[k] : -1e9f;
+            const float mx = fmaxf(fmaxf(l[0], l[1]), fmaxf(l[2], l[3]));
+            float e[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) e[k] = expf(l[k] - mx);
+            const float es = ((e[0] + e[1]) + e[2]) + e[3];
+#pragma unroll
+            for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf;
+        } else {
+            // ---- the critic's value-loss gradient (update_batch :403-498, _get_grad_logits_critic :884-910)
+            const float tg = valid ? a.target[j] : 0.0f;
+            const float diff = lg[0] - tg;
+            const float gd = (a.huber && fabsf(diff) > a.huber_delta) ? copysignf(a.huber_delta, diff) : diff;
+            g[0] = gd * cf;
+            g[1] = g[2] = g[3] = 0.0f;
+            if (valid && h == 0 && a.delta_out) a.delta_out[j] = tg - lg[0];
+        }
         lds_fence();   // the previous group's reads of S.g are done
         if (h == 0) {
 #pragma unroll
@@ -1127,16 +1143,19 @@ int g2048_actor_grad_waves(void) {
     return cus * (kPolBlock / 64);
 }
 
-int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
-                     float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions, const float* coef,
-                     int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, void* stream) {
+// the actor and critic entry points share one kernel (GradArgs::critic selects the loss gradient)
+static int actor_or_critic_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
+                         float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions,
+                         const float* coef, int64_t n, int64_t ld, float* a1t, float* d2t, float* partials,
+                         int64_t waves, void* stream, int critic, int huber, float huber_delta, const float* target,
+                         float* delta_out) {
     if (n < 0 || ld < n || (ld & 31) || ld > ((int64_t)1 << 21)) return pfail(G2048_EINVAL, "fused gradient: bad n / ld");
     if (g2048_grad_packed_size(h1, h2) < 0) return pfail(G2048_EINVAL, "fused gradient: hidden sizes must be in 1..256");
     if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
         return pfail(G2048_EINVAL, "Unsupported activation");
     if (obs_mode != G2048_OBS_LOG2 && obs_mode != G2048_OBS_RAW)
         return pfail(G2048_EINVAL, "fused gradient: obs_mode must be log2 or raw");
-    if (!packed || !grad_packed || !a1t || !d2t || !partials || (n > 0 && (!boards || !actions || !coef)))
+    if (!packed || !grad_packed || !a1t || !d2t || !partials || (n > 0 && (!boards || !coef)))
         return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
     if (waves != g2048_actor_grad_waves()) return pfail(G2048_EINVAL, "fused gradient: waves != g2048_actor_grad_waves()");
     GradArgs a;
@@ -1152,6 +1171,11 @@ int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int 
     a.ld = (uint32_t)ld;
     a.obs_scale = obs_scale;
     a.use_mask = use_mask;
+    a.critic = critic;
+    a.huber = huber;
+    a.huber_delta = huber_delta;
+    a.target = target;
+    a.delta_out = delta_out;
     const int grid = (int)(waves / (kPolBlock / 64));   // one workgroup per CU; every wave writes its partial row
     const int nt1 = tiles_for(h1), nt2 = tiles_for(h2);
     hipStream_t s = (hipStream_t)stream;
@@ -1164,6 +1188,24 @@ int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int 
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return pfail(G2048_EHIP, hipGetErrorString(e));
     return G2048_OK;
+}
+
+int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
+                     float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions, const float* coef,
+                     int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, void* stream) {
+    if (n > 0 && !actions) return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
+    return actor_or_critic_grad(packed, grad_packed, h1, h2, activation, obs_mode, obs_scale, use_mask, boards, actions,
+                                coef, n, ld, a1t, d2t, partials, waves, stream, 0, 0, 0.0f, nullptr, nullptr);
+}
+
+int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
+                      float obs_scale, int loss, float huber_delta, const uint64_t* boards, const float* target,
+                      const float* weight, float* delta_out, int64_t n, int64_t ld, float* a1t, float* d2t,
+                      float* partials, int64_t waves, void* stream) {
+    if (loss != 0 && loss != 1) return pfail(G2048_EINVAL, "Unknown critic loss type");
+    if (n > 0 && !target) return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
+    return actor_or_critic_grad(packed, grad_packed, h1, h2, activation, obs_mode, obs_scale, 0, boards, nullptr, weight,
+                                n, ld, a1t, d2t, partials, waves, stream, 1, loss, huber_delta, target, delta_out);
 }
 
 int g2048_rollout(const float* packed, int h1, int h2, int activation, const g2048_env_cfg* cfg, int greedy,

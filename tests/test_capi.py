@@ -30,7 +30,7 @@ def test_header_declares_expected_api():
         "g2048_abi_version", "g2048_last_error", "g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step",
         "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_packed_size",
         "g2048_policy_pack", "g2048_policy", "g2048_rollout", "g2048_grad_packed_size", "g2048_grad_partial_size",
-        "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad"])
+        "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad"])
 
 
 def test_library_exports_every_declared_symbol(L):
@@ -106,6 +106,8 @@ def test_argument_validation_without_gpu(L):
     assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL   # ld < n
     gargs[12], gargs[5] = 64, L.OBS_ONEHOT
     assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL and b"obs_mode" in lib.g2048_last_error()
+    cargs = [p, p, 32, 32, L.ACT_RELU, L.OBS_LOG2, 1.0, 2, 1.0, p, p, p, None, 40, 64, p, p, p, 1024, None]
+    assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"critic loss" in lib.g2048_last_error()
 
 
 def test_config_validation_messages():

@@ -59,6 +59,38 @@ def test_fused_actor_grad_matches_batched_backprop(case):
         assert _rel(a, b) < 1e-5, (i, _rel(a, b))
 
 
+CRITIC_CASES = [
+    dict(hidden=(256, 256), act="ReLU", obs_mode="log2", critic_loss_type="mse", episodes=64),
+    dict(hidden=(48, 32), act="Sigmoid", obs_mode="raw", critic_loss_type="huber", huber_delta=0.5, episodes=48),
+    dict(hidden=(96, 200), act="ReLU", obs_mode="log2", critic_loss_type="huber", huber_delta=2.0, episodes=32,
+         augmentation=True),
+]
+
+
+@pytest.mark.parametrize("case", CRITIC_CASES, ids=lambda c: f"{c['hidden']}-{c['act']}-{c['critic_loss_type']}")
+def test_fused_critic_grad_matches_batched_backprop(case):
+    """The critic branch (V(s'), TD target, TD errors -> actor advantages, MSE / Huber gradient) through
+    g2048_critic_grad equals the batched torch backprop: critic and actor pre-clip gradients within 1e-5."""
+    case = dict(case)
+    n = case.pop("episodes")
+    hidden, act, obs_mode = case.pop("hidden"), case.pop("act"), case.pop("obs_mode")
+    acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.97, use_critic=True, **case)
+    grads = {}
+    batch = None
+    for fused in (True, False):
+        ag = _agent(hidden, act, obs_mode=obs_mode, **acfg)
+        ag.use_fused_grad = fused
+        if batch is None:
+            batch = ag.rollout_batch(list(range(700, 700 + n)), list(range(1700, 1700 + n)))
+        ag.grad_chunk_steps = 1 << 12
+        ag.update_from_batch(batch)
+        grads[fused] = ([g.cpu().numpy() for g in ag.last_grads["critic"]],
+                        [g.cpu().numpy() for g in ag.last_grads["actor"]])
+    for which in (0, 1):
+        for i, (a, b) in enumerate(zip(grads[True][which], grads[False][which])):
+            assert _rel(a, b) < 1e-5, ("critic" if which == 0 else "actor", i, _rel(a, b))
+
+
 def test_update_matches_oracle_unmasked():
     """update_batch with use_action_mask off (bare-board obs): the device update, with the fused gradient, equals
     the numpy restatement with unmasked probabilities.  (The reference's own update_batch cannot run this case:
