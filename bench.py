@@ -222,17 +222,18 @@ def policy_rollout_rate(torch, B: int, device, steps: int = 20, warmup: int = 5,
             "path": path, "policy_tflops": steps * B * POLICY_FLOP_PER_BOARD / dt / 1e12}
 
 
-def train_iteration_rate(torch, device, episodes: int = 65536, repeats: int = 2) -> dict:
-    """One training iteration of configs[1] (65,536 parallel boards, REINFORCE + the runner-default MLP): the
-    batched rollout of one episode per lane (fused policy kernel + env step) and update_from_batch (batched manual
-    backprop of update_batch, fp32), timed separately; the last of `repeats` iterations after one warm-up."""
+def train_iteration_rate(torch, device, episodes: int = 65536, repeats: int = 2, critic: bool = False) -> dict:
+    """One training iteration of configs[1] (65,536 parallel boards, REINFORCE + the runner-default MLP) or, with
+    critic=True, of configs[2]'s actor-critic: the batched rollout of one episode per lane (g2048_rollout: fused
+    policy + env step) and update_from_batch (fused actor / critic gradient kernels + the layer-2 GEMM, fp32),
+    timed separately; the last of `repeats` iterations after one warm-up."""
     from rl2048_amd import Game2048EnvConfig
     from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
     from rl2048_amd.mlp import MLPConfig
 
     agent = ReinforceAgent(Game2048EnvConfig(), MLPConfig(hidden_sizes=[256, 256], activation="ReLU",
                                                           init_distribution="HeNormal"),
-                           ReinforceAgentConfig(baseline_mode="batch"), device=device)
+                           ReinforceAgentConfig(baseline_mode="batch", use_critic=critic), device=device)
     out = {}
     for rep in range(repeats + 1):
         base = 1000 + rep * episodes
@@ -248,8 +249,11 @@ def train_iteration_rate(torch, device, episodes: int = 65536, repeats: int = 2)
         samples = int(batch.lengths.sum())
         out = {"episodes": episodes, "env_steps": samples, "longest_episode": batch.T, "rollout_s": t1 - t0,
                "update_s": t2 - t1, "iteration_s": t2 - t0, "env_steps_per_s": samples / (t2 - t0),
-               "update_tflops": samples * UPDATE_FLOP_PER_SAMPLE / (t2 - t1) / 1e12,
-               "model": "REINFORCE, MLP 16-256-256-4 ReLU fp32, batch baseline (runner.py defaults)"}
+               "model": ("actor-critic (critic MSE on TD errors)" if critic else "REINFORCE") +
+                        ", MLP 16-256-256-4 ReLU fp32, batch baseline (runner.py defaults)"}
+        if not critic:
+            out["update_tflops"] = samples * UPDATE_FLOP_PER_SAMPLE / (t2 - t1) / 1e12
+        del batch
     return out
 
 
@@ -337,6 +341,9 @@ def main():
             policy = policy_rollout_rate(torch, B, device)
             policy["gemm_path"] = policy_rollout_rate(torch, B, device, fused=False)
             policy["train_iteration_configs1"] = train_iteration_rate(torch, device)
+            # configs[2]: 1,048,576 parallel boards, actor-critic (one warm-up, one timed iteration)
+            policy["train_iteration_configs2"] = train_iteration_rate(torch, device, episodes=1 << 20, repeats=1,
+                                                                      critic=True)
         except Exception as e:  # noqa: BLE001 -- an extra, never the headline
             policy = {"error": repr(e)}
     if world > 1:
