@@ -103,6 +103,13 @@ def _board_values(b: int) -> np.ndarray:
     return np.where(e > 0, np.left_shift(np.int64(1), e), 0).astype(np.int64)
 
 
+def _padded_units(h: int) -> int:
+    """Hidden units as the fused kernels pad them: whole 32-unit MFMA tiles, 1, 2, 4 or 8 of them (tiles_for in
+    csrc/g2048_policy.hip)."""
+    t = (h + 31) // 32
+    return 32 * (1 if t <= 1 else 2 if t <= 2 else 4 if t <= 4 else 8)
+
+
 class _Steps:
     """The valid steps of a batch in time-major order plus how to build their MLP inputs.
 
@@ -441,7 +448,7 @@ class ReinforceAgent:
         kernel, then the layer-2 weight + bias gradient a1^T d2 is one split-K strided-batched GEMM and the
         per-wave partials are summed; the padded gradients are cut to the net's shapes at the end."""
         h1, h2, act = spec
-        H1p, H2p = (32 * min(8, 1 << max(0, (h - 1) // 32).bit_length()) for h in (h1, h2))
+        H1p, H2p = _padded_units(h1), _padded_units(h2)
         packed, gpacked = self._pack_net(params, spec, slot), self._pack_net(params, spec, slot, grad=True)
         waves = int(self._lib.g2048_actor_grad_waves())
         pf = int(self._lib.g2048_grad_partial_size(h1, h2))
