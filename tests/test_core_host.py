@@ -23,7 +23,9 @@ def ch():
     src = os.path.join(NATIVE, "core_host.cpp")
     hdr = os.path.join(CSRC, "g2048_core.h")
     if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
-        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I" + CSRC, "-o", so, src], check=True)
+        tmp = f"{so}.{os.getpid()}.tmp"   # build aside, then rename: parallel workers never load a partial file
+        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I" + CSRC, "-o", tmp, src], check=True)
+        os.replace(tmp, so)
     L = ctypes.CDLL(so)
     u32p = ctypes.POINTER(ctypes.c_uint32)
     L.ch_board_move.restype = ctypes.c_uint64
