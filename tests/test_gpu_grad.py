@@ -91,6 +91,31 @@ def test_fused_critic_grad_matches_batched_backprop(case):
             assert _rel(a, b) < 1e-5, ("critic" if which == 0 else "actor", i, _rel(a, b))
 
 
+@pytest.mark.parametrize("critic", [False, True], ids=["actor", "actor_critic"])
+def test_fused_grad_one_large_chunk_split_k(critic):
+    """One chunk of > 2^17 samples (the default chunk size, so a single launch): the layer-2 weight gradient then runs
+    as a split-K batched GEMM over P = m // 8192 > 16 column blocks of a1^T / d2^T (the small-batch cases above use
+    P = 1), and the kernel's column buffers are wide (ld > 2^17).  Gradients within 1e-5 of the torch backprop."""
+    acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.99)
+    if critic:
+        acfg.update(use_critic=True, critic_loss_type="mse")
+    grads = {}
+    batch = None
+    for fused in (True, False):
+        ag = _agent((256, 256), "ReLU", **acfg)
+        ag.use_fused_grad = fused
+        if batch is None:
+            batch = ag.rollout_batch(list(range(4000, 6048)), list(range(9000, 11048)))
+        ag.update_from_batch(batch)
+        grads[fused] = {k: [g.cpu().numpy() for g in v] for k, v in ag.last_grads.items() if v is not None}
+    assert set(grads[True]) == ({"actor", "critic"} if critic else {"actor"})
+    m = int(batch.lengths.sum())
+    assert m > 17 * 8192 and m <= ag.grad_chunk_steps, m
+    for which, gs in grads[True].items():
+        for i, (a, b) in enumerate(zip(gs, grads[False][which])):
+            assert _rel(a, b) < 1e-5, (which, i, _rel(a, b))
+
+
 def test_update_matches_oracle_unmasked():
     """update_batch with use_action_mask off (bare-board obs): the device update, with the fused gradient, equals
     the numpy restatement with unmasked probabilities.  (The reference's own update_batch cannot run this case:
