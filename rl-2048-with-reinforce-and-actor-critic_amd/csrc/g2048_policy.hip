@@ -728,8 +728,8 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         // weight fragments: two k-tiles in flight (fa = this one, fn = the next; the one after is loaded while this
         // tile's MFMAs run).  Stream order: the forward's (o, t) tiles, then the input-delta's (o1, t2) tiles.
         constexpr int KF = NT2 * NT1, KB = NT1 * NT2;
-        const auto stream_frag = [&](int kt, int q) -> float4 {
-            return kt < KF ? frag_load(rw2, fvo, kt * 4 + q) : frag_load(rwb, fvo, (kt - KF) * 4 + q);
+        const auto stream_frag = [&](int kt, int q) -> float4 {   // k-tiles past the stream's end re-read tile 0
+            return kt < KF ? frag_load(rw2, fvo, kt * 4 + q) : frag_load(rwb, fvo, (kt - KF < KB ? kt - KF : 0) * 4 + q);
         };
         float4 fa[4], fn[4];
 #pragma unroll
@@ -904,8 +904,8 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
             for (int t2 = 0; t2 < NT2; t2++) {
                 float4 fb[4];
 #pragma unroll
-                for (int q = 0; q < 4; q++)   // k-tile + 2 (past the end: the next group's first, harmless)
-                    fb[q] = stream_frag(KF + ((o1 * NT2 + t2 + 2) < KB ? o1 * NT2 + t2 + 2 : 0), q);
+                for (int q = 0; q < 4; q++)   // k-tile + 2 (past the end: tile 0 again, unused)
+                    fb[q] = stream_frag(KF + o1 * NT2 + t2 + 2, q);
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].x, h2[t2][4 * q + 0], acc, 0, 0, 0);
