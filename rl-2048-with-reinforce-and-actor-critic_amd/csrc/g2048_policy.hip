@@ -34,6 +34,9 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // layer 2 + barrier, logits + choice + env step, claims; [4] = steps
 constexpr int kRollDiagBlocks = 4096;
 __device__ unsigned long long g_roll_ph[kRollDiagBlocks * 5];
+// per-workgroup (wave 0) sums of grad_kernel phase durations: layer 1 (+ a1 columns), layer 2 + logits,
+// softmax / loss + dW3, d2 (+ d2 columns), d1 + db1 + dW1; [5] = groups
+__device__ unsigned long long g_grad_ph[kRollDiagBlocks * 6];
 #endif
 
 constexpr int kPolBlock = 256;   // 4 waves; two workgroups per CU (2 waves per SIMD)
@@ -671,12 +674,17 @@ __device__ __forceinline__ float activation_derivative(float a) {   // from the 
 // The a1^T / d2^T column buffers are addressed as buffer resources: element (row, column) at voffset = this lane's
 // column byte offset (one VGPR for every access) + soffset = row * ld * 4 (scalar), so no per-row 64-bit vector
 // address is ever formed (those kept 2 VGPRs live per row across the whole group and spilled the large nets).
-__device__ __forceinline__ void col_store(__amdgpu_buffer_rsrc_t r, uint32_t row, uint32_t ld, uint32_t voff, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, (int)(row * ld * 4u), 0);
+// Column buffers [rows][ld] fp32: row `row` of this lane's column at scalar offset row * ld4 (ld4 = ld * 4 bytes).
+// The caller re-opaques ld4 per tile (opaque_sgpr): otherwise the compiler hoists every row's offset out of the
+// group loop into its own SGPR (hundreds of them), spills them to VGPR lanes, and pays a v_readlane + hazard nops
+// before every column store.
+__device__ __forceinline__ void col_store(__amdgpu_buffer_rsrc_t r, uint32_t row, uint32_t ld4, uint32_t voff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, (int)(row * ld4), 0);
 }
-__device__ __forceinline__ float col_load(__amdgpu_buffer_rsrc_t r, uint32_t row, uint32_t ld, uint32_t voff) {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)(row * ld * 4u), 0));
+__device__ __forceinline__ float col_load(__amdgpu_buffer_rsrc_t r, uint32_t row, uint32_t ld4, uint32_t voff) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)(row * ld4), 0));
 }
+__device__ __forceinline__ void opaque_sgpr(uint32_t& v) { asm volatile("" : "+s"(v)); }
 // packed weight fragment `idx` (64 lanes x float4) at this lane's voffset (lane * 16): the same one-VGPR addressing
 // for the fragment streams (per-fragment 64-bit pointers were hoisted out of the group loop, 2 registers each)
 __device__ __forceinline__ float4 frag_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t idx) {
@@ -713,12 +721,27 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
     for (int k = 0; k < 2 * NT2; k++) dw3acc[k] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
     const uint32_t waves = gridDim.x * (kPolBlock / 64);
     const uint32_t groups = a.ld >> 5;
+#if G2048_DIAG
+    unsigned long long gph[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long gtp = __builtin_amdgcn_s_memrealtime();
+#define GRAD_PH(k)                                                        \
+    do {                                                                  \
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();  \
+        gph[k] += tn - gtp;                                               \
+        gtp = tn;                                                         \
+    } while (0)
+#else
+#define GRAD_PH(k) \
+    do {           \
+    } while (0)
+#endif
     for (uint32_t gi = blockIdx.x * (kPolBlock / 64) + w; gi < groups; gi += waves) {
         const uint32_t j = gi * 32u + (uint32_t)col;   // this lane's sample (both halves)
         // a compiler memory barrier per group: without it the net tensors' LDS reads (loop-invariant) are hoisted
         // out of the group loop into hundreds of registers
         asm volatile("" ::: "memory");
         const uint32_t off = (j + 4u * (uint32_t)h * a.ld) * 4u;   // byte offset: column j, + acc_row's 4h rows
+        uint32_t ld4 = a.ld * 4u;                                    // row stride in bytes (see col_store)
         const bool valid = j < a.n;
         const uint64_t b = valid ? a.boards[j] : 0ull;
         const uint32_t act = (valid && !a.critic) ? a.actions[j] : 0u;   // no actions in critic mode
@@ -744,6 +767,7 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
             for (int s = 0; s < 8; s++) x[s] = obs_value<OBS>(b, 2 * s + h, a.obs_scale);
 #pragma unroll
             for (int t = 0; t < NT1; t++) {
+                opaque_sgpr(ld4);
                 floatx16 acc = {};
 #pragma unroll
                 for (int s = 0; s < 8; s++)
@@ -755,15 +779,16 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                     const float4 hv = make_float4(activate<ACT>(acc[4 * q + 0] + bv.x), activate<ACT>(acc[4 * q + 1] + bv.y),
                                                   activate<ACT>(acc[4 * q + 2] + bv.z), activate<ACT>(acc[4 * q + 3] + bv.w));
                     h1f[(t * 4 + q) * 64 + lane] = hv;
-                    col_store(ra1, 32 * t + acc_row(4 * q + 0, 0), a.ld, off, hv.x);
-                    col_store(ra1, 32 * t + acc_row(4 * q + 1, 0), a.ld, off, hv.y);
-                    col_store(ra1, 32 * t + acc_row(4 * q + 2, 0), a.ld, off, hv.z);
-                    col_store(ra1, 32 * t + acc_row(4 * q + 3, 0), a.ld, off, hv.w);
+                    col_store(ra1, 32 * t + acc_row(4 * q + 0, 0), ld4, off, hv.x);
+                    col_store(ra1, 32 * t + acc_row(4 * q + 1, 0), ld4, off, hv.y);
+                    col_store(ra1, 32 * t + acc_row(4 * q + 2, 0), ld4, off, hv.z);
+                    col_store(ra1, 32 * t + acc_row(4 * q + 3, 0), ld4, off, hv.w);
                 }
             }
         }
         lds_fence();
-        if (h == 0) col_store(ra1, H1p, a.ld, j * 4u, 1.0f);   // the ones row: db2 comes out of the dW2 GEMM
+        if (h == 0) col_store(ra1, H1p, ld4, j * 4u, 1.0f);   // the ones row: db2 comes out of the dW2 GEMM
+        GRAD_PH(0);
         float h2[NT2][16];
         float lg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -810,6 +835,7 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) lg[k] = (lg[k] + __shfl_xor(lg[k], 32, 64)) + sm.b3()[k];
+        GRAD_PH(1);
         float g[4];
         if (!a.critic) {
             // ---- logits_to_probs (src/MLP.py:139-156) and the policy-gradient logits delta (:328-354)
@@ -844,8 +870,9 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         // a1 of the first h1 tile for the input delta, re-read from its columns well ahead of its use (each tile's
         // reload is issued one tile ahead: loaded at the point of use it cost a full memory latency per register)
         float a1n[16];
+        opaque_sgpr(ld4);
 #pragma unroll
-        for (int r = 0; r < 16; r++) a1n[r] = col_load(ra1, acc_row(r, 0), a.ld, off);
+        for (int r = 0; r < 16; r++) a1n[r] = col_load(ra1, acc_row(r, 0), ld4, off);
         // ---- dW3 += a2^T g: per h2 tile, a2 transposed through LDS, 16x16x4 MFMAs over the 32 samples
         //      (A = g^T [action][sample], B = a2^T [sample][unit]; only the 4 action rows are kept)
 #pragma unroll
@@ -864,9 +891,11 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        GRAD_PH(2);
         // ---- d2 = act'(a2) * (W3 g), in place; d2^T columns
 #pragma unroll
         for (int o = 0; o < NT2; o++) {
+            opaque_sgpr(ld4);
             const float4* w3 = reinterpret_cast<const float4*>(sm.w3p() + (o * 2 + h) * 64);
 #pragma unroll
             for (int r = 0; r < 16; r++) {
@@ -876,10 +905,11 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                 dh = fmaf(g[2], wv.z, dh);
                 dh = fmaf(g[3], wv.w, dh);
                 h2[o][r] = dh * activation_derivative<ACT>(h2[o][r]);
-                col_store(rd2, 32 * o + acc_row(r, 0), a.ld, off, h2[o][r]);
+                col_store(rd2, 32 * o + acc_row(r, 0), ld4, off, h2[o][r]);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        GRAD_PH(3);
         // ---- d1 = act'(a1) * (W2 d2) per h1 tile, then db1 and dW1 += x^T d1 (16x16x4 MFMAs: A = x^T
         //      [feature][sample] built from the group's boards, B = d1^T [sample][unit] through LDS)
         float xa[8];
@@ -893,11 +923,12 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         for (int q = 0; q < 4; q++) fw[q] = fa[q];   // input-delta k-tiles 0 and 1, prefetched by the forward
 #pragma unroll
         for (int o1 = 0; o1 < NT1; o1++) {
+            opaque_sgpr(ld4);
             float a1v[16];
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 a1v[r] = a1n[r];
-                if (o1 + 1 < NT1) a1n[r] = col_load(ra1, 32 * (o1 + 1) + acc_row(r, 0), a.ld, off);
+                if (o1 + 1 < NT1) a1n[r] = col_load(ra1, 32 * (o1 + 1) + acc_row(r, 0), ld4, off);
             }
             floatx16 acc = {};
 #pragma unroll
@@ -936,7 +967,16 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                                                                             dw1acc[2 * o1 + c], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
+        GRAD_PH(4);
+#if G2048_DIAG
+        gph[5] += 1;
+#endif
     }
+#if G2048_DIAG
+    if (threadIdx.x == 0 && blockIdx.x < kRollDiagBlocks)
+        for (int k = 0; k < 6; k++) g_grad_ph[blockIdx.x * 6 + k] = gph[k];
+#endif
+#undef GRAD_PH
     // ---- this wave's partial gradients
     const uint32_t wg = blockIdx.x * (kPolBlock / 64) + w;
     float* out = a.part + (size_t)wg * grad_part_floats(NT1, NT2);
@@ -1029,6 +1069,14 @@ int g2048_diag_rollout_phases(unsigned long long* out, int blocks) {
     if (blocks > kRollDiagBlocks) blocks = kRollDiagBlocks;
     if (hipDeviceSynchronize() != hipSuccess) return G2048_EHIP;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_roll_ph), sizeof(unsigned long long) * 5 * blocks, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return G2048_EHIP;
+    return blocks;
+}
+int g2048_diag_grad_phases(unsigned long long* out, int blocks) {
+    if (blocks > kRollDiagBlocks) blocks = kRollDiagBlocks;
+    if (hipDeviceSynchronize() != hipSuccess) return G2048_EHIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_grad_ph), sizeof(unsigned long long) * 6 * blocks, 0,
                             hipMemcpyDeviceToHost) != hipSuccess)
         return G2048_EHIP;
     return blocks;
