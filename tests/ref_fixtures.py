@@ -1,0 +1,91 @@
+"""Loaders for the fixtures tests/golden/make_golden_ref.py generated from the REAL reference (src/env.py,
+src/reinforce_agent.py, runner.py).  Test infrastructure only: the oracle rebuilds reference-format observations
+(src/env.py:131-171) from the recorded bitboards, so the fixtures store boards, not obs."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+from oracle import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+_cache: dict = {}
+
+
+def load(name: str):
+    if name not in _cache:
+        with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+            _cache[name] = {k: z[k] for k in z.files}
+    return _cache[name]
+
+
+def env_configs() -> list[dict]:
+    return json.loads(str(load("env_steps")["configs"]))
+
+
+def update_cases() -> list[dict]:
+    return json.loads(str(load("update")["cases"]))
+
+
+def n_layers(case: dict) -> int:
+    return len(case["mlp"]["hidden_sizes"]) + 1
+
+
+def params_of(ci: int, prefix: str, L: int) -> dict:
+    """prefix: "init_actor", "init_critic", "up{u}_actor", "up{u}_critic" -> {"W": [...], "b": [...]}."""
+    d = load("update")
+    flat = [d[f"u{ci}_{prefix}_{j}"] for j in range(2 * L)]
+    return {"W": [a.copy() for a in flat[:L]], "b": [a.copy() for a in flat[L:]]}
+
+
+def has(ci: int, key: str) -> bool:
+    return f"u{ci}_{key}" in load("update")
+
+
+def arr(ci: int, key: str):
+    return load("update")[f"u{ci}_{key}"]
+
+
+def obs_cfg(env: dict) -> dict:
+    return dict(obs_mode=env.get("obs_mode", "raw"), obs_log2_scale=env.get("obs_log2_scale", 1.0))
+
+
+_obs_cache: dict = {}
+
+
+def obs_for(board: int, env: dict):
+    """Reference-format obs of a bitboard under an env config (dict with mask, or the bare board)."""
+    key = (int(board), env.get("obs_mode", "raw"), env.get("obs_log2_scale", 1.0), env.get("use_action_mask", True))
+    if key not in _obs_cache:
+        x, m = O.obs_of_bitboard(int(board), **obs_cfg(env))
+        b = x.reshape(4, 4, 17) if x.size == 272 else x.reshape(4, 4)
+        _obs_cache[key] = (b, m)
+    b, m = _obs_cache[key]
+    if env.get("use_action_mask", True):
+        return {"board": b.copy(), "action_mask": m.copy()}
+    return b.copy()
+
+
+def trajectories(ci: int, u: int, case: dict) -> list[dict]:
+    """The reference trajectory dicts of update u of case ci (src/reinforce_agent.py:240-247), obs rebuilt."""
+    P = f"up{u}_"
+    lens = arr(ci, P + "lengths")
+    boards, acts, rews = arr(ci, P + "boards"), arr(ci, P + "actions"), arr(ci, P + "rewards")
+    tot, mt = arr(ci, P + "total_reward"), arr(ci, P + "max_tile")
+    out, s = [], 0
+    for i, T in enumerate(lens):
+        T = int(T)
+        out.append({"obs": [obs_for(int(b), case["env"]) for b in boards[s:s + T]],
+                    "actions": [int(a) for a in acts[s:s + T]],
+                    "rewards": [float(r) for r in rews[s:s + T]],
+                    "total_reward": float(tot[i]), "states": [], "max_tile": int(mt[i])})
+        s += T
+    return out
+
+
+def rel(a, b) -> float:
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30)) if b.size else 0.0
