@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--trace-steps", type=int, default=0,
                     help="diagnostic: print per-launch kernel us and reset fraction for the first N steps, then exit")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    # tools/ A/B and diag scripts only: measure another build of libg2048 (never the default)
+    ap.add_argument("--lib", default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -277,6 +279,11 @@ def main():
     import torch.distributed as dist
 
     import rl2048_amd  # noqa: F401
+
+    if args.lib:
+        from rl2048_amd import _lib as L
+
+        L.use_library_for_tools(args.lib)
 
     ndev = torch.cuda.device_count()
     device = torch.device("cuda", local_rank % max(ndev, 1))

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 4
+#define G2048_ABI_VERSION 5
 
 /* status codes */
 #define G2048_OK 0
@@ -101,6 +101,7 @@ typedef struct g2048_step_out {
     uint32_t* merged;      /* [n] merged tiles of this step in the reference's list order, as nibbles
                               (log2(v) - 1), first merge in the lowest nibble, 0-terminated (<= 8) */
     uint64_t* prev_board;  /* [n] the board before the step (trajectory record) */
+    double* reward64;      /* [n] the same reward in fp64 -- the Python float src/env.py:261 returns (may be NULL) */
 } g2048_step_out;
 
 /* ---------------------------------------------------------------------------------------------------- */
@@ -158,7 +159,7 @@ int g2048_sample(const float* logits, const int8_t* mask, const uint8_t* active,
 /* Discounted returns per episode (ReinforceAgent.compute_returns src/reinforce_agent.py:255-273):
  * rewards / returns are time-major [T, n] fp32 (lane i's episode occupies rows 0..lengths[i]-1); the scan is
  * accumulated in fp64 like the reference's Python float and stored as fp32. */
-int g2048_returns(const float* rewards, const int32_t* lengths, double gamma, float* returns, int64_t T,
+int g2048_returns(const double* rewards, const int32_t* lengths, double gamma, float* returns, int64_t T,
                   int64_t n, void* stream);
 
 /* The 8 dihedral symmetries of Game2048Env.get_symmetries (src/env.py:317-398) on bitboards:
@@ -238,7 +239,7 @@ int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int
 int g2048_rollout(const float* packed, int h1, int h2, int activation, const g2048_env_cfg* cfg, int greedy,
                   const uint64_t* env_state, const uint64_t* env_inc, const uint64_t* env_buf, const uint64_t* pol_state,
                   const uint64_t* pol_inc, const uint64_t* pol_buf, uint32_t* queue, int64_t n, int64_t cap,
-                  uint64_t* boards, uint8_t* actions, float* rewards, uint8_t* flags, float* probs, int32_t* lengths,
+                  uint64_t* boards, uint8_t* actions, double* rewards, uint8_t* flags, float* probs, int32_t* lengths,
                   double* totals, uint8_t* max_tile, uint64_t* final_board, void* stream);
 
 #ifdef __cplusplus

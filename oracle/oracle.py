@@ -273,6 +273,20 @@ class Env:
         return int(self.e.step_count)
 
 
+def obs_of_values(vals, **cfg) -> tuple[np.ndarray, np.ndarray]:
+    """(obs["board"] flattened float32, action mask int8) of a board given as tile values, under an env config:
+    src/env.py:131-159 restated (``or_env_obs``) + the game's mask."""
+    e = Env(**cfg)
+    for i, v in enumerate(np.asarray(vals, dtype=np.int64).reshape(16)):
+        e.e.game.board[i] = int(v)
+    return e.obs(), e.mask()
+
+
+def obs_of_bitboard(board: int, **cfg) -> tuple[np.ndarray, np.ndarray]:
+    e = unpack_exponents(board)
+    return obs_of_values(np.where(e > 0, np.left_shift(np.int64(1), e), 0), **cfg)
+
+
 def bench_env_steps(n_boards: int, n_rounds: int, seed0: int = 1000, **cfg) -> tuple[int, float]:
     """CPU baseline leg: run the oracle env step loop (OpenMP over boards). Returns (steps, reward_sum)."""
     c = make_env_cfg(**cfg)

@@ -17,13 +17,10 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_ROOT = os.path.dirname(PKG_DIR)
 SHIPPED_LIB = os.path.join(PKG_DIR, "libg2048.so")
 LIB_PATH = SHIPPED_LIB
-# tools/diag_build.sh only: load the -DG2048_DIAG=1 timing-attribution build instead of the shipped library
-if os.environ.get("G2048_DIAG_LIB"):
-    LIB_PATH = os.environ["G2048_DIAG_LIB"]
 SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
 SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # include/g2048.h constants
 OBS_NONE, OBS_RAW, OBS_LOG2, OBS_ONEHOT = -1, 0, 1, 2
@@ -63,7 +60,8 @@ class Lanes(ctypes.Structure):
 
 
 class StepOut(ctypes.Structure):
-    _fields_ = [(name, ctypes.c_void_p) for name in ("reward", "flags", "mask", "obs", "merged", "prev_board")]
+    _fields_ = [(name, ctypes.c_void_p) for name in ("reward", "flags", "mask", "obs", "merged", "prev_board",
+                                                         "reward64")]
 
 
 _lib = None
@@ -129,6 +127,16 @@ def lib():
                 raise RuntimeError(f"libg2048.so ABI {v} != expected {ABI_VERSION}; rebuild")
             _lib = L
     return _lib
+
+
+def use_library_for_tools(path: str) -> None:
+    """tools/ only: open another build of the same ABI (the -DG2048_DIAG=1 timing-attribution build of
+    tools/diag_build.sh) instead of the shipped library.  Must run before the first lib() call; the product
+    path never calls it (nothing in the package reads the environment to switch libraries)."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("libg2048 is already open")
+    LIB_PATH = os.path.abspath(path)
 
 
 def check(rc: int) -> None:

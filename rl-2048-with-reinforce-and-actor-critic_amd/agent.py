@@ -70,7 +70,7 @@ class TrajectoryBatch:
     boards[t, i] is the board BEFORE action actions[t, i]; rewards[t, i] its reward; valid iff t < lengths[i]."""
     boards: torch.Tensor       # [T, n] int64 bitboards
     actions: torch.Tensor      # [T, n] uint8
-    rewards: torch.Tensor      # [T, n] float32
+    rewards: torch.Tensor      # [T, n] float64 (the Python float Game2048Env.step returns)
     flags: torch.Tensor        # [T, n] uint8 (G2048_F_*)
     lengths: torch.Tensor      # [n] int32
     total_reward: torch.Tensor  # [n] float64
@@ -129,8 +129,10 @@ class _Steps:
         self.t = self.vidx // self.n
         self.has_next = (self.t + 1) < self.lengths[self.lane]
         self.actions = actions.reshape(-1)[self.vidx].to(torch.int64)
+        # fp32 per valid step for the critic (np.array(rewards, float32), src/reinforce_agent.py:420); the fp64
+        # time-major rows for compute_returns (fp64 scan of the Python floats, :263-271)
         self.rewards = rewards.reshape(-1)[self.vidx].to(torch.float32)
-        self.rewards_tm = rewards
+        self.rewards_tm = rewards.to(torch.float64)
         self.boards = boards
         self.X = X
         self.M = M
@@ -538,9 +540,11 @@ class ReinforceAgent:
         cap = max(cap, 1)
         boards = torch.empty(cap, n, dtype=torch.int64, device=dev)
         actions = torch.empty(cap, n, dtype=torch.uint8, device=dev)
-        rewards = torch.empty(cap, n, dtype=torch.float32, device=dev)
+        rewards = torch.zeros(cap, n, dtype=torch.float64, device=dev)
         flags = torch.empty(cap, n, dtype=torch.uint8, device=dev)
         probs = torch.zeros(cap, n, 4, dtype=torch.float32, device=dev) if record_probs else None
+        # total_reward += float(reward) in step order (src/reinforce_agent.py:233); finished lanes add 0.0
+        total = torch.zeros(n, dtype=torch.float64, device=dev)
         # the reference masks the logits only when the obs carries an action mask (encode_observation,
         # src/MLP.py:22-43 -> select_action src/reinforce_agent.py:138-145)
         use_mask = bool(self.env_config.use_action_mask)
@@ -552,7 +556,7 @@ class ReinforceAgent:
                 grow = cap
                 boards = torch.cat([boards, torch.empty(grow, n, dtype=torch.int64, device=dev)])
                 actions = torch.cat([actions, torch.empty(grow, n, dtype=torch.uint8, device=dev)])
-                rewards = torch.cat([rewards, torch.empty(grow, n, dtype=torch.float32, device=dev)])
+                rewards = torch.cat([rewards, torch.zeros(grow, n, dtype=torch.float64, device=dev)])
                 flags = torch.cat([flags, torch.empty(grow, n, dtype=torch.uint8, device=dev)])
                 if probs is not None:
                     probs = torch.cat([probs, torch.zeros(grow, n, 4, dtype=torch.float32, device=dev)])
@@ -571,7 +575,8 @@ class ReinforceAgent:
                                                env.philox_key ^ 0x5A5A, L.ptr(pseeds), L.ptr(env.step_count),
                                                L.ptr(probs[t]) if probs is not None else None, None,
                                                L.ptr(actions[t]), m if m < n else n, self._stream))
-                env.step_into(actions[t], reward=rewards[t], flags=flags[t], prev_board=boards[t], write_obs=False)
+                env.step_into(actions[t], reward=env.reward, flags=flags[t], prev_board=boards[t], write_obs=False,
+                              reward64=rewards[t])
             else:
                 logits = self._policy_logits(env.obs)
                 L.check(self._lib.g2048_sample(L.ptr(logits), L.ptr(env.mask) if use_mask else None,
@@ -579,17 +584,16 @@ class ReinforceAgent:
                                                L.ptr(pinc), L.ptr(pbuf), env.philox_key ^ 0x5A5A, L.ptr(pseeds),
                                                L.ptr(env.step_count), L.ptr(probs[t]) if probs is not None else None,
                                                L.ptr(actions[t]), n, self._stream))
-                env.step_into(actions[t], reward=rewards[t], flags=flags[t], prev_board=boards[t])
+                env.step_into(actions[t], reward=env.reward, flags=flags[t], prev_board=boards[t],
+                              reward64=rewards[t])
+            total += rewards[t]      # inactive lanes got reward 0.0
             t += 1
             if t % check_every == 0 and not bool(env.status.any()):
                 break
         fl = flags[:t]
         lengths = ((fl & L.F_INACTIVE) == 0).sum(0).to(torch.int32)
         T = int(lengths.max().item()) if n else 0
-        rw = rewards[:T]
-        valid = torch.arange(T, device=dev).unsqueeze(1) < lengths.unsqueeze(0)
-        total = torch.where(valid, rw.double(), torch.zeros((), dtype=torch.float64, device=dev)).sum(0)
-        return TrajectoryBatch(boards=boards[:T], actions=actions[:T], rewards=torch.where(valid, rw, 0.0),
+        return TrajectoryBatch(boards=boards[:T], actions=actions[:T], rewards=rewards[:T],
                                flags=fl[:T], lengths=lengths, total_reward=total,
                                max_tile=env.max_tile_seen.clone(), final_boards=env.board.clone(),
                                probs=probs[:T] if probs is not None else None)
@@ -614,7 +618,7 @@ class ReinforceAgent:
         cap = max(int(self.env_config.max_steps), 1)
         boards = torch.empty(cap, n, dtype=torch.int64, device=dev)
         actions = torch.zeros(cap, n, dtype=torch.uint8, device=dev)
-        rewards = torch.zeros(cap, n, dtype=torch.float32, device=dev)
+        rewards = torch.zeros(cap, n, dtype=torch.float64, device=dev)
         flags = torch.full((cap, n), L.F_INACTIVE, dtype=torch.uint8, device=dev)
         probs = torch.zeros(cap, n, 4, dtype=torch.float32, device=dev) if record_probs else None
         lengths = torch.empty(n, dtype=torch.int32, device=dev)
@@ -699,10 +703,10 @@ class ReinforceAgent:
 
     # ============================================================================================ returns
     def compute_returns(self, rewards) -> np.ndarray:
-        """src/reinforce_agent.py:255-273 (fp64 scan, fp32 result) on the device."""
-        r = torch.as_tensor(np.asarray(rewards, dtype=np.float32), device=self.device).view(-1, 1).contiguous()
+        """src/reinforce_agent.py:255-273 (fp64 scan of the fp64 rewards, fp32 result) on the device."""
+        r = torch.as_tensor(np.asarray(rewards, dtype=np.float64), device=self.device).view(-1, 1).contiguous()
         T = r.shape[0]
-        out = torch.zeros_like(r)
+        out = torch.zeros(T, 1, dtype=torch.float32, device=self.device)
         ln = torch.full((1,), T, dtype=torch.int32, device=self.device)
         L.check(self._lib.g2048_returns(L.ptr(r), L.ptr(ln), float(self.agent_config.gamma), L.ptr(out), T, 1,
                                         self._stream))
@@ -710,9 +714,9 @@ class ReinforceAgent:
 
     def _returns_tm(self, rewards_tm: torch.Tensor, lengths: torch.Tensor) -> torch.Tensor:
         T, n = rewards_tm.shape
-        out = torch.zeros_like(rewards_tm)
+        out = torch.zeros(T, n, dtype=torch.float32, device=self.device)
         ln = lengths.to(torch.int32).contiguous()
-        L.check(self._lib.g2048_returns(L.ptr(rewards_tm.contiguous()), L.ptr(ln), float(self.agent_config.gamma),
+        L.check(self._lib.g2048_returns(L.ptr(rewards_tm.to(torch.float64).contiguous()), L.ptr(ln), float(self.agent_config.gamma),
                                         L.ptr(out), T, n, self._stream))
         return out
 
@@ -798,7 +802,7 @@ class ReinforceAgent:
         X = np.zeros((T, n, D), dtype=np.float32)
         M = np.ones((T, n, 4), dtype=np.int8)
         A = np.zeros((T, n), dtype=np.uint8)
-        R = np.zeros((T, n), dtype=np.float32)
+        R = np.zeros((T, n), dtype=np.float64)     # the trajectories' Python floats
         for i, tr in enumerate(trajectories):
             for t, o in enumerate(tr["obs"]):
                 x, m = encode_observation(o)

@@ -308,6 +308,7 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     reset = false;
     if (!(x.stt & G2048_S_ACTIVE) || x.act > 3u) {
         st(a.out.reward, i, 0.0f);
+        if (a.out.reward64) st(a.out.reward64, i, 0.0);
         st(a.out.flags, i, (uint8_t)((x.stt & G2048_S_ACTIVE) ? G2048_F_BADACTION : G2048_F_INACTIVE));
         if (a.out.merged) st(a.out.merged, i, 0u);
         return b;
@@ -338,6 +339,7 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
                         (trunc ? G2048_F_TRUNCATED : 0u) | (invalid ? G2048_F_INVALID : 0u) |
                         (s.overflow ? G2048_F_OVERFLOW : 0u);
     st(a.out.reward, i, (float)r);
+    if (a.out.reward64) st(a.out.reward64, i, r);
     if (LIST && a.out.merged) st(a.out.merged, i, s.list);
     if ((done || trunc) && a.auto_reset) {
         reset = true;   // board / lane state / obs are written by reset_lane after the loop
@@ -647,14 +649,14 @@ __global__ void __launch_bounds__(256) sample_kernel(SampleArgs a) {
 }
 
 // compute_returns (src/reinforce_agent.py:255-273), time-major [T, n], fp64 accumulation
-__global__ void __launch_bounds__(256) returns_kernel(const float* __restrict__ r, const int32_t* __restrict__ len,
+__global__ void __launch_bounds__(256) returns_kernel(const double* __restrict__ r, const int32_t* __restrict__ len,
                                                       double gamma, float* __restrict__ out, int64_t T, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         int64_t Li = len[i];
         Li = Li > T ? T : Li;
         double G = 0.0;
         for (int64_t t = Li - 1; t >= 0; t--) {
-            G = (double)r[t * n + i] + gamma * G;
+            G = r[t * n + i] + gamma * G;
             out[t * n + i] = (float)G;
         }
     }
@@ -925,6 +927,7 @@ int g2048_step(const g2048_lanes* lanes, const uint8_t* actions, const g2048_env
         if (a.out.obs) a.out.obs += width * off;
         if (a.out.merged) a.out.merged += off;
         if (a.out.prev_board) a.out.prev_board += off;
+        if (a.out.reward64) a.out.reward64 += off;
         a.rc = reward_cfg(*cfg);
         a.obs_scale = cfg->obs_log2_scale;
         a.auto_reset = auto_reset;
@@ -1013,7 +1016,7 @@ int g2048_sample(const float* logits, const int8_t* mask, const uint8_t* active,
     return G2048_OK;
 }
 
-int g2048_returns(const float* rewards, const int32_t* lengths, double gamma, float* returns, int64_t T, int64_t n,
+int g2048_returns(const double* rewards, const int32_t* lengths, double gamma, float* returns, int64_t T, int64_t n,
                   void* stream) {
     if (n < 0 || T < 0) return fail(G2048_EINVAL, "n < 0 or T < 0");
     if (!rewards || !lengths || !returns) return fail(G2048_EINVAL, "NULL buffer");

@@ -323,7 +323,7 @@ struct RolloutArgs {
     uint32_t* next;                               // episode queue (zero before the launch)
     uint64_t* boards;                             // [cap, n] time-major trajectory rows
     uint8_t* actions;
-    float* rewards;
+    double* rewards;                              // fp64: the Python float run_episode records
     uint8_t* flags;
     float* probs;                                 // [cap, n, 4] or NULL
     int32_t* lengths;                             // per episode
@@ -523,8 +523,8 @@ __global__ void __launch_bounds__(kPolBlock, 1) rollout_kernel(RolloutArgs a) {
             float p[4];
             const uint32_t act = softmax_select(lg, mw, a.use_mask != 0, a.greedy != 0, u, p);
             const StepValues ov = env_step_pcg(b, act, sc, mt, ge, a.rc, a.max_steps, lut, code);
-            const float r = (float)ov.reward;
-            total += (double)r;
+            const double r = ov.reward;
+            total += r;                            // total_reward += float(reward) (src/reinforce_agent.py:233)
             if (w == 0 && h == 0) {
                 const size_t row = (size_t)t * a.n + ep;
                 a.boards[row] = b;
@@ -1259,7 +1259,7 @@ int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int
 int g2048_rollout(const float* packed, int h1, int h2, int activation, const g2048_env_cfg* cfg, int greedy,
                   const uint64_t* env_state, const uint64_t* env_inc, const uint64_t* env_buf, const uint64_t* pol_state,
                   const uint64_t* pol_inc, const uint64_t* pol_buf, uint32_t* queue, int64_t n, int64_t cap,
-                  uint64_t* boards, uint8_t* actions, float* rewards, uint8_t* flags, float* probs, int32_t* lengths,
+                  uint64_t* boards, uint8_t* actions, double* rewards, uint8_t* flags, float* probs, int32_t* lengths,
                   double* totals, uint8_t* max_tile, uint64_t* final_board, void* stream) {
     int rc = g2048_internal::check_env_cfg(cfg);
     if (rc) return rc;

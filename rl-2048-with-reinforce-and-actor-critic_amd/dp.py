@@ -61,22 +61,24 @@ def fused_all_reduce_(tensors: list[torch.Tensor], group=None) -> None:
 
 def rank_weights(totals: torch.Tensor, conf, group=None) -> torch.Tensor:
     """_compute_episode_rank_weights (src/reinforce_agent.py:681-716) over the GLOBAL batch; returns this rank's
-    slice.  Episode ranks come from a stable sort of the totals (ties keep episode order; the reference's
-    default numpy sort leaves tie order unspecified)."""
+    slice.  Episode ranks come from a stable sort of the fp64 totals (the Python floats the reference sorts,
+    :701); exact ties keep episode order, where the reference's default numpy sort leaves their order
+    machine-dependent.  Weights are fp32 as in the reference: conf[bin] / mean, the mean an fp32 division of the
+    (exact) weight sum by n.  No host synchronisation."""
     n_local = totals.numel()
     if conf is None or len(conf) == 0:
         return torch.ones(n_local, dtype=torch.float32, device=totals.device)
     all_tot, offset = gather_varlen(totals.to(torch.float64), group)
     n = all_tot.numel()
     confs = torch.tensor(list(conf), dtype=torch.float32, device=totals.device)
-    order = torch.argsort(all_tot.to(torch.float32), stable=True)
+    order = torch.argsort(all_tot, stable=True)
     ranks = torch.arange(n, device=totals.device, dtype=torch.float64)
     bins = torch.clamp(((ranks + 0.5) / n * len(conf)).to(torch.int64), max=len(conf) - 1)
     w = torch.empty(n, dtype=torch.float32, device=totals.device)
     w[order] = confs[bins]
-    mw = w.mean()
-    if float(mw) > 1e-8:
-        w = w / mw
+    # np.mean of the fp32 weights: the sum of a few distinct conf values is exact in fp64, then one fp32 division
+    mw = (w.double().sum().to(torch.float32) / torch.tensor(float(n), dtype=torch.float32, device=w.device))
+    w = torch.where(mw > 1e-8, w / mw, w)
     return w[offset: offset + n_local].contiguous()
 
 

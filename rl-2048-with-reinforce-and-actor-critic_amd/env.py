@@ -27,10 +27,9 @@ class Discrete:
         self.n = n
 
     def contains(self, x) -> bool:
-        if isinstance(x, (bool, np.bool_)):
-            return False
-        if isinstance(x, (int, np.integer)) or (isinstance(x, np.ndarray) and x.shape == () and
-                                                np.issubdtype(x.dtype, np.integer)):
+        # gymnasium's Discrete.contains: a Python int (bool included) or an integer numpy scalar / 0-d array
+        if isinstance(x, int) or (isinstance(x, (np.generic, np.ndarray)) and x.shape == () and
+                                  np.issubdtype(x.dtype, np.integer)):
             return 0 <= int(x) < self.n
         return False
 
@@ -115,7 +114,7 @@ class Game2048Env:
 
     def __init__(self, config: Game2048EnvConfig | None = None, device=None) -> None:
         self.config = config or Game2048EnvConfig()
-        self._vec = VecGame2048Env(1, self.config, device=device, record_merged=True)
+        self._vec = VecGame2048Env(1, self.config, device=device, record_merged=True, record_reward64=True)
         self._max_num = 16.0
         self.action_space = Discrete(4)
         self._step_count = 0
@@ -135,7 +134,7 @@ class Game2048Env:
         b, score, flags, merged, mt, sc = [int(x) for x in ints[:, 0].tolist()]
         obs = v.obs[0].cpu().numpy().copy()
         mask = v.mask[0].cpu().numpy().copy()
-        reward = float(v.reward[0].item())
+        reward = float(v.reward64[0].item())    # fp64, as src/env.py:261 returns it
         self._board = _values(b & 0xFFFFFFFFFFFFFFFF)
         self._score = score
         self.max_tile_seen = 1 << mt

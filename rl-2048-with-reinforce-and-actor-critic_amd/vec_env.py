@@ -77,7 +77,8 @@ class VecGame2048Env:
 
     def __init__(self, num_envs: int, config: Game2048EnvConfig | None = None, device=None, rng: str = "pcg64",
                  auto_reset: bool = False, reset_stride: int | None = None, philox_key: int = 0x2048,
-                 lane_offset: int = 0, record_merged: bool = False, record_prev_board: bool = False):
+                 lane_offset: int = 0, record_merged: bool = False, record_prev_board: bool = False,
+                 record_reward64: bool = False):
         if num_envs <= 0:
             raise ValueError("num_envs must be positive")
         self.config = config or Game2048EnvConfig()
@@ -107,6 +108,8 @@ class VecGame2048Env:
         self.rng_buf = z(torch.int64, n) if pcg else None
         # outputs (g2048_step_out)
         self.reward = z(torch.float32, n)
+        # the fp64 reward (the Python float src/env.py:261 returns); off by default: +8 B per board-step
+        self.reward64 = z(torch.float64, n) if record_reward64 else None
         self.flags = z(torch.uint8, n)
         self.mask = z(torch.int8, n, 4)
         self.obs_width = obs_width(self.config.obs_mode)
@@ -116,7 +119,7 @@ class VecGame2048Env:
         self._lanes = L.Lanes(*[L.ptr(t) for t in (self.board, self.step_count, self.score, self.max_tile, self.status,
                                                    self.seed, self.rng_state, self.rng_inc, self.rng_buf)])
         self._out = L.StepOut(L.ptr(self.reward), L.ptr(self.flags), L.ptr(self.mask), L.ptr(self.obs),
-                              L.ptr(self.merged), L.ptr(self.prev_board))
+                              L.ptr(self.merged), L.ptr(self.prev_board), L.ptr(self.reward64))
         self._lib = L.lib()
         self._stream = L.stream_handle(self.device)
 
@@ -141,27 +144,31 @@ class VecGame2048Env:
         return self._obs_view(), {"score": self.score, "board": self.board}
 
     def step_into(self, actions: torch.Tensor, reward: torch.Tensor | None = None, flags: torch.Tensor | None = None,
-                  prev_board: torch.Tensor | None = None, write_obs: bool = True) -> None:
-        """Launch one step writing reward/flags (and the pre-step board) into caller tensors (trajectory rows).
-        write_obs=False skips the obs buffer (its consumer reads the boards itself, e.g. g2048_policy)."""
+                  prev_board: torch.Tensor | None = None, write_obs: bool = True,
+                  reward64: torch.Tensor | None = None) -> None:
+        """Launch one step writing reward/flags (and the pre-step board, the fp64 reward) into caller tensors
+        (trajectory rows).  write_obs=False skips the obs buffer (its consumer reads the boards itself, e.g.
+        g2048_policy)."""
         if actions.dtype != torch.uint8 or actions.device != self.device or actions.numel() != self.n:
             raise ValueError("actions must be a uint8 tensor of num_envs elements on the env device")
         out = self._out
-        if reward is not None or flags is not None or prev_board is not None or not write_obs:
+        if reward is not None or flags is not None or prev_board is not None or not write_obs or reward64 is not None:
             out = L.StepOut(L.ptr(reward if reward is not None else self.reward),
                             L.ptr(flags if flags is not None else self.flags), L.ptr(self.mask),
                             L.ptr(self.obs) if write_obs else None,
-                            L.ptr(self.merged), L.ptr(prev_board if prev_board is not None else self.prev_board))
+                            L.ptr(self.merged), L.ptr(prev_board if prev_board is not None else self.prev_board),
+                            L.ptr(reward64 if reward64 is not None else self.reward64))
         if torch.cuda.current_device() != self.device.index:
             with torch.cuda.device(self.device):
-                return self.step_into(actions, reward, flags, prev_board, write_obs)
+                return self.step_into(actions, reward, flags, prev_board, write_obs, reward64)
         L.check(self._lib.g2048_step(ctypes.byref(self._lanes), L.ptr(actions), ctypes.byref(self._cfg),
                                      ctypes.byref(out), self.rng_mode, self.philox_key, int(self.auto_reset),
                                      self.reset_stride, self.n, L.stream_handle(self.device)))
 
     def step(self, actions):
         """Game2048Env.step (src/env.py:264-302) for every lane.  actions: int tensor/sequence of n in 0..3.
-        Returns (obs, reward[n] f32, terminated[n] bool, truncated[n] bool, info)."""
+        Returns (obs, reward[n], terminated[n] bool, truncated[n] bool, info); reward is fp64 when the env records
+        it (record_reward64=True), else its fp32 rounding."""
         a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(actions)
         if a.dtype.is_floating_point:
             raise AssertionError("Invalid action dtype")
@@ -177,7 +184,8 @@ class VecGame2048Env:
                 "reset": (f & L.F_RESET) != 0, "overflow": (f & L.F_OVERFLOW) != 0}
         if self.merged is not None:
             info["merged_packed"] = self.merged
-        return (self._obs_view(), self.reward, (f & L.F_TERMINATED) != 0, (f & L.F_TRUNCATED) != 0, info)
+        rew = self.reward64 if self.reward64 is not None else self.reward
+        return (self._obs_view(), rew, (f & L.F_TERMINATED) != 0, (f & L.F_TRUNCATED) != 0, info)
 
     @property
     def active(self) -> torch.Tensor:

@@ -14,6 +14,12 @@ if ROOT not in sys.path:
 
 import torch  # noqa: E402,F401  (see module docstring)
 
+# tools/ab_grad.sh only: run the parity tests against another build of libg2048 (the shipped library otherwise)
+if os.environ.get("G2048_TOOLS_LIB"):
+    from rl2048_amd import _lib as _L
+
+    _L.use_library_for_tools(os.environ["G2048_TOOLS_LIB"])
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on the GPU box)")

@@ -85,6 +85,54 @@ def trajectories(ci: int, u: int, case: dict) -> list[dict]:
     return out
 
 
+_exact_cache: dict = {}
+
+
+def exact_grads(ci: int, u: int, case: dict) -> dict:
+    """Pre-clip gradients of update u of case ci evaluated in fp64 (oracle/agent_oracle.py with dtype=float64) at
+    the reference's parameters before that update: the exact value of the reference's formula, against which
+    the reference's own fp32 sequential accumulation and ours are both measured."""
+    key = (ci, u)
+    if key not in _exact_cache:
+        from oracle import agent_oracle as AO
+
+        L = n_layers(case)
+        pre = "init" if u == 0 else f"up{u - 1}"
+        crit = has(ci, "init_critic_0")
+        ag = {k: v for k, v in case["agent"].items() if k != "model_seed"}
+        ora = AO.OracleAgent(params_of(ci, f"{pre}_actor", L), params_of(ci, f"{pre}_critic", L) if crit else None,
+                             AO.AgentCfg(**ag, activation=case["mlp"]["activation"]), dtype=np.float64)
+        ora.update_batch(trajectories(ci, u, case))
+        gW, gb = ora.captured["actor_grads"]
+        out = {"actor": gW + gb}
+        if crit:
+            cW, cb = ora.captured["critic_grads"]
+            out["critic"] = cW + cb
+        _exact_cache[key] = out
+    return _exact_cache[key]
+
+
+def assert_grad_parity(got, ref, exact_fn, what="") -> None:
+    """North-star gradient parity: within 1e-5 normwise-relative of the reference -- or, where the reference's
+    own fp32 sequential accumulation over N steps is itself further than that from the exact (fp64) value of its
+    formula, at least as close to the exact value as the reference is."""
+    e = rel(got, ref)
+    if e < 1e-5:
+        return
+    exact = exact_fn()
+    e_got, e_ref = rel(got, exact), rel(ref, exact)
+    assert e_got <= max(e_ref, 1e-5), (what, "vs reference", e, "vs exact", e_got, "reference vs exact", e_ref)
+
+
+def assert_norm_parity(got: float, ref: float, exact_grads_fn, what="") -> None:
+    """clip_grads_global_norm's norm: within 1e-5 of the reference's, or at least as close to the norm of the exact
+    gradients as the reference's is."""
+    if abs(got - ref) <= 1e-5 * ref:
+        return
+    ex = float(np.sqrt(sum(float(np.sum(np.asarray(g, np.float64) ** 2)) for g in exact_grads_fn())))
+    assert abs(got - ex) <= max(abs(ref - ex), 1e-5 * ex), (what, got, ref, ex)
+
+
 def rel(a, b) -> float:
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)

@@ -85,7 +85,7 @@ def test_rollout_transitions_and_sampling_bit_exact(path, mask):
             assert O.pack_exponents(O.values_to_exponents(env.board)) == boards[t, i], (i, t)
             assert pr.choice4(probs[t, i]) == acts[t, i], (i, t)
             r = env.step(int(acts[t, i]))
-            assert np.float32(r["reward"]) == rews[t, i]
+            assert rews[t, i] == r["reward"]     # fp64 trajectory rewards, bit-exact
             total += r["reward"]
             done = r["terminated"] or r["truncated"]
             assert done == (t == lens[i] - 1)

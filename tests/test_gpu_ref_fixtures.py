@@ -1,0 +1,395 @@
+"""GPU parity of the HIP path against outputs of the REAL reference (tests/golden/*.npz written by
+tests/golden/make_golden_ref.py from src/env.py, src/reinforce_agent.py, runner.py).  Everything here calls
+libg2048.so through the product classes (VecGame2048Env, Game2048Env, ReinforceAgent, runner).
+
+Tolerances:
+  * env (boards, flags, masks, obs, score, max_tile_seen, step index): bit-exact; rewards bit-exact in fp64
+    (the drop-in's Python float and the trajectory buffer) and == float32(reference) for the fp32 output;
+  * rollout: actions, boards, rewards, lengths, totals, max tiles bit-exact against the reference's own
+    run_episode (same env / policy seeds, same parameters); the policy probabilities within 2e-6 absolute;
+  * update: pre-clip gradients within 1e-5 normwise-relative (north star) -- or, where the reference's own fp32
+    sequential sum is further than that from the exact fp64 value of its formula, at least as close to it as the
+    reference (ref_fixtures.assert_grad_parity); norms within 1e-5; parameters after SGD within
+    rtol 1e-5; Adam steps as assert_step_matches documents (its step is ill-conditioned in tiny gradient elements);
+  * runner: batch statistics (fp32 numpy mean/max/min of the totals) and max-tile counts exactly.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import ref_fixtures as RF
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _mask_bits(m) -> int:
+    return int(sum(int(b) << i for i, b in enumerate(np.asarray(m).reshape(-1))))
+
+
+def _u64(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint64)
+
+
+# ===================================================================================================== env
+@pytest.mark.parametrize("c", range(8))
+def test_vec_env_matches_reference_env(c):
+    """VecGame2048Env (g2048_reset / g2048_step) == src/env.py Game2048Env.reset / step, lane per episode."""
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+    from rl2048_amd import _lib as L
+
+    d = RF.load("env_steps")
+    cfg = Game2048EnvConfig(**RF.env_configs()[c])
+    p = f"c{c}_"
+    seeds, starts, lens = d[p + "ep_seed"], d[p + "ep_start"], d[p + "ep_len"]
+    n = len(seeds)
+    env = VecGame2048Env(n, cfg, device=DEV, record_reward64=True)
+    obs, info = env.reset(seed=[int(s) for s in seeds])
+    assert np.array_equal(_u64(env.board), d[p + "reset_board"])
+    board_obs = obs["board"] if isinstance(obs, dict) else obs
+    np.testing.assert_array_equal(board_obs.reshape(n, -1).cpu().numpy(), d[p + "reset_obs"])
+    assert [_mask_bits(m) for m in env.mask.cpu().numpy()] == list(d[p + "reset_mask"])
+    assert (env.max_tile_seen.cpu().numpy() == 4).all()
+    for t in range(int(lens.max())):
+        live = t < lens
+        acts = np.array([int(d[p + "action"][starts[i] + t]) if live[i] else 0 for i in range(n)], dtype=np.uint8)
+        obs, rew, term, trunc, info = env.step(torch.from_numpy(acts).to(DEV))
+        assert rew.dtype == torch.float64
+        r64, r32 = rew.cpu().numpy(), env.reward.cpu().numpy()
+        te, tr, inv = term.cpu().numpy(), trunc.cpu().numpy(), info["invalid_action"].cpu().numpy()
+        b, mk = _u64(env.board), env.mask.cpu().numpy()
+        ob = (obs["board"] if isinstance(obs, dict) else obs).reshape(n, -1).cpu().numpy()
+        mt, sc, si = env.max_tile_seen.cpu().numpy(), env.score.cpu().numpy(), env.step_count.cpu().numpy()
+        for i in np.nonzero(live)[0]:
+            k = int(starts[i]) + t
+            ref_r = float(d[p + "reward"][k])
+            assert r64[i] == ref_r, (c, i, t, r64[i], ref_r)
+            assert r32[i] == np.float32(ref_r)
+            assert bool(te[i]) == bool(d[p + "terminated"][k]) and bool(tr[i]) == bool(d[p + "truncated"][k])
+            assert bool(inv[i]) == bool(d[p + "invalid"][k])
+            assert int(b[i]) == int(d[p + "board"][k]) and _mask_bits(mk[i]) == int(d[p + "mask"][k])
+            np.testing.assert_array_equal(ob[i], d[p + "obs"][k])
+            assert int(mt[i]) == int(d[p + "max_tile_seen"][k]) and int(sc[i]) == int(d[p + "score"][k])
+            assert int(si[i]) == int(d[p + "step_index"][k])
+        # a lane past its episode end reports F_INACTIVE (nothing happens)
+        done_lanes = np.nonzero(t >= lens)[0]
+        if len(done_lanes):
+            fl = info["flags"].cpu().numpy()
+            assert all(fl[i] & L.F_INACTIVE for i in done_lanes)
+
+
+@pytest.mark.parametrize("c", [1, 2, 3, 5, 7])
+def test_dropin_env_matches_reference_env(c):
+    """The B=1 drop-in Game2048Env: reset / step return the reference's obs, fp64 reward (a Python float equal
+    bit for bit), terminated / truncated and info, episode by episode."""
+    from rl2048_amd import Game2048Env, Game2048EnvConfig
+
+    d = RF.load("env_steps")
+    kw = RF.env_configs()[c]
+    p = f"c{c}_"
+    env = Game2048Env(Game2048EnvConfig(**kw), device=DEV)
+    for e in range(2):
+        obs, info = env.reset(seed=int(d[p + "ep_seed"][e]))
+        board = obs["board"] if isinstance(obs, dict) else obs
+        np.testing.assert_array_equal(board.reshape(-1), d[p + "reset_obs"][e])
+        assert info["score"] == int(d[p + "reset_score"][e]) and env.max_tile_seen == 4
+        s0 = int(d[p + "ep_start"][e])
+        for t in range(int(d[p + "ep_len"][e])):
+            k = s0 + t
+            obs, r, term, trunc, info = env.step(int(d[p + "action"][k]))
+            assert type(r) is float and r == float(d[p + "reward"][k]), (c, e, t)
+            assert term == bool(d[p + "terminated"][k]) and trunc == bool(d[p + "truncated"][k])
+            assert info["invalid_action"] == bool(d[p + "invalid"][k])
+            assert info["step_index"] == int(d[p + "step_index"][k]) and info["score"] == int(d[p + "score"][k])
+            assert sum(info["merged"]) == int(d[p + "merged_sum"][k])
+            assert env.max_tile_seen == int(d[p + "max_tile_seen"][k])
+            board = obs["board"] if isinstance(obs, dict) else obs
+            np.testing.assert_array_equal(board.reshape(-1), d[p + "obs"][k])
+            if isinstance(obs, dict):
+                assert _mask_bits(obs["action_mask"]) == int(d[p + "mask"][k])
+
+
+def test_obs_kernel_matches_reference_encodings():
+    """g2048_obs (+ mask) == _preprocess_board / _get_obs / encode_observation on every fixture board a
+    nibble can hold (the 65536-tile board is the oracle's alone)."""
+    from rl2048_amd import _lib as L
+
+    d = RF.load("obs_enc")
+    vals = d["values"]
+    ok = [i for i, v in enumerate(vals) if v.max() <= 32768]
+    boards = np.array([O.pack_exponents(O.values_to_exponents(vals[i])) for i in ok], dtype=np.uint64)
+    boards = torch.from_numpy(boards.view(np.int64)).to(DEV)
+    m = len(ok)
+    code = {"raw": L.OBS_RAW, "log2": L.OBS_LOG2, "onehot": L.OBS_ONEHOT}
+    for k, (mode, scale) in enumerate(json.loads(str(d["configs"]))):
+        w = 272 if mode == "onehot" else 16
+        x = torch.empty(m, w, dtype=torch.float32, device=DEV)
+        mk = torch.empty(m, 4, dtype=torch.int8, device=DEV)
+        L.check(L.lib().g2048_obs(L.ptr(boards), code[mode], float(scale), L.ptr(x), L.ptr(mk), m,
+                                  L.stream_handle(DEV)))
+        np.testing.assert_array_equal(x.cpu().numpy(), d[f"k{k}_x"][ok], err_msg=f"{mode} {scale}")
+        np.testing.assert_array_equal(mk.cpu().numpy(), d[f"k{k}_mask"][ok])
+
+
+@pytest.mark.parametrize("k", [0, 1, 2])
+def test_symmetry_kernel_matches_reference(k):
+    """g2048_symmetries (8 dihedral nibble permutations + action remap) followed by g2048_obs == get_symmetries
+    (src/env.py:317-398): the transformed obs, the remapped action and -- recomputed from the transformed board
+    -- the remapped mask."""
+    from rl2048_amd import _lib as L
+
+    d = RF.load("symmetries")
+    mode, with_mask = json.loads(str(d[f"k{k}_kind"]))
+    bin_ = d[f"k{k}_board_in"]
+    if mode == "onehot":
+        ex = bin_.reshape(-1, 16, 17).argmax(-1)
+    elif mode == "raw":
+        ex = np.where(bin_ > 0, np.log2(np.maximum(bin_, 1)), 0).round().astype(np.int64)
+    else:
+        ex = np.round(bin_ / 0.25).astype(np.int64)
+    m = len(ex)
+    boards = torch.from_numpy(np.array([O.pack_exponents(e) for e in ex], dtype=np.uint64).view(np.int64)).to(DEV)
+    acts = torch.from_numpy(d[f"k{k}_action_in"].copy()).to(DEV)
+    ob = torch.empty(8 * m, dtype=torch.int64, device=DEV)
+    oa = torch.empty(8 * m, dtype=torch.uint8, device=DEV)
+    lib, s = L.lib(), L.stream_handle(DEV)
+    L.check(lib.g2048_symmetries(L.ptr(boards), L.ptr(acts), L.ptr(ob), L.ptr(oa), m, s))
+    w = 272 if mode == "onehot" else 16
+    code = {"raw": L.OBS_RAW, "log2": L.OBS_LOG2, "onehot": L.OBS_ONEHOT}[mode]
+    x = torch.empty(8 * m, w, dtype=torch.float32, device=DEV)
+    mk = torch.empty(8 * m, 4, dtype=torch.int8, device=DEV)
+    L.check(lib.g2048_obs(L.ptr(ob), code, 0.25, L.ptr(x), L.ptr(mk), 8 * m, s))
+    x = x.view(8, m, w).permute(1, 0, 2).cpu().numpy()
+    mk = mk.view(8, m, 4).permute(1, 0, 2).cpu().numpy()
+    oa = oa.view(8, m).t().cpu().numpy()
+    np.testing.assert_array_equal(x, d[f"k{k}_board_out"])
+    np.testing.assert_array_equal(oa, d[f"k{k}_action_out"])
+    if with_mask:
+        np.testing.assert_array_equal(mk, d[f"k{k}_mask_out"])
+
+
+# ===================================================================================================== agent
+def _agent(case: dict):
+    from rl2048_amd import Game2048EnvConfig
+    from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
+    from rl2048_amd.mlp import MLPConfig
+
+    return ReinforceAgent(Game2048EnvConfig(**case["env"]), MLPConfig(**case["mlp"]),
+                          ReinforceAgentConfig(**case["agent"]), device=DEV)
+
+
+def _set_params(agent, params: dict, critic: bool = False):
+    t = {k: [torch.from_numpy(a.copy()).to(DEV) for a in v] for k, v in params.items()}
+    if critic:
+        agent.critic_params = t
+    else:
+        agent.params = t
+    agent._params_version += 1
+
+
+def _params_before(ci: int, u: int, L: int, which: str):
+    return RF.params_of(ci, f"init_{which}" if u == 0 else f"up{u - 1}_{which}", L)
+
+
+ROLLOUT_PATHS = ["rollout", "policy", "gemm"]
+
+
+@pytest.mark.parametrize("ci", range(34))
+def test_rollout_matches_reference_run_episode(ci):
+    """rollout_batch == the reference's run_episode for each (env_seed, policy_seed) of the fixture, from the
+    same parameters: every action (numpy Generator.choice replayed on the device), board, fp64 reward, episode
+    length, total reward and max tile.  Cases rotate over the three rollout paths (one launch / per-step fused
+    policy / per-step GEMMs + g2048_sample)."""
+    case = RF.update_cases()[ci]
+    L = RF.n_layers(case)
+    agent = _agent(case)
+    path = ROLLOUT_PATHS[ci % 3]
+    agent.use_fused_policy = path != "gemm"
+    agent.use_fused_rollout = path == "rollout"
+    for u in range(case["updates"]):
+        P = f"up{u}_"
+        _set_params(agent, _params_before(ci, u, L, "actor"))
+        es = [int(s) for s in RF.arr(ci, P + "env_seeds")]
+        ps = [int(s) for s in RF.arr(ci, P + "policy_seeds")]
+        batch = agent.rollout_batch(es, ps, record_probs=True)
+        lens = RF.arr(ci, P + "lengths")
+        np.testing.assert_array_equal(batch.lengths.cpu().numpy(), lens)
+        boards, acts = _u64(batch.boards), batch.actions.cpu().numpy()
+        rews, probs = batch.rewards.cpu().numpy(), batch.probs.cpu().numpy()
+        assert batch.rewards.dtype == torch.float64
+        s = 0
+        for i, T in enumerate(lens):
+            T = int(T)
+            np.testing.assert_array_equal(boards[:T, i], RF.arr(ci, P + "boards")[s:s + T])
+            np.testing.assert_array_equal(acts[:T, i], RF.arr(ci, P + "actions")[s:s + T], err_msg=f"{path} ep {i}")
+            np.testing.assert_array_equal(rews[:T, i], RF.arr(ci, P + "rewards")[s:s + T])
+            np.testing.assert_allclose(probs[:T, i], RF.arr(ci, P + "probs")[s:s + T], rtol=0, atol=2e-6)
+            s += T
+        np.testing.assert_array_equal(batch.total_reward.cpu().numpy(), RF.arr(ci, P + "total_reward"))
+        np.testing.assert_array_equal(batch.max_tile.cpu().numpy(), RF.arr(ci, P + "max_tile"))
+
+
+def _batch_from_fixture(ci: int, u: int):
+    """The reference's trajectories of update u as a device TrajectoryBatch (time-major)."""
+    from rl2048_amd.agent import TrajectoryBatch
+
+    P = f"up{u}_"
+    lens = RF.arr(ci, P + "lengths")
+    n, T = len(lens), int(lens.max())
+    boards = np.zeros((T, n), dtype=np.uint64)
+    acts = np.zeros((T, n), dtype=np.uint8)
+    rews = np.zeros((T, n), dtype=np.float64)
+    s = 0
+    for i, Ti in enumerate(lens):
+        Ti = int(Ti)
+        boards[:Ti, i] = RF.arr(ci, P + "boards")[s:s + Ti]
+        acts[:Ti, i] = RF.arr(ci, P + "actions")[s:s + Ti]
+        rews[:Ti, i] = RF.arr(ci, P + "rewards")[s:s + Ti]
+        s += Ti
+    t = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    return TrajectoryBatch(boards=t(boards.view(np.int64)), actions=t(acts), rewards=t(rews),
+                           flags=torch.zeros(T, n, dtype=torch.uint8, device=DEV),
+                           lengths=t(lens.astype(np.int32)), total_reward=t(RF.arr(ci, P + "total_reward").copy()),
+                           max_tile=t(RF.arr(ci, P + "max_tile").copy()),
+                           final_boards=torch.zeros(n, dtype=torch.int64, device=DEV))
+
+
+def assert_step_matches(got_after, got_before, ref_after, ref_before, grads_ref, noisy_prev, lr, adam):
+    """Parameters after one update.  SGD (linear in the gradient): within rtol 1e-5.  Adam: its step
+    lr * m_hat / (sqrt(v_hat) + eps) depends on the gradient only through ratios of its history, so it is compared
+    as a step (ours from our parameters, the reference's from its own) on the well-conditioned elements -- whose
+    reference gradient exceeds 1e-3 of its tensor's largest in every update so far -- within 5e-2 lr; on the
+    others (their sign within the north star's 1e-5 normwise tolerance is rounding noise) only |step| <= 3 lr is
+    required.  Returns the updated ill-conditioned masks."""
+    out = []
+    for k, (ga, gb, ra, rb, gr) in enumerate(zip(got_after, got_before, ref_after, ref_before, grads_ref)):
+        ga, gb, ra, rb = (np.asarray(x, np.float64) for x in (ga, gb, ra, rb))
+        gr = np.asarray(gr, np.float64)
+        if not adam:
+            np.testing.assert_allclose(ga, ra, rtol=1e-5, atol=1e-7 + 1e-5 * lr * np.abs(gr).max())
+            out.append(None)
+            continue
+        noisy = np.abs(gr) <= 1e-3 * max(np.abs(gr).max(), 1e-30)
+        if noisy_prev is not None and noisy_prev[k] is not None:
+            noisy = noisy | noisy_prev[k]
+        np.testing.assert_allclose((ga - gb)[~noisy], (ra - rb)[~noisy], rtol=0,
+                                   atol=5e-2 * lr + 1e-6 * np.abs(ra).max(), err_msg=f"tensor {k}")
+        assert np.all(np.abs(ga - gb)[noisy] <= 3 * lr + 1e-6)
+        out.append(noisy)
+    return out
+
+
+@pytest.mark.parametrize("path", ["device", "dropin"])
+@pytest.mark.parametrize("ci", range(34))
+def test_update_matches_reference_update_batch(ci, path):
+    """update_from_batch (device trajectory buffer: fused gradient kernels where the net fits) and update_batch
+    (drop-in, reference trajectory dicts) == src/reinforce_agent.py update_batch, update after update: pre-clip
+    gradients (captured at clip_grads_global_norm), norms, parameters after SGD / Adam (actor and critic)."""
+    case = RF.update_cases()[ci]
+    L = RF.n_layers(case)
+    agent = _agent(case)
+    crit = RF.has(ci, "init_critic_0")
+    # the agent's own initialisation is the reference's (init_model_params, actor then critic from one rng)
+    init = RF.params_of(ci, "init_actor", L)
+    for a, b in zip(agent.params["W"] + agent.params["b"], init["W"] + init["b"]):
+        np.testing.assert_array_equal(a.cpu().numpy(), b)
+    if crit:
+        cinit = RF.params_of(ci, "init_critic", L)
+        for a, b in zip(agent.critic_params["W"] + agent.critic_params["b"], cinit["W"] + cinit["b"]):
+            np.testing.assert_array_equal(a.cpu().numpy(), b)
+    lr = case["agent"].get("learning_rate", 1e-3)
+    lr_c = case["agent"].get("critic_learning_rate", 1e-3)
+    adam = case["agent"].get("optimizer", "sgd") == "adam"
+    noisy_a = noisy_c = None
+    for u in range(case["updates"]):
+        P = f"up{u}_"
+        if u:
+            # continue from the reference's parameters (our Adam moments carry over): the gradient of update u is
+            # then taken at the same point, not at ours, which differ from the reference's by rounding-level
+            # Adam steps on ill-conditioned elements
+            _set_params(agent, _params_before(ci, u, L, "actor"))
+            if crit:
+                _set_params(agent, _params_before(ci, u, L, "critic"), critic=True)
+        before = [p.cpu().numpy().copy() for p in agent.params["W"] + agent.params["b"]]
+        cbefore = [p.cpu().numpy().copy() for p in agent.critic_params["W"] + agent.critic_params["b"]] if crit \
+            else None
+        if path == "device":
+            stats = agent.update_from_batch(_batch_from_fixture(ci, u))
+        else:
+            agent.update_batch(RF.trajectories(ci, u, case))
+            stats = agent.last_stats
+        gref = [RF.arr(ci, P + f"actor_grad_{j}") for j in range(2 * L)]
+        exact = lambda: RF.exact_grads(ci, u, case)  # noqa: E731
+        for j, (g, r) in enumerate(zip(agent.last_grads["actor"], gref)):
+            RF.assert_grad_parity(g.cpu().numpy(), r, lambda: exact()["actor"][j], (u, "actor", j))
+        nref = float(RF.arr(ci, P + "actor_norm"))
+        RF.assert_norm_parity(stats["actor_grad_norm"], nref, lambda: exact()["actor"], (u, "actor norm"))
+        ref, rb = RF.params_of(ci, P + "actor", L), _params_before(ci, u, L, "actor")
+        noisy_a = assert_step_matches([p.cpu().numpy() for p in agent.params["W"] + agent.params["b"]], before,
+                                      ref["W"] + ref["b"], rb["W"] + rb["b"], gref, noisy_a, lr, adam)
+        if crit:
+            cref = [RF.arr(ci, P + f"critic_grad_{j}") for j in range(2 * L)]
+            for j, (g, r) in enumerate(zip(agent.last_grads["critic"], cref)):
+                RF.assert_grad_parity(g.cpu().numpy(), r, lambda: exact()["critic"][j], (u, "critic", j))
+            cn = float(RF.arr(ci, P + "critic_norm"))
+            RF.assert_norm_parity(stats["critic_grad_norm"], cn, lambda: exact()["critic"], (u, "critic norm"))
+            ref, rb = RF.params_of(ci, P + "critic", L), _params_before(ci, u, L, "critic")
+            noisy_c = assert_step_matches(
+                [p.cpu().numpy() for p in agent.critic_params["W"] + agent.critic_params["b"]], cbefore,
+                ref["W"] + ref["b"], rb["W"] + rb["b"], cref, noisy_c, lr_c, adam)
+
+
+def test_returns_and_rank_weights_match_reference():
+    """compute_returns (fp64 scan of non-dyadic fp64 rewards, fp32 result) bit-exact; rank weights on near ties."""
+    from test_oracle_ref_fixtures import assert_rank_weights_match
+
+    from rl2048_amd import dp
+
+    d = RF.load("small")
+    rewards = [float(x) for x in d["returns_rewards"]]
+    for gi in range(4):
+        agent = _agent({"env": {}, "mlp": {"hidden_sizes": [4]}, "agent": {"gamma": float(d[f"returns_gamma{gi}"])}})
+        np.testing.assert_array_equal(agent.compute_returns(rewards), d[f"returns_g{gi}"])
+    for si in range(3):
+        tot = torch.from_numpy(d[f"rank_totals{si}"].copy()).to(DEV)
+        for cj, conf in enumerate(json.loads(str(d["rank_confs"]))):
+            assert_rank_weights_match(d[f"rank_totals{si}"], dp.rank_weights(tot, conf).cpu().numpy(),
+                                      d[f"rank_w{si}_{cj}"])
+
+
+# ===================================================================================================== runner
+def test_runner_matches_reference_training_and_evaluation(tmp_path):
+    """runner.training_loop / evaluation_loop on the batched path == the reference runner.py (:495-679,
+    :737-828) at the fixture's tiny config: every CSV row (fp32 avg / max / min of the batch totals, max-tile
+    counts), the actor after 3 Adam updates, and both evaluation summaries (greedy, stochastic)."""
+    from rl2048_amd import runner as R
+
+    d = RF.load("runner")
+    conf = json.loads(str(d["conf"]))
+    R.reset_defaults()
+    try:
+        R.apply_config_overrides_from_dict(conf)
+        agent, ec, mc, ac, tc = R.build_training_components(DEV)
+        rows = R.training_loop(agent, ec, mc, ac, tc, tmp_path, "golden")
+        assert [r["batch"] for r in rows] == list(d["train_batch"])
+        for k in ("avg_reward", "max_reward", "min_reward"):
+            np.testing.assert_array_equal([r[k] for r in rows], d["train_" + k], err_msg=k)
+        assert [json.loads(r["max_tile_counts"]) for r in rows] == d["train_max_tile_counts"].tolist()
+        header = (tmp_path / "training_stats.csv").read_text().splitlines()[0].split(",")
+        assert header == json.loads(str(d["train_csv_header"]))
+        L = len(agent.params["W"])
+        for j, p in enumerate(agent.params["W"] + agent.params["b"]):
+            r = d[f"train_final_actor_{j}"]
+            assert RF.rel(p.cpu().numpy(), r) < 1e-4, j
+        for gi, greedy in enumerate((True, False)):
+            s = R.evaluation_loop(agent, dict(conf["eval"], use_greedy=greedy))
+            assert s["episodes"] == int(d[f"eval{gi}_episodes"])
+            np.testing.assert_array_equal([s["avg_reward"], s["max_reward"], s["min_reward"]], d[f"eval{gi}_summary"])
+            ref_tiles = {int(k): v for k, v in json.loads(str(d[f"eval{gi}_max_tiles"])).items()}
+            assert s["max_tile_counts"] == ref_tiles
+        assert L == 3
+    finally:
+        R.reset_defaults()

@@ -11,12 +11,12 @@ O=$R/gpurun_out/ab_grad
 mkdir -p "$O"
 T=$1
 shift
-G2048_DIAG_LIB=$R/tools/libg2048_$T.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_grad.py -x -q \
+G2048_TOOLS_LIB=$R/tools/libg2048_$T.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_grad.py -x -q \
     --timeout 240 --timeout-method thread -p no:cacheprovider > "$O/tests_$T.log" 2>&1 || exit 1
 i=0
 for v in "$@"; do
     i=$((i + 1))
-    G2048_DIAG_LIB=$R/tools/libg2048_$v.so timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$O/$i-$v" -o run -- python3 "$R/tools/bench_update.py" --episodes 65536 --repeats 2 --critic \
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$O/$i-$v" -o run -- python3 "$R/tools/bench_update.py" --episodes 65536 --repeats 2 --critic --lib $R/tools/libg2048_$v.so \
         > "$O/$i-$v.log" 2>&1 || exit 1
 done

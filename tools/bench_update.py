@@ -23,10 +23,15 @@ def main():
     ap.add_argument("--critic", action="store_true")
     ap.add_argument("--max-steps", type=int, default=1024)
     ap.add_argument("--repeats", type=int, default=2)
+    ap.add_argument("--lib", default=None, help="another build of libg2048 (A/B scripts)")
     args = ap.parse_args()
     import torch
 
     from rl2048_amd import Game2048EnvConfig
+    from rl2048_amd import _lib as L
+
+    if args.lib:
+        L.use_library_for_tools(args.lib)
     from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
     from rl2048_amd.mlp import MLPConfig
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Timing-attribution build of the step kernel (-DG2048_DIAG=1: G2048_DIAG_FLAGS removes pieces of the kernel,
-# see csrc/g2048.hip).  Loaded instead of the shipped library when G2048_DIAG_LIB points at it.  Never shipped.
+# see csrc/g2048.hip).  Loaded instead of the shipped library only through _lib.use_library_for_tools (tools, bench.py --lib).  Never shipped.
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG="$ROOT/rl-2048-with-reinforce-and-actor-critic_amd"

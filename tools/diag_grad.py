@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--critic", action="store_true")
     args = ap.parse_args()
     assert os.environ.get("G2048_DIAG_LIB"), "set G2048_DIAG_LIB to the diag build"
+    from rl2048_amd import _lib as _L0
+
+    _L0.use_library_for_tools(os.environ["G2048_DIAG_LIB"])
     import torch
 
     from rl2048_amd import Game2048EnvConfig

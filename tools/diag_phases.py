@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--launches", type=int, default=5)
     args = ap.parse_args()
     assert os.environ.get("G2048_DIAG_LIB"), "set G2048_DIAG_LIB to the diag build"
+    from rl2048_amd import _lib as _L0
+
+    _L0.use_library_for_tools(os.environ["G2048_DIAG_LIB"])
     import torch
 
     import bench

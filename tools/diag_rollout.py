@@ -24,6 +24,7 @@ def main():
 
     from rl2048_amd import Game2048EnvConfig
     from rl2048_amd import _lib as L
+    L.use_library_for_tools(os.environ["G2048_DIAG_LIB"])
     from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
     from rl2048_amd.mlp import MLPConfig
 
