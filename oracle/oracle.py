@@ -90,6 +90,12 @@ def lib():
         L.or_move_packed.argtypes = [ctypes.c_uint64, ctypes.c_int, P(ctypes.c_uint64), P(ctypes.c_int64),
                                      P(ctypes.c_int32), P(ctypes.c_int32)]
         L.or_move_packed.restype = ctypes.c_int
+        L.or_philox4x32_10.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
+        L.or_env_reset_philox.argtypes = [P(EnvState), ctypes.c_uint64, ctypes.c_uint64]
+        L.or_env_step_philox.argtypes = [P(EnvState), P(EnvCfg), ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                         P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_int32), P(ctypes.c_int32),
+                                         P(ctypes.c_int32)]
+        L.or_env_step_philox.restype = ctypes.c_int
         L.or_bench_env_steps.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, P(EnvCfg),
                                          P(ctypes.c_double)]
         L.or_bench_env_steps.restype = ctypes.c_int64
@@ -223,22 +229,43 @@ def make_env_cfg(**kw) -> EnvCfg:
     return c
 
 
-class Env:
-    """Oracle twin of src/env.py:Game2048Env (reset/step/obs/mask)."""
+def philox4x32_10(ctr, key) -> list[int]:
+    c = (ctypes.c_uint32 * 4)(*[int(x) & 0xFFFFFFFF for x in ctr])
+    k = (ctypes.c_uint32 * 2)(*[int(x) & 0xFFFFFFFF for x in key])
+    out = (ctypes.c_uint32 * 4)()
+    lib().or_philox4x32_10(c, k, out)
+    return list(out)
 
-    def __init__(self, **cfg):
+
+class Env:
+    """Oracle twin of src/env.py:Game2048Env (reset/step/obs/mask).  rng="philox" replays the build's Philox
+    throughput-mode spawn stream (key `philox_key`, the current episode's seed) instead of numpy's PCG64."""
+
+    def __init__(self, rng: str = "pcg64", philox_key: int = 0x2048, **cfg):
         self.cfg = make_env_cfg(**cfg)
         self.e = EnvState()
+        self.rng = rng
+        self.key = int(philox_key) & 0xFFFFFFFFFFFFFFFF
+        self.seed = 0
 
     def reset(self, seed: int):
-        lib().or_env_reset(ctypes.byref(self.e), ctypes.c_uint64(seed))
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        if self.rng == "philox":
+            lib().or_env_reset_philox(ctypes.byref(self.e), ctypes.c_uint64(self.seed), ctypes.c_uint64(self.key))
+        else:
+            lib().or_env_reset(ctypes.byref(self.e), ctypes.c_uint64(seed))
         return self.obs(), self.mask()
 
     def step(self, action: int):
         r = ctypes.c_double()
         ch, te, tr, inv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
-        rc = lib().or_env_step(ctypes.byref(self.e), ctypes.byref(self.cfg), action, ctypes.byref(r), ctypes.byref(ch),
-                               ctypes.byref(te), ctypes.byref(tr), ctypes.byref(inv))
+        if self.rng == "philox":
+            rc = lib().or_env_step_philox(ctypes.byref(self.e), ctypes.byref(self.cfg), action,
+                                          ctypes.c_uint64(self.seed), ctypes.c_uint64(self.key), ctypes.byref(r),
+                                          ctypes.byref(ch), ctypes.byref(te), ctypes.byref(tr), ctypes.byref(inv))
+        else:
+            rc = lib().or_env_step(ctypes.byref(self.e), ctypes.byref(self.cfg), action, ctypes.byref(r),
+                                   ctypes.byref(ch), ctypes.byref(te), ctypes.byref(tr), ctypes.byref(inv))
         if rc != 0:
             raise AssertionError(f"Invalid action: {action}")
         return dict(reward=r.value, changed=bool(ch.value), terminated=bool(te.value), truncated=bool(tr.value),

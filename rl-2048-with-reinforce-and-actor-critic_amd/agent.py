@@ -455,8 +455,10 @@ class ReinforceAgent:
         waves = int(self._lib.g2048_actor_grad_waves())
         pf = int(self._lib.g2048_grad_partial_size(h1, h2))
         part = torch.empty(waves, pf, dtype=torch.float32, device=self.device)
-        small = torch.zeros(pf, dtype=torch.float32, device=self.device)
-        big = torch.zeros(H1p + 1, H2p, dtype=torch.float32, device=self.device)
+        # cross-chunk / cross-block sums in fp64: at millions of samples the fp32 error of the gradient is set by
+        # how long each fp32 accumulation runs (tests/test_gpu_configs_at_size.py measures it against fp64)
+        small = torch.zeros(pf, dtype=torch.float64, device=self.device)
+        big = torch.zeros(H1p + 1, H2p, dtype=torch.float64, device=self.device)
         obs_code, scale = _OBS_CODE[self.env_config.obs_mode], float(self.env_config.obs_log2_scale)
         flat = steps.boards.reshape(-1)
         for k in range(K):
@@ -465,14 +467,18 @@ class ReinforceAgent:
                 b = flat[steps.vidx[sel]].contiguous()
                 if k:
                     b = self._symmetry_boards(b, k)
-                P = max(1, min(64, m // 8192))       # split-K of the layer-2 weight gradient over P column blocks
+                # split-K of the layer-2 weight gradient over P column blocks of ~2048 samples (each an fp32 GEMM
+                # accumulation), the blocks summed in fp64
+                P = max(1, min(512, m // 2048))
                 ld = -(-m // (32 * P)) * 32 * P
                 q = ld // P
                 a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
                 d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
                 launch(k, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale)
-                big += torch.bmm(a1t.view(H1p + 1, P, q).transpose(0, 1), d2t.view(H2p, P, q).permute(1, 2, 0)).sum(0)
-                small += part.sum(0)
+                big += torch.bmm(a1t.view(H1p + 1, P, q).transpose(0, 1),
+                                 d2t.view(H2p, P, q).permute(1, 2, 0)).sum(0, dtype=torch.float64)
+                small += part.sum(0, dtype=torch.float64)
+        big, small = big.to(torch.float32), small.to(torch.float32)
         gW[0] += small[:16 * H1p].view(16, H1p)[:, :h1]
         gb[0] += small[16 * H1p:17 * H1p][:h1]
         gW[1] += big[:h1, :h2]

@@ -92,4 +92,9 @@ double ch_reward(int reward_mode, int bonus_mode, int use_mask, const double* sc
     s.count = count; s.sum_e = sum_e; s.score = score; s.max_e = max_e;
     return env_reward(c, s, final_board, done != 0, invalid != 0, *max_tile_e);
 }
+void ch_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    const U4 r = philox4x32(U4{ctr[0], ctr[1], ctr[2], ctr[3]}, key[0], key[1]);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
+}
+uint64_t ch_spawn_philox(uint64_t b, uint32_t x, uint32_t y) { return spawn_philox(b, U4{x, y, 0u, 0u}); }
 }

@@ -34,6 +34,9 @@ def ch():
     L.ch_board_move_coded.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [u32p] * 6
     L.ch_board_move_coded_nolist.restype = ctypes.c_uint64
     L.ch_board_move_coded_nolist.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [u32p] * 6
+    L.ch_philox.argtypes = [u32p, u32p, u32p]
+    L.ch_spawn_philox.restype = ctypes.c_uint64
+    L.ch_spawn_philox.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
     L.ch_bits_mask.restype = ctypes.c_uint32
     L.ch_bits_mask.argtypes = [ctypes.c_uint64]
     L.ch_bits_done.argtypes = [ctypes.c_uint64]
@@ -192,3 +195,32 @@ def test_reward_vs_oracle(ch, cfg):
             assert (1 << mt.value) == env.max_tile_seen
             if r["terminated"] or r["truncated"]:
                 break
+
+
+# Random123 known-answer vectors for philox4x32 with 10 rounds (kat_vectors of the published library)
+PHILOX_KAT = [([0, 0, 0, 0], [0, 0], [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]),
+              ([0xffffffff] * 4, [0xffffffff] * 2, [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]),
+              ([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0],
+               [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1])]
+
+
+def test_philox_kat_and_spawn_vs_oracle(ch):
+    """The build's Philox4x32-10 (throughput mode) against Random123's known answers, and its spawn against the
+    oracle's independent restatement of the same spec on random boards / draws."""
+    u32x4, u32x2 = ctypes.c_uint32 * 4, ctypes.c_uint32 * 2
+    for ctr, key, exp in PHILOX_KAT:
+        out = u32x4()
+        ch.ch_philox(u32x4(*ctr), u32x2(*key), out)
+        assert list(out) == exp
+        assert O.philox4x32_10(ctr, key) == exp
+    rng = np.random.default_rng(9)
+    for b in _rand_boards(rng, 2000):
+        x, y = (int(v) for v in rng.integers(0, 2**32, size=2, dtype=np.uint64))
+        got = ch.ch_spawn_philox(int(b), x, y)
+        e = O.unpack_exponents(int(b)).reshape(16)
+        empties = np.nonzero(e == 0)[0]
+        if len(empties) == 0:
+            assert got == int(b)
+            continue
+        cell = empties[(x * len(empties)) >> 32]
+        assert got == int(b) | ((1 if y < 3865470566 else 2) << (4 * int(cell)))

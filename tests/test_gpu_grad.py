@@ -94,8 +94,8 @@ def test_fused_critic_grad_matches_batched_backprop(case):
 @pytest.mark.parametrize("critic", [False, True], ids=["actor", "actor_critic"])
 def test_fused_grad_one_large_chunk_split_k(critic):
     """One chunk of > 2^17 samples (the default chunk size, so a single launch): the layer-2 weight gradient then runs
-    as a split-K batched GEMM over P = m // 8192 > 16 column blocks of a1^T / d2^T (the small-batch cases above use
-    P = 1), and the kernel's column buffers are wide (ld > 2^17).  Gradients within 1e-5 of the torch backprop."""
+    as a split-K batched GEMM over P = m // 2048 > 64 column blocks of a1^T / d2^T (the small-batch cases above use
+    P = 2), and the kernel's column buffers are wide (ld > 2^17).  Gradients within 1e-5 of the torch backprop."""
     acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.99)
     if critic:
         acfg.update(use_critic=True, critic_loss_type="mse")
@@ -139,3 +139,34 @@ def test_update_matches_oracle_unmasked():
             assert _rel(a, b) < 1e-5, path
         for a, b in zip(ag.params["W"] + ag.params["b"], ora.params["W"] + ora.params["b"]):
             np.testing.assert_allclose(a.cpu().numpy(), b, rtol=1e-5, atol=2e-7)
+
+
+@pytest.mark.parametrize("act", ["Sigmoid", "ReLU"])
+@pytest.mark.parametrize("chunk", [4096 + 17, 8192 * 17 + 5])
+def test_fused_critic_grad_ragged_chunks(chunk, act):
+    """Regression for the round-1 hipErrorIllegalAddress seen after the 256x256 critic's V(s') launch
+    ("Fault audit"): every chunk of the fused critic + actor gradient is ragged (m not a
+    multiple of 32, so the last 32-sample group of each launch is partial), the last chunk is short, and the
+    second size makes the split-K layer-2 GEMM run P = 68 column blocks; the device stays healthy (a
+    synchronising copy after each update).  Gradients against the torch backprop: within 1e-5 for Sigmoid; for
+    ReLU within 5e-5, because at ~150k samples the two fp32 forwards flip a few ReLU derivatives of
+    pre-activations rounded next to 0 on different samples (tests/test_gpu_configs_at_size.py measures this
+    against fp64)."""
+    acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.97, use_critic=True, critic_loss_type="mse")
+    grads = {}
+    batch = None
+    for fused in (True, False):
+        ag = _agent((256, 256), act, **acfg)
+        ag.use_fused_grad = fused
+        if batch is None:
+            batch = ag.rollout_batch(list(range(3000, 3000 + 1200)), list(range(7000, 7000 + 1200)))
+        ag.grad_chunk_steps = chunk
+        ag.update_from_batch(batch)
+        torch.cuda.synchronize()
+        grads[fused] = {k: [g.cpu().numpy() for g in v] for k, v in ag.last_grads.items()}
+    N = int(batch.lengths.sum())
+    assert N % chunk and (N % chunk) % 32 and N > chunk, (N, chunk)
+    tol = 1e-5 if act == "Sigmoid" else 5e-5
+    for which in ("critic", "actor"):
+        for i, (a, b) in enumerate(zip(grads[True][which], grads[False][which])):
+            assert _rel(a, b) < tol, (which, i, _rel(a, b))
