@@ -12,10 +12,13 @@ per-lane seeds seed0 + global lane for auto-reset.  Weak scaling: every GPU owns
     python bench.py [--gpus N --steps K --warmup W --boards B --rng pcg64|philox --obs log2|onehot|raw|none]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line.  Extras: `roofline` of the step kernel (algorithmic bytes / HIP-event kernel time vs
-8 TB/s; `traffic` = HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes when rocprofv3 is present),
-`cpu_baseline` (the C oracle's env step on host cores, a bounded sample), and `policy_rollout` (env steps/s with
-the [256,256] ReLU policy MLP + on-device sampling in the loop, N=1 only).
+Rank 0 prints ONE JSON line.  Extras: `roofline` of the step kernel (SURVEY.md section 8(d)'s algorithmic bytes per
+board-step / HIP-event kernel time vs 8 TB/s; the build's layout bytes beside them; `traffic` = HBM bytes per launch
+from rocprofv3 FETCH_SIZE/WRITE_SIZE passes when rocprofv3 is present), `cpu_baseline` (the reference's CPU step
+loop restated in Python -- oracle/pyref.py, pinned to the reference -- one process per host core, a bounded sample;
+the C port beside it), `train_iteration_dp` (configs[3]'s training iteration per GPU shard, every rank, with the
+gradient all-reduce inside the timed region) and, at N=1, `policy_rollout` (env steps/s with the [256,256] ReLU
+policy MLP + on-device sampling in the loop; the configs[1] / configs[2] training iterations).
 """
 from __future__ import annotations
 
@@ -38,7 +41,13 @@ POLICY_FLOP_PER_BOARD = 2 * (16 * 256 + 256 * 256 + 256 * 4)  # 141,312: the run
 # update per sample: forward + weight / input gradients of layers 2 and 3, weight gradient of layer 1
 UPDATE_FLOP_PER_SAMPLE = POLICY_FLOP_PER_BOARD + 2 * (256 * 256 * 2 + 256 * 4 * 2 + 16 * 256)
 
-# Algorithmic bytes one g2048_step moves per board in steady state (no reset), by mode.  Reads / writes:
+# ALGORITHMIC bytes per board-step -- SURVEY.md section 8(d)'s table, the roofline's numerator: core (board
+# 8/8, action 1, reward 4, flags 1) 22 B + env lane state (step count u16, max tile exp u8, pad) 8 B = 30 B (Philox,
+# counter from the step), + the numpy-PCG64-compatible RNG (state 16 r/w, inc 16 r, uinteger 4 + has 1 r/w) = 88 B;
+# obs: + 64 B log2 / raw fp32, + 1092 B one-hot fp32 + int8 mask.
+SURVEY_RNG_BYTES = {"pcg64": 88, "philox": 30}
+SURVEY_OBS_BYTES = {"none": 0, "raw": 64, "log2": 64, "onehot": 1092}
+# LAYOUT bytes: what this build's structure-of-arrays lane layout actually moves per board-step (reads / writes):
 #   board 8/8, action 1/-, status 1/-, step_count 4/4, max_tile 1/1, score 4/4, reward -/4, flags -/1, mask -/4
 #   PCG64: rng_state 16/16, rng_inc 16/-, rng_buf 8/8          Philox: lane seed 8/-
 #   obs: log2/raw -/64, onehot -/1088
@@ -47,7 +56,12 @@ RNG_BYTES = {"pcg64": (40, 24), "philox": (8, 0)}
 OBS_BYTES = {"none": 0, "raw": 64, "log2": 64, "onehot": 1088}
 
 
+def survey_bytes_per_step(rng: str, obs: str) -> int:
+    return SURVEY_RNG_BYTES[rng] + SURVEY_OBS_BYTES[obs]
+
+
 def bytes_per_step(rng: str, obs: str) -> tuple[int, int]:
+    """Layout bytes (reads, writes) per board-step."""
     r = CORE_R + RNG_BYTES[rng][0]
     w = CORE_W + RNG_BYTES[rng][1] + OBS_BYTES[obs]
     return r, w
@@ -61,7 +75,10 @@ def parse():
     ap.add_argument("--boards", type=int, default=1 << 20, help="boards per GPU")
     ap.add_argument("--rng", default="pcg64", choices=["pcg64", "philox"])
     ap.add_argument("--obs", default="log2", choices=["log2", "onehot", "raw", "none"])
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--train-episodes", type=int, default=1 << 19,
+                    help="episodes per GPU of the data-parallel training-iteration leg (configs[3]'s shard)")
+    ap.add_argument("--no-train", action="store_true", help="skip the data-parallel training-iteration leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"])
     ap.add_argument("--no-policy", action="store_true")
@@ -148,26 +165,58 @@ def pmc_traffic(args) -> dict | None:
 
 
 # ---------------------------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(args, seconds: float) -> dict:
-    from oracle import oracle as O
+def host_cores() -> dict:
+    """Cores this process may use: the affinity set, capped by a cgroup CPU quota when there is one (the GPU box
+    grants a share of a larger machine; os.cpu_count() reports the whole machine)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    return {"cores": max(1, min(aff, int(quota))) if quota else aff, "affinity_cores": aff, "cgroup_cpu_quota": quota}
 
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(cores, 16))
-    os.environ["OMP_NUM_THREADS"] = str(cores)
+
+# oracle/pyref.py's single-core speed relative to the real src/env.py on the same workload, measured in the build
+# container where the reference exists (tools/pyref_ratio.py -> profiles/round2/pyref_ratio.txt)
+PYREF_OVER_REFERENCE = 1.442
+
+
+def cpu_baseline(args, seconds: float) -> dict:
+    """The reference's CPU step loop on this box's host cores: oracle/pyref.py (the Python + NumPy restatement of
+    src/game2048.py + src/env.py, pinned bit for bit to the reference's outputs) as one process per core, each
+    stepping its own boards (obs + action mask every step, auto-reset), for a bounded `seconds`.  Beside it the
+    C port (oracle/g2048_oracle.c, OpenMP over the same cores)."""
+    from oracle import oracle as O
+    from oracle import pyref
+
+    hc = host_cores()
+    cores = hc["cores"]
     cfg = dict(obs_mode="log2" if args.obs == "none" else args.obs, obs_log2_scale=0.0625, reward_mode="log2",
                base_reward_scale=0.5, max_steps=1024)
+    steps, dt = pyref.bench(cores, seconds, cfg)
+    out = {"value": steps / dt, "unit": "env steps/s", "cores": cores, "kind": "port",
+           "sample": f"oracle/pyref.py (Python + NumPy restatement of src/game2048.py + src/env.py step loop, "
+                     f"{args.obs} obs + action mask, numpy PCG64 spawn), {cores} processes x 64 boards, "
+                     f"{steps} env steps in {dt:.1f} s",
+           "reference_equivalent": steps / dt / PYREF_OVER_REFERENCE,
+           "pyref_over_reference_single_core": PYREF_OVER_REFERENCE,
+           "affinity_cores": hc["affinity_cores"], "cgroup_cpu_quota": hc["cgroup_cpu_quota"]}
+    os.environ["OMP_NUM_THREADS"] = str(cores)
     boards = 64 * cores
     t0 = time.perf_counter()
-    steps, _ = O.bench_env_steps(boards, 32, **cfg)
-    dt = time.perf_counter() - t0
-    rounds = max(32, int(32 * seconds / max(dt, 1e-6)))
+    csteps, _ = O.bench_env_steps(boards, 32, **cfg)
+    cdt = time.perf_counter() - t0
+    rounds = max(32, int(32 * min(seconds, 5.0) / max(cdt, 1e-6)))
     t0 = time.perf_counter()
-    steps, _ = O.bench_env_steps(boards, rounds, **cfg)
-    dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "env steps/s", "cores": cores, "kind": "port",
-            "sample": f"C oracle (oracle/g2048_oracle.c, literal restatement of src/game2048.py + src/env.py step, "
-                      f"{args.obs} obs + action mask, numpy-PCG64 spawn) {boards} boards x {rounds} steps = "
-                      f"{steps} env steps in {dt:.1f} s, OpenMP over boards"}
+    csteps, _ = O.bench_env_steps(boards, rounds, **cfg)
+    cdt = time.perf_counter() - t0
+    out["c_port"] = {"value": csteps / cdt, "unit": "env steps/s", "cores": cores,
+                     "sample": f"oracle/g2048_oracle.c {boards} boards x {rounds} steps = {csteps} env steps in "
+                               f"{cdt:.1f} s, OpenMP"}
+    return out
 
 
 # ---------------------------------------------------------------------------------------------- policy loop
@@ -259,6 +308,71 @@ def train_iteration_rate(torch, device, episodes: int = 65536, repeats: int = 2,
     return out
 
 
+def train_iteration_dp(torch, device, episodes_per_rank: int, rank: int, world: int) -> dict:
+    """configs[3]'s training iteration, weak-scaled: every rank plays `episodes_per_rank` episodes of the global
+    batch (global episode g = rank * E + i; env seed 1000 + g, policy seed 2**40 + g, so N ranks play a partition
+    of one global batch) with the runner-default net (16-256-256-4 ReLU, REINFORCE, batch baseline, SGD), then
+    update_from_batch -- whose ONE gradient all-reduce (RCCL over xGMI on a multi-GPU node) is inside the timed
+    region.  One warm-up iteration, one timed; time = max over ranks; env steps summed over ranks.  The gradient
+    all-reduce alone is timed beside it (20 back-to-back dp.reduce_gradients_ of the same buffer)."""
+    import numpy as np
+    import torch.distributed as dist
+
+    from rl2048_amd import Game2048EnvConfig, dp
+    from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
+    from rl2048_amd.mlp import MLPConfig
+
+    agent = ReinforceAgent(Game2048EnvConfig(), MLPConfig(hidden_sizes=[256, 256], activation="ReLU",
+                                                          init_distribution="HeNormal"),
+                           ReinforceAgentConfig(baseline_mode="batch", gamma=0.99, learning_rate=1e-4), device=device)
+    E = int(episodes_per_rank)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    res = {}
+    for it in range(2):
+        base = 1000 + it * E * world + rank * E
+        es = np.arange(base, base + E, dtype=np.int64)
+        ps = es + (1 << 40)
+        barrier()
+        t0 = time.perf_counter()
+        batch = agent.rollout_batch(es, ps)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        agent.update_from_batch(batch)
+        barrier()
+        t2 = time.perf_counter()
+        res = {"rollout_s": t1 - t0, "update_s": t2 - t1, "iteration_s": t2 - t0,
+               "env_steps": int(batch.lengths.sum())}
+        del batch
+    n_par = sum(p.numel() for p in agent.params["W"] + agent.params["b"])
+    buf = [torch.zeros(n_par, dtype=torch.float32, device=device)]
+    dp.reduce_gradients_(buf, E)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        dp.reduce_gradients_(buf, E)
+    barrier()
+    ar_ms = (time.perf_counter() - t0) / 20 * 1e3
+    if world > 1:
+        t = torch.tensor([res["rollout_s"], res["update_s"], res["iteration_s"], ar_ms], dtype=torch.float64,
+                         device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        steps = torch.tensor([res["env_steps"]], dtype=torch.int64, device=device)
+        dist.all_reduce(steps)
+        res.update(rollout_s=float(t[0]), update_s=float(t[1]), iteration_s=float(t[2]), env_steps=int(steps[0]))
+        ar_ms = float(t[3])
+    backend = dist.get_backend() if world > 1 else "none (1 rank)"
+    return {"episodes": E * world, "episodes_per_gpu": E, **res,
+            "env_steps_per_s": res["env_steps"] / res["iteration_s"],
+            "grad_allreduce_ms": ar_ms, "grad_allreduce_bytes": 4 * (n_par + 1), "backend": str(backend),
+            "model": "REINFORCE, MLP 16-256-256-4 ReLU fp32, batch baseline (runner.py defaults)",
+            "scaling": "weak"}
+
+
 # ---------------------------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -340,11 +454,17 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
     if args.pmc_child:
         return
+    del actions
+    torch.cuda.empty_cache()
+    train = None
+    if not args.no_train and args.train_episodes > 0:
+        try:
+            train = train_iteration_dp(torch, device, args.train_episodes, rank, world)
+        except Exception as e:  # noqa: BLE001 -- an extra, never the headline
+            train = {"error": repr(e)}
     policy = None
     if rank == 0 and world == 1 and not args.no_policy:
         try:
-            del actions
-            torch.cuda.empty_cache()
             policy = policy_rollout_rate(torch, B, device)
             policy["gemm_path"] = policy_rollout_rate(torch, B, device, fused=False)
             policy["train_iteration_configs1"] = train_iteration_rate(torch, device)
@@ -359,8 +479,10 @@ def main():
     if rank != 0:
         return
     rb, wb = bytes_per_step(args.rng, args.obs)
-    alg_bytes = (rb + wb) * B
+    sb = survey_bytes_per_step(args.rng, args.obs)
+    alg_bytes = sb * B
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    layout_achieved = (rb + wb) * B / (kern_ms * 1e-3) / 1e9
     total_steps = K * B * world
     line = {
         "metric": METRIC, "value": total_steps / elapsed, "unit": "env steps/s", "n_gpus": world, "steps": K,
@@ -374,12 +496,18 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic["bytes"] if traffic else None,
-                     "algorithmic_bytes_per_launch": alg_bytes, "bytes_per_board_step": rb + wb,
+                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "bytes_per_board_step": sb, "bytes_basis": "SURVEY.md section 8(d) algorithmic bytes",
+                     "layout_bytes_per_board_step": rb + wb, "layout_achieved": layout_achieved,
+                     "layout_frac": layout_achieved / HBM_PEAK_GBS,
+                     "traffic_over_algorithmic": (traffic["bytes"] / alg_bytes) if traffic else None,
                      "kernel_ms": kern_ms, "kernel": "step_kernel (g2048_step)"},
         "cpu_baseline": cpu,
     }
     if traffic:
         line["roofline"]["traffic_detail"] = traffic
+    if train is not None:
+        line["train_iteration_dp"] = train
     if policy is not None:
         line["policy_rollout"] = policy
     print(json.dumps(line), flush=True)

@@ -147,8 +147,11 @@ class _Steps:
 
     def features(self, sel: torch.Tensor, k: int = 0, nxt: bool = False):
         """(x [m, D] f32, mask [m, 4] int8) of the valid steps `sel` (indices into vidx), symmetry k, or of
-        their successor step (nxt=True)."""
-        flat = self.vidx[sel] + (self.n if nxt else 0)
+        their successor step (nxt=True; a step without one -- its episode's last -- gives itself, masked by the
+        caller, like the reference's padding src/reinforce_agent.py:423)."""
+        flat = self.vidx[sel]
+        if nxt:
+            flat = torch.where(self.has_next[sel], flat + self.n, flat)
         if self.boards is not None:
             return self._board_obs(flat, k)
         x = self.X.reshape(self.T * self.n, -1)[flat]
@@ -405,7 +408,7 @@ class ReinforceAgent:
         writes.  Accumulates into gW / gb like mlp_backward_."""
         use_mask = int(bool(self.env_config.use_action_mask))
 
-        def launch(k, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale):
+        def launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale):
             a = steps.actions_k(sel, k).to(torch.uint8).contiguous()
             coef = (adv[k, sel] * step_w[sel]).contiguous()
             L.check(self._lib.g2048_actor_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, use_mask,
@@ -424,7 +427,7 @@ class ReinforceAgent:
         loss = {"mse": 0, "huber": 1}[c.critic_loss_type]
         flat = steps.boards.reshape(-1)
 
-        def launch(k, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale):
+        def launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale):
             fi, hn = steps.vidx[sel], steps.has_next[sel]
             bn = flat[torch.where(hn, fi + steps.n, fi)].contiguous()
             if k:
@@ -436,7 +439,6 @@ class ReinforceAgent:
                                            m, self._stream))
             tgt = (steps.rewards[sel] + (float(c.gamma) * lg[:, 0]) * hn.to(torch.float32)).contiguous()
             w = step_w[sel].contiguous()
-            s0 = int(sel[0])
             L.check(self._lib.g2048_critic_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, loss,
                                                 float(c.huber_delta), L.ptr(b), L.ptr(tgt), L.ptr(w),
                                                 L.ptr(deltas[k, s0:s0 + m]), m, ld, L.ptr(a1t), L.ptr(d2t), L.ptr(part),
@@ -462,8 +464,9 @@ class ReinforceAgent:
         obs_code, scale = _OBS_CODE[self.env_config.obs_mode], float(self.env_config.obs_log2_scale)
         flat = steps.boards.reshape(-1)
         for k in range(K):
-            for sel in self._chunks(steps.N, self.grad_chunk_steps):
-                m = int(sel.numel())
+            for s0 in range(0, steps.N, self.grad_chunk_steps):
+                m = min(self.grad_chunk_steps, steps.N - s0)
+                sel = torch.arange(s0, s0 + m, device=self.device)
                 b = flat[steps.vidx[sel]].contiguous()
                 if k:
                     b = self._symmetry_boards(b, k)
@@ -474,7 +477,7 @@ class ReinforceAgent:
                 q = ld // P
                 a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
                 d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
-                launch(k, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale)
+                launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale)
                 big += torch.bmm(a1t.view(H1p + 1, P, q).transpose(0, 1),
                                  d2t.view(H2p, P, q).permute(1, 2, 0)).sum(0, dtype=torch.float64)
                 small += part.sum(0, dtype=torch.float64)
@@ -733,7 +736,8 @@ class ReinforceAgent:
 
     def _advantages(self, values: torch.Tensor, lane: torch.Tensor, n_lanes: int, step_rank_w: torch.Tensor) -> torch.Tensor:
         """_compute_advantages (src/reinforce_agent.py:276-325) + _compute_weighted_stats (:864-881) over flat
-        steps; 'batch' statistics are global across ranks (one tiny all-reduce)."""
+        steps, on the device; 'batch' statistics are global across ranks (dp.batch_mean_std: one tiny
+        all-reduce, no host sync).  As in the reference, mean and std are applied in fp32."""
         mode = self.agent_config.baseline_mode
         if mode == "off":
             return values
@@ -745,11 +749,10 @@ class ReinforceAgent:
             return values - mean[lane]
         if mode not in ("batch", "batch_norm"):
             raise ValueError(f"Unknown baseline mode: {mode}")
-        mean, std = dp.weighted_stats(values, step_rank_w)
+        mean, std = dp.batch_mean_std(values, step_rank_w)
         if mode == "batch":
-            return (values - np.float32(mean)).to(torch.float32)
-        std = max(std, 1e-8)
-        return ((values - np.float32(mean)) / np.float32(std)).to(torch.float32)
+            return values - mean.to(torch.float32)
+        return (values - mean.to(torch.float32)) / std.clamp(min=1e-8).to(torch.float32)
 
     # ============================================================================================ optimiser
     def _init_adam(self, params, prefix="actor"):
@@ -762,19 +765,25 @@ class ReinforceAgent:
             self._adam_m_W_c, self._adam_v_W_c = z(params["W"]), z(params["W"])
             self._adam_m_B_c, self._adam_v_B_c = z(params["b"]), z(params["b"])
 
-    def clip_grads_global_norm(self, grad_W_list, grad_b_list):
-        """src/reinforce_agent.py:835-861: fp32 L2 over all W then all b; scale in place if > max_grad_norm."""
+    def _clip_(self, grads: list[torch.Tensor]) -> torch.Tensor:
+        """clip_grads_global_norm on the device: fp32 L2 over all W then all b, scaled in place by
+        max_norm / norm when that is < 1 (a multiply by exactly 1.0 otherwise).  Returns the norm as a device
+        scalar -- no host synchronisation."""
         max_norm = self.agent_config.max_grad_norm
         sq = torch.zeros((), dtype=torch.float32, device=self.device)
-        for g in list(grad_W_list) + list(grad_b_list):
+        for g in grads:
             sq = sq + torch.linalg.vector_norm(g.float()) ** 2
         total = torch.sqrt(sq)
-        tn = float(total)
-        coef = np.float32(max_norm) / np.float32(max(tn, 1e-8))
-        if coef < 1.0:
-            for g in list(grad_W_list) + list(grad_b_list):
-                g.mul_(float(coef))
-        return tn
+        coef = torch.tensor(np.float32(max_norm), device=self.device) / total.clamp(min=1e-8)
+        coef = torch.where(coef < 1.0, coef, torch.ones_like(coef))
+        for g in grads:
+            g.mul_(coef)
+        return total
+
+    def clip_grads_global_norm(self, grad_W_list, grad_b_list):
+        """src/reinforce_agent.py:835-861: scale the gradients in place if their global norm exceeds max_grad_norm;
+        returns the (pre-clip) norm as a Python float like the reference."""
+        return float(self._clip_(list(grad_W_list) + list(grad_b_list)))
 
     def _adam_update(self, grad_W_list, grad_b_list, prefix="actor") -> None:
         """src/reinforce_agent.py:719-770 (fp32, eps outside the sqrt, separate step counters)."""
@@ -834,16 +843,17 @@ class ReinforceAgent:
             yield torch.arange(s, min(N, s + size), device=self.device)
 
     def _update(self, steps: _Steps, totals: torch.Tensor) -> dict:
+        """update_batch (src/reinforce_agent.py:357-620) on a batch of valid steps.  Per-step weights are
+        rank_w / T_i; the 1 / n_traj factor is applied after the gradient all-reduce (dp.reduce_gradients_), so the
+        data-parallel update needs ONE gradient collective and nothing synchronises the host before the final
+        statistics."""
         c = self.agent_config
         n_local = steps.n
-        n_global = dp.global_count(n_local, self.device)
         K = 8 if c.augmentation else 1
-        n_traj = n_global * K
         rank_w = self._compute_episode_rank_weights(totals)               # [n_local]
         lane = steps.lane
         lens_f = steps.lengths.to(torch.float64)
-        step_w = (rank_w[lane].double() / (lens_f[lane] * n_traj)).to(torch.float32)   # rank_w / (T_i * n)
-        stats: dict = {}
+        step_w = (rank_w[lane].double() / lens_f[lane]).to(torch.float32)   # rank_w / T_i (1 / n: after the reduce)
 
         actor_g = [torch.zeros_like(p) for p in self.params["W"] + self.params["b"]]
         critic_g = None
@@ -863,11 +873,9 @@ class ReinforceAgent:
                         v, kept = mlp_forward_kept(self.critic_params, x, self.mlp_config.activation)
                         v = v.view(-1)
                         hn = steps.has_next[sel]
-                        vn = torch.zeros_like(v)
-                        if bool(hn.any()):
-                            xn, _ = steps.features(sel[hn], k, nxt=True)
-                            vn[hn] = forward_logits(self.critic_params, xn, self.mlp_config.activation,
-                                                    keep_cache=False)[0].view(-1)
+                        xn, _ = steps.features(sel, k, nxt=True)   # the step itself where there is no successor
+                        vn = forward_logits(self.critic_params, xn, self.mlp_config.activation,
+                                            keep_cache=False)[0].view(-1)
                         r = steps.rewards[sel]
                         tgt = r + (float(c.gamma) * vn) * hn.to(torch.float32)
                         deltas[k, sel] = tgt - v
@@ -890,8 +898,6 @@ class ReinforceAgent:
             G = self._returns_tm(steps.rewards_tm, steps.lengths).reshape(-1)[steps.vidx]
             adv1 = self._advantages(G, lane, n_local, rank_w[lane])
             adv = adv1.unsqueeze(0).expand(K, -1)
-        stats["adv_mean"] = float(adv.mean()) if adv.numel() else 0.0
-        stats["adv_std"] = float(adv.std(unbiased=False)) if adv.numel() else 0.0
 
         nW = len(self.params["W"])
         gspec = self._fused_grad_spec() if steps.boards is not None else None
@@ -909,34 +915,50 @@ class ReinforceAgent:
                     g = (onehot - p) * (adv[k, sel] * step_w[sel]).unsqueeze(1)
                     mlp_backward_(self.params, kept, self.mlp_config.activation, g, actor_g[:nW], actor_g[nW:])
 
-        # one fused all-reduce of actor (+ critic) gradients across ranks, before clipping
-        dp.fused_all_reduce_(actor_g + (critic_g or []))
-        self.last_grads = {"actor": [g.clone() for g in actor_g],
-                           "critic": [g.clone() for g in critic_g] if critic_g else None}
-        gW, gb = actor_g[:nW], actor_g[nW:]
-        stats["actor_grad_norm"] = self.clip_grads_global_norm(gW, gb)
-        if c.use_critic:
-            ncW = len(self.critic_params["W"])
-            gWc, gbc = critic_g[:ncW], critic_g[ncW:]
-            stats["critic_grad_norm"] = self.clip_grads_global_norm(gWc, gbc)
-        if c.optimizer == "sgd":
-            for l in range(nW):
-                self.params["W"][l] = self.params["W"][l] + c.learning_rate * gW[l]
-                self.params["b"][l] = self.params["b"][l] + c.learning_rate * gb[l]
+            # ONE collective: actor + critic gradients and the episode count; then the 1 / n_traj weight
+            dp.reduce_gradients_(actor_g + (critic_g or []), n_local * K)
+            self.last_grads = {"actor": [g.clone() for g in actor_g],
+                               "critic": [g.clone() for g in critic_g] if critic_g else None}
+            gW, gb = actor_g[:nW], actor_g[nW:]
+            norms = [self._clip_(actor_g)]
             if c.use_critic:
-                for l in range(ncW):
-                    self.critic_params["W"][l] = self.critic_params["W"][l] - c.critic_learning_rate * gWc[l]
-                    self.critic_params["b"][l] = self.critic_params["b"][l] - c.critic_learning_rate * gbc[l]
-        elif c.optimizer == "adam":
-            self._adam_update(gW, gb)
-            if c.use_critic:
-                self._adam_update(gWc, gbc, prefix="critic")
-        else:
-            raise ValueError(f"Unknown optimizer: {c.optimizer}")
+                ncW = len(self.critic_params["W"])
+                gWc, gbc = critic_g[:ncW], critic_g[ncW:]
+                norms.append(self._clip_(critic_g))
+            if c.optimizer == "sgd":
+                for l in range(nW):
+                    self.params["W"][l] = self.params["W"][l] + c.learning_rate * gW[l]
+                    self.params["b"][l] = self.params["b"][l] + c.learning_rate * gb[l]
+                if c.use_critic:
+                    for l in range(ncW):
+                        self.critic_params["W"][l] = self.critic_params["W"][l] - c.critic_learning_rate * gWc[l]
+                        self.critic_params["b"][l] = self.critic_params["b"][l] - c.critic_learning_rate * gbc[l]
+            elif c.optimizer == "adam":
+                self._adam_update(gW, gb)
+                if c.use_critic:
+                    self._adam_update(gWc, gbc, prefix="critic")
+            else:
+                raise ValueError(f"Unknown optimizer: {c.optimizer}")
         self._params_version += 1
+        vals = torch.stack(norms).tolist()          # the update's only host synchronisation
+        stats = {"actor_grad_norm": vals[0]}
+        if c.use_critic:
+            stats["critic_grad_norm"] = vals[1]
         if self._logger.isEnabledFor(logging.INFO):
-            self._logger.info(f"Global Grad Norms: Actor: {stats['actor_grad_norm']:.4f}")
-            if c.use_critic:
-                self._logger.info(f"Global Grad Norms: Critic: {stats['critic_grad_norm']:.4f}")
+            self._log_update(stats, adv.reshape(-1))   # the augmented list when augmentation is on (:596)
         self.last_stats = stats
         return stats
+
+    def _log_update(self, stats: dict, adv: torch.Tensor) -> None:
+        """The INFO log lines of src/reinforce_agent.py:585-620 (gradient norms, advantage statistics)."""
+        self._logger.info(f"Global Grad Norms: Actor: {stats['actor_grad_norm']:.4f}")
+        if "critic_grad_norm" in stats:
+            self._logger.info(f"Global Grad Norms: Critic: {stats['critic_grad_norm']:.4f}")
+        if adv.numel() == 0:
+            return
+        a = adv.float()
+        k = min(5, a.numel())
+        top = a[torch.topk(a.abs(), k).indices].tolist()
+        self._logger.info("Advantages stats: mean=%.6f, std=%.6f, min=%.6f, max=%.6f, pos=%d, neg=%d, total=%d, "
+                          "top|A|=%s", float(a.mean()), float(a.std(unbiased=False)), float(a.min()), float(a.max()),
+                          int((a > 0).sum()), int((a < 0).sum()), a.numel(), ", ".join(f"{v:.4f}" for v in top))

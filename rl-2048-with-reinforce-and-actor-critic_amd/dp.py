@@ -1,13 +1,15 @@
 """Data-parallel collectives of the update (one process per GPU, torch.distributed; "nccl" = RCCL on ROCm).
 
 The env step needs no communication (boards are independent; each rank owns a contiguous global lane range).
-Per update_batch the only exchanges are tiny except one:
-  * episode totals  -> all-gather (global reward ranks, src/reinforce_agent.py:681-716)
-  * baseline sums   -> all-reduce of 2 + 1 fp64 scalars ('batch' / 'batch_norm', :864-881)
-  * gradients       -> ONE fused fp32 all-reduce of actor + critic gradients, before clipping (:558-561)
-The fused buffer is 0.3-1.1 MB for the reference configs: latency-bound on xGMI, so a single bucket is the
-right size (no bucketing / overlap needed at this size).  These helpers are device-agnostic (gloo on CPU in
-the tests, RCCL on the GPUs).
+Per update_batch there is ONE gradient all-reduce, plus two tiny exchanges only where the configuration needs
+global statistics before the gradient pass:
+  * gradients       -> ONE fused fp32 all-reduce of actor + critic gradients and the episode count, before
+                       clipping (src/reinforce_agent.py:558-561); the 1 / n_traj weight is applied after it
+  * baseline sums   -> 'batch' / 'batch_norm' only: one all-reduce of 3 fp64 scalars (:864-881)
+  * episode totals  -> reward_rank_weights only: an all-gather (global reward ranks, :681-716)
+None of them synchronises the host.  The fused buffer is 0.3-1.1 MB for the reference configs: latency-bound on
+xGMI, so a single bucket is the right size (no bucketing / overlap needed at this size).  These helpers are
+device-agnostic (gloo on CPU in the tests, RCCL on the GPUs).
 """
 from __future__ import annotations
 
@@ -82,21 +84,41 @@ def rank_weights(totals: torch.Tensor, conf, group=None) -> torch.Tensor:
     return w[offset: offset + n_local].contiguous()
 
 
-def weighted_stats(values: torch.Tensor, weights: torch.Tensor, group=None) -> tuple[float, float]:
-    """_compute_weighted_stats (src/reinforce_agent.py:864-881) across ranks: two-pass, fp64 accumulation."""
+def batch_mean_std(values: torch.Tensor, weights: torch.Tensor, group=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """_compute_weighted_stats (src/reinforce_agent.py:864-881) over the global batch: the fp64 sums
+    [sum w, sum w v, sum w v^2] of every rank in ONE all-reduce, then mean and the (single-pass, fp64) weighted
+    standard deviation as device scalars -- no host synchronisation.  sum w < 1e-8 gives (0, 1) like the
+    reference.  (In fp64 the single-pass variance loses ~1e-16 (mu / sigma)^2 relative: far below the fp32 the
+    reference computes these statistics in.)"""
     w = weights.double()
     v = values.double()
-    sums = torch.stack([w.sum(), (w * v).sum()])
+    sums = torch.stack([w.sum(), (w * v).sum(), (w * v * v).sum()])
     all_reduce_sum_(sums, group)
-    if float(sums[0]) < 1e-8:
-        return 0.0, 1.0
-    mean = sums[1] / sums[0]
-    var_num = (w * (v - mean) ** 2).sum().reshape(1)
-    all_reduce_sum_(var_num, group)
-    return float(mean), float(torch.sqrt(var_num[0] / sums[0]))
+    ok = sums[0] >= 1e-8
+    sw = torch.where(ok, sums[0], torch.ones_like(sums[0]))
+    mean = sums[1] / sw
+    var = torch.clamp(sums[2] / sw - mean * mean, min=0.0)
+    return torch.where(ok, mean, torch.zeros_like(mean)), torch.where(ok, torch.sqrt(var), torch.ones_like(var))
 
 
-def global_count(n_local: int, device, group=None) -> int:
-    t = torch.tensor([n_local], dtype=torch.int64, device=device)
-    all_reduce_sum_(t, group)
-    return int(t.item())
+def reduce_gradients_(tensors: list[torch.Tensor], n_local: int, group=None) -> None:
+    """Finish the gradients of update_batch across ranks with ONE collective: every rank accumulated its
+    episodes' sum of rank_w / T_i-weighted per-step gradients; the flat fp32 buffer of all of them (actor +
+    critic) plus this rank's episode count is all-reduced, and each gradient is divided by the global count --
+    the 1 / n_traj of src/reinforce_agent.py:467, :533 -- on the device (no host synchronisation).  The count
+    travels as an fp32 element: exact up to 2^24 episodes per update.  Single process: just the division."""
+    if not tensors:
+        return
+    if not active(group):
+        inv = 1.0 / max(int(n_local), 1)
+        for t in tensors:
+            t.mul_(inv)
+        return
+    flat = torch.cat([t.reshape(-1) for t in tensors] +
+                     [torch.full((1,), float(n_local), dtype=tensors[0].dtype, device=tensors[0].device)])
+    dist.all_reduce(flat, group=group)
+    flat[:-1].div_(flat[-1].clamp(min=1.0))
+    off = 0
+    for t in tensors:
+        t.copy_(flat[off: off + t.numel()].view_as(t))
+        off += t.numel()

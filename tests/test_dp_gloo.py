@@ -40,11 +40,14 @@ def _worker(rank, world, port, q):
         vals = torch.tensor(rng.standard_normal(40), dtype=torch.float32)
         wts = torch.tensor(rng.random(40), dtype=torch.float32)
         vshard, wshard = vals[rank * 20:(rank + 1) * 20], wts[rank * 20:(rank + 1) * 20]
-        mean, std = dp.weighted_stats(vshard, wshard)
+        mean, std = dp.batch_mean_std(vshard, wshard)
         g = [torch.full((3, 2), float(rank + 1)), torch.arange(4, dtype=torch.float32) * (rank + 1)]
         dp.fused_all_reduce_(g)
-        n = dp.global_count(sizes[rank], "cpu")
-        q.put((rank, w_local.numpy(), allg.numpy(), o, mean, std, [t.numpy() for t in g], n))
+        # reduce_gradients_: sum over ranks / global episode count (6 + 7), one collective
+        h = [torch.full((2, 2), float(rank + 1) * 13.0), torch.ones(3) * (rank + 1) * 26.0]
+        dp.reduce_gradients_(h, sizes[rank])
+        q.put((rank, w_local.numpy(), allg.numpy(), o, float(mean), float(std), [t.numpy() for t in g],
+               [t.numpy() for t in h]))
     finally:
         dist.destroy_process_group()
 
@@ -74,12 +77,17 @@ def test_dp_collectives_equal_single_process():
     np.testing.assert_array_equal(np.concatenate([res[0][1], res[1][1]]), w_single)
     np.testing.assert_array_equal(res[0][2], totals)
     assert res[0][3] == 0 and res[1][3] == 6
-    m1, s1 = dp.weighted_stats(torch.tensor(vals), torch.tensor(wts))
+    m1, s1 = (float(x) for x in dp.batch_mean_std(torch.tensor(vals), torch.tensor(wts)))
+    from oracle import agent_oracle as AO
+
+    m_ref, s_ref = AO.OracleAgent.weighted_stats(vals, wts)        # src/reinforce_agent.py:864-881 (two-pass)
+    assert abs(m1 - float(m_ref)) < 1e-6 and abs(s1 - float(s_ref)) < 1e-6
     for r in (0, 1):
         assert abs(res[r][4] - m1) < 1e-12 and abs(res[r][5] - s1) < 1e-12
         np.testing.assert_array_equal(res[r][6][0], np.full((3, 2), 3.0))
         np.testing.assert_array_equal(res[r][6][1], np.arange(4) * 3.0)
-        assert res[r][7] == 13
+        np.testing.assert_allclose(res[r][7][0], np.full((2, 2), 3.0), rtol=1e-7)     # (13 + 26) / 13
+        np.testing.assert_allclose(res[r][7][1], np.full(3, 6.0), rtol=1e-7)          # (26 + 52) / 13
 
 
 def test_rank_weights_match_reference_formula():
@@ -97,13 +105,16 @@ def test_rank_weights_match_reference_formula():
             np.testing.assert_allclose(got, ref, rtol=1e-6)
 
 
-@pytest.mark.parametrize("n", [0, 5])
-def test_weighted_stats_single(n):
+@pytest.mark.parametrize("n", [0, 5, 1000])
+def test_batch_mean_std_single(n):
+    """dp.batch_mean_std (fp64 single-pass) against the reference's two-pass weighted statistics, including the
+    empty batch's (0, 1); values with a large mean relative to their spread (the returns' typical shape)."""
     from rl2048_amd import dp
     from oracle import agent_oracle as AO
 
-    v = np.arange(n, dtype=np.float32)
-    w = np.ones(n, dtype=np.float32)
-    got = dp.weighted_stats(torch.tensor(v), torch.tensor(w))
-    ref = AO.OracleAgent.weighted_stats(v, w)
-    assert abs(got[0] - float(ref[0])) < 1e-6 and abs(got[1] - float(ref[1])) < 1e-6
+    rng = np.random.default_rng(n)
+    v = (rng.standard_normal(n) * 3 + 250).astype(np.float32)
+    w = rng.choice([0.5, 1.0, 3.0], size=n).astype(np.float32)
+    got = [float(x) for x in dp.batch_mean_std(torch.tensor(v), torch.tensor(w))]
+    ref = AO.OracleAgent.weighted_stats(v.astype(np.float64), w.astype(np.float64))
+    assert abs(got[0] - float(ref[0])) < 1e-9 * max(1.0, abs(float(ref[0]))) and abs(got[1] - float(ref[1])) < 1e-9
