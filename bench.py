@@ -48,11 +48,11 @@ UPDATE_FLOP_PER_SAMPLE = POLICY_FLOP_PER_BOARD + 2 * (256 * 256 * 2 + 256 * 4 * 
 SURVEY_RNG_BYTES = {"pcg64": 88, "philox": 30}
 SURVEY_OBS_BYTES = {"none": 0, "raw": 64, "log2": 64, "onehot": 1092}
 # LAYOUT bytes: what this build's structure-of-arrays lane layout actually moves per board-step (reads / writes):
-#   board 8/8, action 1/-, status 1/-, step_count 4/4, max_tile 1/1, score 4/4, reward -/4, flags -/1, mask -/4
-#   PCG64: rng_state 16/16, rng_inc 16/-, rng_buf 8/8          Philox: lane seed 8/-
+#   board 8/8, action 1/-, lane state word (step count, max tile, active, PCG64 buffer flag) 4/4, reward -/4,
+#   flags -/1, mask -/4;  PCG64: rng_state 16/16, rng_inc 16/-, rng_uint 4/4;  Philox: lane seed 8/-
 #   obs: log2/raw -/64, onehot -/1088
-CORE_R, CORE_W = 8 + 1 + 1 + 4 + 1 + 4, 8 + 4 + 1 + 4 + 4 + 1 + 4
-RNG_BYTES = {"pcg64": (40, 24), "philox": (8, 0)}
+CORE_R, CORE_W = 8 + 1 + 4, 8 + 4 + 4 + 1 + 4
+RNG_BYTES = {"pcg64": (36, 20), "philox": (8, 0)}
 OBS_BYTES = {"none": 0, "raw": 64, "log2": 64, "onehot": 1088}
 
 
@@ -114,16 +114,13 @@ def make_env(torch, args, B, lane_offset, device):
     cfg = Game2048EnvConfig(obs_mode="log2" if args.obs == "none" else args.obs, obs_log2_scale=0.0625,
                             reward_mode="log2", base_reward_scale=0.5, max_steps=1024)
     env = VecGame2048Env(B, cfg, device=device, rng=args.rng, auto_reset=not args.no_auto_reset,
-                         reset_stride=B * max(args.gpus, 1), lane_offset=lane_offset)
+                         reset_stride=B * max(args.gpus, 1), lane_offset=lane_offset, track_score=False)
     if args.obs == "none":
         env._out.obs = None
-    env.seed.copy_(torch.arange(B, dtype=torch.int64, device=device) + (1_000_003 + lane_offset))
-    if env.rng_mode == L.RNG_PCG64:
-        L.check(L.lib().g2048_seed_pcg64(L.ptr(env.seed), L.ptr(env.rng_state), L.ptr(env.rng_inc),
-                                         L.ptr(env.rng_buf), B, L.stream_handle(device)))
+    # per-lane episode seeds (PCG64: default_rng(seed) streams) via g2048_reset, then the random-state boards
+    env.reset(seed=torch.arange(B, dtype=torch.int64, device=device) + (1_000_003 + lane_offset))
     env.board.copy_(synthetic_boards(torch, B, lane_offset, device))
-    env.status.fill_(L.S_ACTIVE)
-    env.max_tile.fill_(2)
+    env.set_lane_state(step_count=0, max_tile_exp=2, active=True)
     return env
 
 
@@ -232,7 +229,7 @@ def policy_rollout_rate(torch, B: int, device, steps: int = 20, warmup: int = 5,
     cfg = Game2048EnvConfig(obs_mode="log2", obs_log2_scale=0.0625, reward_mode="log2", base_reward_scale=0.5)
     agent = ReinforceAgent(cfg, MLPConfig(hidden_sizes=[256, 256], activation="ReLU", init_distribution="HeNormal"),
                            ReinforceAgentConfig(), device=device)
-    env = VecGame2048Env(B, cfg, device=device, auto_reset=True)
+    env = VecGame2048Env(B, cfg, device=device, auto_reset=True, track_score=False)
     env.reset(seed=7)
     lib = L.lib()
     st = torch.empty(2 * B, dtype=torch.int64, device=device)
@@ -247,14 +244,14 @@ def policy_rollout_rate(torch, B: int, device, steps: int = 20, warmup: int = 5,
 
     def one():
         if fused:
-            L.check(lib.g2048_policy(L.ptr(packed), spec[0], spec[1], spec[2], L.ptr(env.board), L.ptr(env.status),
+            L.check(lib.g2048_policy(L.ptr(packed), spec[0], spec[1], spec[2], L.ptr(env.board), L.ptr(env.state),
                                      None, L.OBS_LOG2, 0.0625, 1, 0, L.RNG_PCG64, L.ptr(st), L.ptr(inc), L.ptr(buf), 0,
-                                     None, None, None, None, L.ptr(acts), B, stream))
+                                     None, None, None, L.ptr(acts), B, stream))
             env.step_into(acts, write_obs=False)
         else:
             logits = agent._policy_logits(env.obs)
             L.check(lib.g2048_sample(L.ptr(logits), L.ptr(env.mask), None, 0, 0, L.ptr(st), L.ptr(inc), L.ptr(buf),
-                                     0, None, None, None, L.ptr(acts), B, stream))
+                                     0, None, None, L.ptr(acts), B, stream))
             env.step_into(acts)
 
     with torch.no_grad():
@@ -423,7 +420,7 @@ def main():
             e_.record()
             torch.cuda.synchronize()
             rf = float(((env.flags & L.F_RESET) != 0).float().mean())
-            act = float(((env.status & L.S_ACTIVE) != 0).float().mean())
+            act = float(env.active.float().mean())
             print(json.dumps({"step": k, "us": round(s_.elapsed_time(e_) * 1e3, 2), "reset_frac": round(rf, 5),
                               "active_frac": round(act, 4)}), flush=True)
         return

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 5
+#define G2048_ABI_VERSION 7
 
 /* status codes */
 #define G2048_OK 0
@@ -58,8 +58,18 @@ extern "C" {
 #define G2048_F_INACTIVE 0x40    /* lane was already finished (no auto-reset): nothing happened */
 #define G2048_F_BADACTION 0x80   /* action outside 0..3: lane untouched (reference raises) */
 
-/* lane status bits (g2048_lanes.status) */
-#define G2048_S_ACTIVE 0x01
+/* Per-lane state word (g2048_lanes.state, one uint32 per lane; read and written once per step):
+ *   bits  0..19  Game2048Env._step_count (== Game2048.step_count); saturates at 2^20 - 1, so cfg->max_steps must
+ *                be < 2^20 (checked; max_steps None only stops counting step_index past 1,048,575 steps)
+ *   bits 20..24  log2(Game2048Env.max_tile_seen)
+ *   bit  25      the lane is in an episode (G2048_LS_ACTIVE)
+ *   bit  26      numpy PCG64's next_uint32 buffer is full (has_uint32; the value is g2048_lanes.rng_uint) */
+#define G2048_LS_STEP_MASK 0x000FFFFFu
+#define G2048_LS_MAXT_SHIFT 20
+#define G2048_LS_MAXT_MASK 0x01F00000u
+#define G2048_LS_ACTIVE 0x02000000u
+#define G2048_LS_HAS_U32 0x04000000u
+#define G2048_MAX_STEPS_LIMIT 0x000FFFFF
 
 /* Game2048EnvConfig (src/env.py:19-40).  size is fixed at 4. */
 typedef struct g2048_env_cfg {
@@ -76,20 +86,19 @@ typedef struct g2048_env_cfg {
     double step_reward;
     double endgame_penalty;
     double invalid_action_penalty;
-    int64_t max_steps;             /* < 0 means None */
+    int64_t max_steps;             /* < 0 means None; otherwise <= G2048_MAX_STEPS_LIMIT */
 } g2048_env_cfg;
 
-/* Per-lane environment state, structure-of-arrays, each array of length n (rng_* of length 2n). */
+/* Per-lane environment state, structure-of-arrays, each array of length n (rng_state / rng_inc of length 2n).
+ * 49 B read + 33 B written per lane per step in PCG64 mode (board, state word, RNG), 20 / 12 B with Philox. */
 typedef struct g2048_lanes {
     uint64_t* board;       /* Game2048.board as a bitboard */
-    uint32_t* step_count;  /* Game2048Env._step_count (== Game2048.step_count) */
-    uint32_t* score;       /* Game2048.score */
-    uint8_t* max_tile;     /* log2(Game2048Env.max_tile_seen) */
-    uint8_t* status;       /* G2048_S_* */
-    uint64_t* seed;        /* seed of the lane's current episode (Game2048.reset(seed)) */
+    uint32_t* state;       /* the lane state word (G2048_LS_*) */
+    uint64_t* seed;        /* seed of the lane's current episode (Game2048.reset(seed)); read every step only in
+                              Philox mode (PCG64 mode reads it when an episode ends and auto-resets) */
     uint64_t* rng_state;   /* PCG64 128-bit state, (lo, hi) per lane            [PCG64 mode only] */
     uint64_t* rng_inc;     /* PCG64 128-bit increment, (lo, hi) per lane        [PCG64 mode only] */
-    uint64_t* rng_buf;     /* PCG64 next_uint32 buffer: has_uint32 << 32 | uinteger [PCG64 mode only] */
+    uint32_t* rng_uint;    /* PCG64 next_uint32 buffer value (its flag: G2048_LS_HAS_U32) [PCG64 mode only] */
 } g2048_lanes;
 
 /* Outputs of one step.  reward and flags are required; the others may be NULL. */
@@ -102,6 +111,8 @@ typedef struct g2048_step_out {
                               (log2(v) - 1), first merge in the lowest nibble, 0-terminated (<= 8) */
     uint64_t* prev_board;  /* [n] the board before the step (trajectory record) */
     double* reward64;      /* [n] the same reward in fp64 -- the Python float src/env.py:261 returns (may be NULL) */
+    uint32_t* score_add;   /* [n] sum of this step's merged tiles: Game2048.score's increment (src/game2048.py:54);
+                              the caller keeps the running score when it needs one (may be NULL) */
 } g2048_step_out;
 
 /* ---------------------------------------------------------------------------------------------------- */
@@ -150,11 +161,12 @@ int g2048_move(const uint64_t* boards, const uint8_t* actions, uint64_t* out_boa
  * (src/reinforce_agent.py:178-190).  logits [n*4] fp32, mask [n*4] int8 (NULL = no mask).
  * greedy != 0: argmax(probs * mask).  Otherwise rng_mode PCG64: Generator.choice(4, p=probs) on the lane's
  * stream (rng_* as in g2048_seed_pcg64); PHILOX: inverse-CDF on a Philox draw keyed (philox_key, lane_seed[i],
- * counter[i]).  active: [n] (NULL = all); inactive lanes are left untouched.  probs_out [n*4] may be NULL. */
-int g2048_sample(const float* logits, const int8_t* mask, const uint8_t* active, int greedy, int rng_mode,
+ * the lane's step count).  lane_state: the env lanes' state words [n] (g2048_lanes.state: the active bit and, for
+ * Philox, the step count; NULL = all active, count 0); inactive lanes are left untouched.  probs_out [n*4] may
+ * be NULL. */
+int g2048_sample(const float* logits, const int8_t* mask, const uint32_t* lane_state, int greedy, int rng_mode,
                  uint64_t* rng_state, uint64_t* rng_inc, uint64_t* rng_buf, uint64_t philox_key,
-                 const uint64_t* lane_seed, const uint32_t* counter, float* probs_out, uint8_t* actions,
-                 int64_t n, void* stream);
+                 const uint64_t* lane_seed, float* probs_out, uint8_t* actions, int64_t n, void* stream);
 
 /* Discounted returns per episode (ReinforceAgent.compute_returns src/reinforce_agent.py:255-273):
  * rewards / returns are time-major [T, n] fp32 (lane i's episode occupies rows 0..lengths[i]-1); the scan is
@@ -185,17 +197,18 @@ int64_t g2048_policy_packed_size(int h1, int h2);
 int g2048_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                       const float* b3, int in_dim, int h1, int h2, float* packed, int64_t packed_len, void* stream);
 
-/* boards / active / rng / counters / outputs are per lane; the call covers n entries: entry j is lane
+/* boards / lane_state / rng / outputs are per lane; the call covers n entries: entry j is lane
  * lane_index[j] (int32, NULL = lane j), so a rollout can run the net on its still-active lanes only;
- * active: status bytes (bit 0 = active; NULL = all) -- inactive lanes are left untouched;
+ * lane_state: the env lanes' state words (G2048_LS_ACTIVE; NULL = all active) -- inactive lanes are left
+ * untouched;
  * use_mask: mask the logits with the boards' action masks (Game2048.get_action_mask, src/game2048.py:95-99);
- * greedy / rng_mode / rng_* / philox_key / lane_seed / counter / probs_out / actions as in g2048_sample;
+ * greedy / rng_mode / rng_* / philox_key / lane_seed / probs_out / actions as in g2048_sample;
  * logits_out [n*4] may be NULL. */
-int g2048_policy(const float* packed, int h1, int h2, int activation, const uint64_t* boards, const uint8_t* active,
-                 const int32_t* lane_index, int obs_mode, float obs_scale, int use_mask, int greedy, int rng_mode, uint64_t* rng_state,
-                 const uint64_t* rng_inc, const uint64_t* rng_buf, uint64_t philox_key, const uint64_t* lane_seed,
-                 const uint32_t* counter, float* probs_out, float* logits_out, uint8_t* actions, int64_t n,
-                 void* stream);
+int g2048_policy(const float* packed, int h1, int h2, int activation, const uint64_t* boards,
+                 const uint32_t* lane_state, const int32_t* lane_index, int obs_mode, float obs_scale, int use_mask,
+                 int greedy, int rng_mode, uint64_t* rng_state, const uint64_t* rng_inc, const uint64_t* rng_buf,
+                 uint64_t philox_key, const uint64_t* lane_seed, float* probs_out, float* logits_out,
+                 uint8_t* actions, int64_t n, void* stream);
 
 /* ---- fused actor gradient (update_batch's actor branch) ---------------------------------------------------
  * For the same nets as g2048_policy: ReinforceAgent.update_batch's actor gradient (src/reinforce_agent.py:502-555:
@@ -222,19 +235,26 @@ int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int 
  * kernel: the critic packed like the actor with its value head [h2 x 1] / [1] as output 0 of a 4-wide layer (outputs
  * 1..3 zero); per sample the value V(s), the TD error delta_out = target - V (target = r + gamma V(s') m from the
  * host), and dL/dV = (V - target) (loss 0, MSE) or its Huber clip at huber_delta (loss 1), times weight[i];
- * the outputs as for g2048_actor_grad (only column / entry 0 of dW3 / db3 is the value head's). */
+ * the outputs as for g2048_actor_grad (only column / entry 0 of dW3 / db3 is the value head's), plus V(s) per
+ * sample in value_out (NULL ok).  Column window: sample i's a1^T / d2^T column is col_off + i, and the columns
+ * col_off .. col_off + ncols - 1 are written (those past n as zero-coefficient padding; col_off, ncols multiples
+ * of 32, n <= ncols, col_off + ncols <= ld) -- so consecutive launches (one per time row of a batch, whose V(s)
+ * is the previous row's V(s')) can fill one column buffer before one layer-2 GEMM.  accumulate != 0 adds this
+ * launch's per-wave partials into `partials` instead of overwriting them. */
 int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
                       float obs_scale, int loss, float huber_delta, const uint64_t* boards, const float* target,
-                      const float* weight, float* delta_out, int64_t n, int64_t ld, float* a1t, float* d2t,
-                      float* partials, int64_t waves, void* stream);
+                      const float* weight, float* delta_out, float* value_out, int64_t n, int64_t ld, int64_t col_off,
+                      int64_t ncols, float* a1t, float* d2t, float* partials, int accumulate, int64_t waves,
+                      void* stream);
 
 /* The whole batched rollout in one launch: ReinforceAgent.run_episode (src/reinforce_agent.py:195-252) for n
  * (env_seed, policy_seed) pairs -- select_action (the fused policy above) + Game2048Env.step until terminated or
  * truncated, per episode.  env_* / pol_*: the PCG64 streams of default_rng(env_seed) / default_rng(policy_seed)
  * per episode (g2048_seed_pcg64); queue: one uint32, zero before the call (episode work queue).
- * Trajectory rows are time-major [cap, n]: boards (pre-step), actions, rewards (fp32), flags (G2048_F_*),
- * probs [cap, n, 4] (NULL ok); rows at or past an episode's length are not written.  Per episode: lengths,
- * totals (fp64 sum of the fp32 rewards), max_tile (log2 of max_tile_seen), final_board.
+ * Trajectory rows are time-major [cap, n]: boards (pre-step), actions, rewards (fp64, the Python floats
+ * run_episode records), flags (G2048_F_*), probs [cap, n, 4] (NULL ok); rows at or past an episode's length are
+ * not written.  Per episode: lengths, totals (fp64 running sum in step order, src/reinforce_agent.py:233),
+ * max_tile (log2 of max_tile_seen), final_board.
  * Requires obs_mode log2 / raw, cfg->max_steps >= 0 and cap >= max(max_steps, 1) (episodes end by then). */
 int g2048_rollout(const float* packed, int h1, int h2, int activation, const g2048_env_cfg* cfg, int greedy,
                   const uint64_t* env_state, const uint64_t* env_inc, const uint64_t* env_buf, const uint64_t* pol_state,

@@ -20,7 +20,7 @@ LIB_PATH = SHIPPED_LIB
 SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
 SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 5
+ABI_VERSION = 7
 
 # include/g2048.h constants
 OBS_NONE, OBS_RAW, OBS_LOG2, OBS_ONEHOT = -1, 0, 1, 2
@@ -28,7 +28,9 @@ ACT_RELU, ACT_SIGMOID = 0, 1
 RNG_PCG64, RNG_PHILOX = 0, 1
 F_CHANGED, F_TERMINATED, F_TRUNCATED, F_INVALID = 0x01, 0x02, 0x04, 0x08
 F_OVERFLOW, F_RESET, F_INACTIVE, F_BADACTION = 0x10, 0x20, 0x40, 0x80
-S_ACTIVE = 0x01
+# lane state word (g2048_lanes.state)
+LS_STEP_MASK, LS_MAXT_SHIFT, LS_ACTIVE, LS_HAS_U32 = 0x000FFFFF, 20, 0x02000000, 0x04000000
+MAX_STEPS_LIMIT = 0x000FFFFF
 G2048_OK, G2048_EINVAL, G2048_EHIP, G2048_ENOINIT = 0, 1, 2, 3
 
 
@@ -56,12 +58,12 @@ class EnvCfg(ctypes.Structure):
 
 class Lanes(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in
-                ("board", "step_count", "score", "max_tile", "status", "seed", "rng_state", "rng_inc", "rng_buf")]
+                ("board", "state", "seed", "rng_state", "rng_inc", "rng_uint")]
 
 
 class StepOut(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in ("reward", "flags", "mask", "obs", "merged", "prev_board",
-                                                         "reward64")]
+                                                         "reward64", "score_add")]
 
 
 _lib = None
@@ -80,14 +82,14 @@ def _declare(L):
     L.g2048_step.argtypes = [P(Lanes), vp, P(EnvCfg), P(StepOut), i32, u64, i32, u64, i64, vp]
     L.g2048_obs.argtypes = [vp, i32, f, vp, vp, i64, vp]
     L.g2048_move.argtypes = [vp, vp, vp, vp, vp, i64, vp]
-    L.g2048_sample.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp, u64, vp, vp, vp, vp, i64, vp]
+    L.g2048_sample.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp, u64, vp, vp, vp, i64, vp]
     L.g2048_returns.argtypes = [vp, vp, d, vp, i64, i64, vp]
     L.g2048_symmetries.argtypes = [vp, vp, vp, vp, i64, vp]
     L.g2048_policy_packed_size.argtypes = [i32, i32]
     L.g2048_policy_packed_size.restype = i64
     L.g2048_policy_pack.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i64, vp]
     L.g2048_policy.argtypes = [vp, i32, i32, i32, vp, vp, vp, i32, f, i32, i32, i32, vp, vp, vp, u64, vp, vp, vp, vp,
-                               vp, i64, vp]
+                               i64, vp]
     L.g2048_rollout.argtypes = [vp, i32, i32, i32, P(EnvCfg), i32, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp,
                                 vp, vp, vp, vp, vp, vp]
     L.g2048_grad_packed_size.argtypes = [i32, i32]
@@ -97,7 +99,8 @@ def _declare(L):
     L.g2048_grad_pack.argtypes = [vp, i32, i32, vp, i64, vp]
     L.g2048_actor_grad_waves.argtypes = []
     L.g2048_actor_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, vp, vp, vp, i64, i64, vp, vp, vp, i64, vp]
-    L.g2048_critic_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, f, vp, vp, vp, vp, i64, i64, vp, vp, vp, i64, vp]
+    L.g2048_critic_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, f, vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, vp,
+                                    vp, i32, i64, vp]
     for name in ("g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step", "g2048_obs", "g2048_move",
                  "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy",
                  "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad"):

@@ -213,6 +213,8 @@ class ReinforceAgent:
         self.use_fused_rollout = True
         # update_batch's actor gradient through the fused g2048_actor_grad kernel when the net fits it (batched path)
         self.use_fused_grad = True
+        # ... and the fused critic per time row, V(s') taken from the next row's pass (large batches)
+        self.use_critic_rows = True
         self.grad_chunk_steps = 1 << 20
         self._pack_cache: dict[str, list] = {}
         self._params_version = 0
@@ -334,7 +336,7 @@ class ReinforceAgent:
         key = (n, rng)
         if key not in self._vec_cache:
             self._vec_cache.clear()
-            self._vec_cache[key] = VecGame2048Env(n, self.env_config, device=self.device, rng=rng)
+            self._vec_cache[key] = VecGame2048Env(n, self.env_config, device=self.device, rng=rng, track_score=False)
         return self._vec_cache[key]
 
     def _policy_logits(self, x: torch.Tensor) -> torch.Tensor:
@@ -435,16 +437,110 @@ class ReinforceAgent:
             lg = torch.empty(m, 4, dtype=torch.float32, device=self.device)
             dummy = torch.empty(m, dtype=torch.uint8, device=self.device)
             L.check(self._lib.g2048_policy(L.ptr(packed), h1, h2, act, L.ptr(bn), None, None, obs_code, scale, 0, 1,
-                                           L.RNG_PCG64, None, None, None, 0, None, None, None, L.ptr(lg), L.ptr(dummy),
+                                           L.RNG_PCG64, None, None, None, 0, None, None, L.ptr(lg), L.ptr(dummy),
                                            m, self._stream))
             tgt = (steps.rewards[sel] + (float(c.gamma) * lg[:, 0]) * hn.to(torch.float32)).contiguous()
             w = step_w[sel].contiguous()
             L.check(self._lib.g2048_critic_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, loss,
                                                 float(c.huber_delta), L.ptr(b), L.ptr(tgt), L.ptr(w),
-                                                L.ptr(deltas[k, s0:s0 + m]), m, ld, L.ptr(a1t), L.ptr(d2t), L.ptr(part),
-                                                waves, self._stream))
+                                                L.ptr(deltas[k, s0:s0 + m]), None, m, ld, 0, ld, L.ptr(a1t),
+                                                L.ptr(d2t), L.ptr(part), 0, waves, self._stream))
 
+        if self._critic_by_rows(steps):
+            self._critic_grad_rows(steps, step_w, K, gW, gb, deltas, spec)
+            return
         self._fused_grad(self.critic_params, "critic", spec, steps, K, gW, gb, 1, launch)
+
+    # the per-row critic pass pays ~7 small launches per time row; worth it from this many samples per row
+    critic_rows_min_avg = 16384
+
+    def _critic_by_rows(self, steps: "_Steps") -> bool:
+        if not self.use_critic_rows or steps.N == 0:
+            return False
+        T_used = int(steps.lengths.max())
+        return steps.N >= self.critic_rows_min_avg * max(T_used, 1) and steps.n + 32 <= (1 << 21) - 2048
+
+    def _critic_grad_rows(self, steps: "_Steps", step_w: torch.Tensor, K: int, gW: list[torch.Tensor],
+                          gb: list[torch.Tensor], deltas: torch.Tensor, spec) -> None:
+        """The critic branch without a separate V(s') forward: the valid steps are time-major, so the steps of one
+        time row are a contiguous range; rows run LAST first, one g2048_critic_grad launch each, and every launch
+        returns V(s) of its row (value_out) -- which is the V(s') the previous row's TD targets r + gamma V(s') m need
+        (src/reinforce_agent.py:423-443: X_next = the next step's obs).  The launches fill one a1^T / d2^T column
+        buffer (column window per row) and accumulate their per-wave partials; the layer-2 GEMM runs once per full
+        buffer.  Saves the ~141 kflop / sample V(s') forward of the chunked path."""
+        c = self.agent_config
+        loss = {"mse": 0, "huber": 1}[c.critic_loss_type]
+        h1, h2, act = spec
+        H1p, H2p = _padded_units(h1), _padded_units(h2)
+        params = self.critic_params
+        packed, gpacked = self._pack_net(params, spec, "critic"), self._pack_net(params, spec, "critic", grad=True)
+        waves = int(self._lib.g2048_actor_grad_waves())
+        pf = int(self._lib.g2048_grad_partial_size(h1, h2))
+        part = torch.zeros(waves, pf, dtype=torch.float32, device=self.device)
+        big = torch.zeros(H1p + 1, H2p, dtype=torch.float64, device=self.device)
+        obs_code, scale = _OBS_CODE[self.env_config.obs_mode], float(self.env_config.obs_log2_scale)
+        flat = steps.boards.reshape(-1)
+        n = steps.n
+        counts = torch.bincount(steps.t, minlength=steps.T).tolist()      # samples per time row (one host sync)
+        starts = [0] * len(counts)
+        for t in range(1, len(counts)):
+            starts[t] = starts[t - 1] + counts[t - 1]
+        blk = 2048                                                         # 64 split-K blocks x 32 columns
+        ld = -(-max(self.grad_chunk_steps, max(counts) + 32) // blk) * blk
+        a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
+        d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
+        vout = torch.empty(max(counts), dtype=torch.float32, device=self.device)
+        gamma = float(c.gamma)
+
+        def flush(used: int) -> None:
+            nonlocal big
+            if used == 0:
+                return
+            m = -(-used // blk) * blk
+            a1t[:, used:m].zero_()
+            d2t[:, used:m].zero_()
+            P = 1
+            while P < 64 and m // (2 * P) >= 8192:
+                P *= 2
+            q = m // P
+            big += torch.bmm(a1t[:, :m].view(H1p + 1, P, q).transpose(0, 1),
+                             d2t[:, :m].view(H2p, P, q).permute(1, 2, 0)).sum(0)
+
+        col = 0
+        for k in range(K):
+            vb = [torch.zeros(n, dtype=torch.float32, device=self.device) for _ in range(2)]
+            for t in range(len(counts) - 1, -1, -1):
+                cnt = counts[t]
+                if cnt == 0:
+                    continue
+                s0 = starts[t]
+                lanes = steps.lane[s0:s0 + cnt]
+                hn = steps.has_next[s0:s0 + cnt]
+                vn = vb[(t + 1) & 1].index_select(0, lanes)
+                tgt = (steps.rewards[s0:s0 + cnt] + (gamma * vn) * hn.to(torch.float32)).contiguous()
+                b = flat[steps.vidx[s0:s0 + cnt]].contiguous()
+                if k:
+                    b = self._symmetry_boards(b, k)
+                ncols = -(-cnt // 32) * 32
+                if col + ncols > ld:
+                    flush(col)
+                    col = 0
+                L.check(self._lib.g2048_critic_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, loss,
+                                                    float(c.huber_delta), L.ptr(b), L.ptr(tgt),
+                                                    L.ptr(step_w[s0:s0 + cnt]), L.ptr(deltas[k, s0:s0 + cnt]),
+                                                    L.ptr(vout), cnt, ld, col, ncols, L.ptr(a1t), L.ptr(d2t),
+                                                    L.ptr(part), 1, waves, self._stream))
+                vb[t & 1].index_copy_(0, lanes, vout[:cnt])
+                col += ncols
+        flush(col)
+        small = part.sum(0, dtype=torch.float64).to(torch.float32)
+        big = big.to(torch.float32)
+        gW[0] += small[:16 * H1p].view(16, H1p)[:, :h1]
+        gb[0] += small[16 * H1p:17 * H1p][:h1]
+        gW[1] += big[:h1, :h2]
+        gb[1] += big[H1p, :h2]
+        gW[2] += small[17 * H1p:17 * H1p + 4 * H2p].view(H2p, 4)[:h2, :1]
+        gb[2] += small[17 * H1p + 4 * H2p:][:1]
 
     def _fused_grad(self, params, slot: str, spec, steps: "_Steps", K: int, gW: list[torch.Tensor],
                     gb: list[torch.Tensor], out_dim: int, launch) -> None:
@@ -457,8 +553,7 @@ class ReinforceAgent:
         waves = int(self._lib.g2048_actor_grad_waves())
         pf = int(self._lib.g2048_grad_partial_size(h1, h2))
         part = torch.empty(waves, pf, dtype=torch.float32, device=self.device)
-        # cross-chunk / cross-block sums in fp64: at millions of samples the fp32 error of the gradient is set by
-        # how long each fp32 accumulation runs (tests/test_gpu_configs_at_size.py measures it against fp64)
+        # cross-chunk sums in fp64 (the per-chunk results are added into these as fp32 tensors)
         small = torch.zeros(pf, dtype=torch.float64, device=self.device)
         big = torch.zeros(H1p + 1, H2p, dtype=torch.float64, device=self.device)
         obs_code, scale = _OBS_CODE[self.env_config.obs_mode], float(self.env_config.obs_log2_scale)
@@ -470,17 +565,18 @@ class ReinforceAgent:
                 b = flat[steps.vidx[sel]].contiguous()
                 if k:
                     b = self._symmetry_boards(b, k)
-                # split-K of the layer-2 weight gradient over P column blocks of ~2048 samples (each an fp32 GEMM
-                # accumulation), the blocks summed in fp64
-                P = max(1, min(512, m // 2048))
+                # split-K of the layer-2 weight gradient over P column blocks (a strided-batched fp32 GEMM; at most
+                # 64 blocks of >= 8192 samples: measured faster than 512 blocks of 2048, and the gradient's fp32
+                # error at millions of samples is set by ReLU-derivative flips, not by this accumulation --
+                # tests/test_gpu_configs_at_size.py), blocks summed in fp32, chunks accumulated in fp64
+                P = max(1, min(64, m // 8192))
                 ld = -(-m // (32 * P)) * 32 * P
                 q = ld // P
                 a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
                 d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
                 launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale)
-                big += torch.bmm(a1t.view(H1p + 1, P, q).transpose(0, 1),
-                                 d2t.view(H2p, P, q).permute(1, 2, 0)).sum(0, dtype=torch.float64)
-                small += part.sum(0, dtype=torch.float64)
+                big += torch.bmm(a1t.view(H1p + 1, P, q).transpose(0, 1), d2t.view(H2p, P, q).permute(1, 2, 0)).sum(0)
+                small += part.sum(0)
         big, small = big.to(torch.float32), small.to(torch.float32)
         gW[0] += small[:16 * H1p].view(16, H1p)[:, :h1]
         gb[0] += small[16 * H1p:17 * H1p][:h1]
@@ -574,14 +670,14 @@ class ReinforceAgent:
                 # fused forward + choice straight from the boards, on the lanes still active at the last check
                 # (compacted every check_every steps); the step then skips the obs buffer
                 if active_idx is None or t % check_every == 0:
-                    active_idx = torch.nonzero(env.status & 1).view(-1).to(torch.int32)
+                    active_idx = torch.nonzero(env.active).view(-1).to(torch.int32)
                 m = int(active_idx.numel())
                 L.check(self._lib.g2048_policy(L.ptr(packed), spec[0], spec[1], spec[2], L.ptr(env.board),
-                                               L.ptr(env.status), L.ptr(active_idx) if m < n else None,
+                                               L.ptr(env.state), L.ptr(active_idx) if m < n else None,
                                                _OBS_CODE[self.env_config.obs_mode],
                                                float(self.env_config.obs_log2_scale), int(use_mask),
                                                int(use_greedy), rng_mode, L.ptr(pst), L.ptr(pinc), L.ptr(pbuf),
-                                               env.philox_key ^ 0x5A5A, L.ptr(pseeds), L.ptr(env.step_count),
+                                               env.philox_key ^ 0x5A5A, L.ptr(pseeds),
                                                L.ptr(probs[t]) if probs is not None else None, None,
                                                L.ptr(actions[t]), m if m < n else n, self._stream))
                 env.step_into(actions[t], reward=env.reward, flags=flags[t], prev_board=boards[t], write_obs=False,
@@ -589,15 +685,15 @@ class ReinforceAgent:
             else:
                 logits = self._policy_logits(env.obs)
                 L.check(self._lib.g2048_sample(L.ptr(logits), L.ptr(env.mask) if use_mask else None,
-                                               L.ptr(env.status), int(use_greedy), rng_mode, L.ptr(pst),
+                                               L.ptr(env.state), int(use_greedy), rng_mode, L.ptr(pst),
                                                L.ptr(pinc), L.ptr(pbuf), env.philox_key ^ 0x5A5A, L.ptr(pseeds),
-                                               L.ptr(env.step_count), L.ptr(probs[t]) if probs is not None else None,
+                                               L.ptr(probs[t]) if probs is not None else None,
                                                L.ptr(actions[t]), n, self._stream))
                 env.step_into(actions[t], reward=env.reward, flags=flags[t], prev_board=boards[t],
                               reward64=rewards[t])
             total += rewards[t]      # inactive lanes got reward 0.0
             t += 1
-            if t % check_every == 0 and not bool(env.status.any()):
+            if t % check_every == 0 and not bool(env.active.any()):
                 break
         fl = flags[:t]
         lengths = ((fl & L.F_INACTIVE) == 0).sum(0).to(torch.int32)

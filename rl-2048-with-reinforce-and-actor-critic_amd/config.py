@@ -67,4 +67,6 @@ def env_cfg_struct(cfg: Game2048EnvConfig) -> L.EnvCfg:
         setattr(c, k, float(getattr(cfg, k)))
     # None -> -1 (never truncate); any int n truncates once _step_count >= n (n <= 0: at the first step)
     c.max_steps = -1 if cfg.max_steps is None else max(int(cfg.max_steps), 0)
+    if c.max_steps > L.MAX_STEPS_LIMIT:
+        raise ValueError(f"max_steps must be <= {L.MAX_STEPS_LIMIT} on the device (20-bit lane step count) or None")
     return c

@@ -202,24 +202,30 @@ __device__ inline uint32_t mask_word(uint32_t m) {
 }
 
 // ------------------------------------------------------------------------------------- RNG state
+// The lane's numpy PCG64 stream: state and increment (16 + 16 B) and the next_uint32 buffer value (4 B); the
+// buffer's has_uint32 flag lives in the lane state word (G2048_LS_HAS_U32) and is set by the caller.
 __device__ inline Pcg64 load_pcg(const g2048_lanes& L, uint32_t i) {
     Pcg64 g;
     const ulonglong2 s = ld(reinterpret_cast<const ulonglong2*>(L.rng_state), i);
     const ulonglong2 c = ld(reinterpret_cast<const ulonglong2*>(L.rng_inc), i);
-    const uint64_t buf = ld(L.rng_buf, i);
     g.s_lo = s.x;
     g.s_hi = s.y;
     g.i_lo = c.x;
     g.i_hi = c.y;
-    g.has_uint32 = (uint32_t)(buf >> 32);
-    g.uinteger = (uint32_t)buf;
+    g.has_uint32 = 0u;
+    g.uinteger = ld(L.rng_uint, i);
     return g;
 }
 
 __device__ inline void store_pcg(const g2048_lanes& L, uint32_t i, const Pcg64& g, bool with_inc) {
     st(reinterpret_cast<ulonglong2*>(L.rng_state), i, make_ulonglong2(g.s_lo, g.s_hi));
     if (with_inc) st(reinterpret_cast<ulonglong2*>(L.rng_inc), i, make_ulonglong2(g.i_lo, g.i_hi));
-    st(L.rng_buf, i, ((uint64_t)g.has_uint32 << 32) | g.uinteger);
+    st(L.rng_uint, i, g.uinteger);
+}
+
+// a fresh episode's state word: step 0, max_tile_seen 4 (src/env.py:183), active, the PCG64 buffer flag
+__device__ inline uint32_t fresh_state(const Pcg64& g) {
+    return (2u << G2048_LS_MAXT_SHIFT) | G2048_LS_ACTIVE | (g.has_uint32 ? G2048_LS_HAS_U32 : 0u);
 }
 
 __device__ inline U4 philox_ctr(uint64_t key, uint64_t seed, uint32_t ctr, uint32_t tag) {
@@ -264,12 +270,11 @@ __device__ inline void reset_lane(const StepArgs& a, uint32_t i, uint64_t prev_s
     const g2048_lanes& L = a.L;
     const uint64_t seed = prev_seed + a.stride;
     Pcg64 g;
+    g.has_uint32 = 0u;
     const uint64_t b = fresh_board<RNG>(seed, a.key, g);
     st(L.seed, i, seed);
     st(L.board, i, b);
-    st(L.step_count, i, 0u);
-    st(L.score, i, 0u);
-    st(L.max_tile, i, (uint8_t)2);
+    st(L.state, i, fresh_state(g));
     if constexpr (RNG == G2048_RNG_PCG64) store_pcg(L, i, g, true);
     if (a.out.mask) st(reinterpret_cast<uint32_t*>(a.out.mask), i, mask_word(action_mask(b)));
     if constexpr (OBS != G2048_OBS_NONE)
@@ -279,7 +284,7 @@ __device__ inline void reset_lane(const StepArgs& a, uint32_t i, uint64_t prev_s
 // Everything one lane reads for one board's step (all boards of a sweep are loaded before any is computed).
 struct LaneIn {
     uint64_t b, seed;
-    uint32_t stt, act, sc, mt, score;
+    uint32_t st, act;    // lane state word (G2048_LS_*), action
     Pcg64 g;
 };
 
@@ -287,11 +292,8 @@ template <int RNG>
 __device__ inline void load_lane(const StepArgs& a, uint32_t i, LaneIn& x) {
     const g2048_lanes& L = a.L;
     x.b = ld(L.board, i);
-    x.stt = ld(L.status, i);
+    x.st = ld(L.state, i);
     x.act = ld(a.actions, i);
-    x.sc = ld(L.step_count, i);
-    x.mt = ld(L.max_tile, i);
-    x.score = ld(L.score, i);
     if constexpr (RNG == G2048_RNG_PCG64) x.g = load_pcg(L, i);   // PCG64 mode reads the seed only on reset
     else x.seed = ld(L.seed, i);
 }
@@ -306,15 +308,18 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     if (a.out.prev_board) st(a.out.prev_board, i, b);
     wobs = false;
     reset = false;
-    if (!(x.stt & G2048_S_ACTIVE) || x.act > 3u) {
+    if (!(x.st & G2048_LS_ACTIVE) || x.act > 3u) {
         st(a.out.reward, i, 0.0f);
         if (a.out.reward64) st(a.out.reward64, i, 0.0);
-        st(a.out.flags, i, (uint8_t)((x.stt & G2048_S_ACTIVE) ? G2048_F_BADACTION : G2048_F_INACTIVE));
+        st(a.out.flags, i, (uint8_t)((x.st & G2048_LS_ACTIVE) ? G2048_F_BADACTION : G2048_F_INACTIVE));
         if (a.out.merged) st(a.out.merged, i, 0u);
+        if (a.out.score_add) st(a.out.score_add, i, 0u);
         return b;
     }
-    const uint32_t sc = x.sc + 1u;
-    uint32_t mt = x.mt;
+    const uint32_t sc0 = x.st & G2048_LS_STEP_MASK;
+    const uint32_t sc = sc0 + (sc0 < G2048_LS_STEP_MASK ? 1u : 0u);   // saturating 20-bit step count
+    uint32_t mt = (x.st >> G2048_LS_MAXT_SHIFT) & 31u;
+    if constexpr (RNG == G2048_RNG_PCG64) x.g.has_uint32 = (x.st & G2048_LS_HAS_U32) ? 1u : 0u;
 
     // Game2048.step (src/game2048.py:40-70): move, score, spawn only if changed, done of the final board
     MoveSummary s;
@@ -341,17 +346,17 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     st(a.out.reward, i, (float)r);
     if (a.out.reward64) st(a.out.reward64, i, r);
     if (LIST && a.out.merged) st(a.out.merged, i, s.list);
+    if (a.out.score_add) st(a.out.score_add, i, s.score);
     if ((done || trunc) && a.auto_reset) {
         reset = true;   // board / lane state / obs are written by reset_lane after the loop
         st(a.out.flags, i, (uint8_t)(fl | G2048_F_RESET));
         return m;
     }
-    if (done || trunc) st(L.status, i, (uint8_t)(x.stt & ~G2048_S_ACTIVE));
+    uint32_t nst = sc | (mt << G2048_LS_MAXT_SHIFT) | ((done || trunc) ? 0u : G2048_LS_ACTIVE);
+    if constexpr (RNG == G2048_RNG_PCG64) nst |= x.g.has_uint32 ? G2048_LS_HAS_U32 : 0u;
     st(a.out.flags, i, (uint8_t)fl);
     st(L.board, i, m);
-    st(L.step_count, i, sc);
-    st(L.score, i, x.score + s.score);
-    st(L.max_tile, i, (uint8_t)mt);
+    st(L.state, i, nst);
     if constexpr (RNG == G2048_RNG_PCG64) store_pcg(L, i, x.g, false);
     wobs = true;
     mbits = bits_mask(bits);
@@ -533,13 +538,11 @@ __global__ void __launch_bounds__(256) reset_kernel(ResetArgs a) {
         if (i < a.n && (!a.reset_mask || ld(a.reset_mask, i))) {
             const uint64_t seed = a.seeds ? ld(a.seeds, i) : ld(a.L.seed, i);
             Pcg64 g;
+            g.has_uint32 = 0u;
             b = fresh_board<RNG>(seed, a.key, g);
             st(a.L.seed, i, seed);
             st(a.L.board, i, b);
-            st(a.L.step_count, i, 0u);
-            st(a.L.score, i, 0u);
-            st(a.L.max_tile, i, (uint8_t)2);  // Game2048Env.max_tile_seen = 4 (src/env.py:183)
-            st(a.L.status, i, (uint8_t)G2048_S_ACTIVE);
+            st(a.L.state, i, fresh_state(g));   // step 0, max_tile_seen 4 (src/env.py:182-183), active
             if constexpr (RNG == G2048_RNG_PCG64) store_pcg(a.L, i, g, true);
             w = true;
             if (a.mask_out) st(reinterpret_cast<uint32_t*>(a.mask_out), i, mask_word(action_mask(b)));
@@ -604,11 +607,10 @@ __global__ void __launch_bounds__(256) seed_kernel(const uint64_t* __restrict__ 
 struct SampleArgs {
     const float* logits;
     const int8_t* mask;
-    const uint8_t* active;
+    const uint32_t* lane_state;
     uint64_t *rs, *inc, *buf;
     uint64_t key;
     const uint64_t* lane_seed;
-    const uint32_t* counter;
     float* probs_out;
     uint8_t* actions;
     uint32_t n;
@@ -619,7 +621,8 @@ struct SampleArgs {
 template <int RNG>
 __global__ void __launch_bounds__(256) sample_kernel(SampleArgs a) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
-        if (a.active && !ld(a.active, i)) continue;
+        const uint32_t ls = a.lane_state ? ld(a.lane_state, i) : G2048_LS_ACTIVE;
+        if (!(ls & G2048_LS_ACTIVE)) continue;
         const float4 lg4 = ld(reinterpret_cast<const float4*>(a.logits), i);
         const float lg[4] = {lg4.x, lg4.y, lg4.z, lg4.w};
         const uint32_t mw = a.mask ? ld(reinterpret_cast<const uint32_t*>(a.mask), i) : 0x01010101u;
@@ -636,7 +639,7 @@ __global__ void __launch_bounds__(256) sample_kernel(SampleArgs a) {
                 st(reinterpret_cast<ulonglong2*>(a.rs), i, make_ulonglong2(g.s_lo, g.s_hi));
             } else {
                 const U4 r = philox_ctr(a.key, a.lane_seed ? ld(a.lane_seed, i) : (uint64_t)i,
-                                        a.counter ? ld(a.counter, i) : 0u, 3u);
+                                        ls & G2048_LS_STEP_MASK, 3u);
                 const uint64_t x = ((uint64_t)r.x << 32) | r.y;
                 u = (double)(x >> 11) * (1.0 / 9007199254740992.0);
             }
@@ -717,6 +720,9 @@ RewardCfg reward_cfg(const g2048_env_cfg& c) {
 
 int check_cfg(const g2048_env_cfg* c) {
     if (!c) return fail(G2048_EINVAL, "cfg is NULL");
+    if (c->max_steps > G2048_MAX_STEPS_LIMIT)
+        return fail(G2048_EINVAL, "max_steps must be <= " + std::to_string(G2048_MAX_STEPS_LIMIT) +
+                                      " (the lane step count is 20 bits) or None");
     if (c->obs_mode < G2048_OBS_NONE || c->obs_mode > G2048_OBS_ONEHOT)
         return fail(G2048_EINVAL, "Unsupported obs_mode: " + std::to_string(c->obs_mode));
     if (c->reward_mode < 0 || c->reward_mode > 1)
@@ -727,10 +733,9 @@ int check_cfg(const g2048_env_cfg* c) {
 }
 
 int check_lanes(const g2048_lanes* L, int rng_mode) {
-    if (!L || !L->board || !L->step_count || !L->score || !L->max_tile || !L->status || !L->seed)
-        return fail(G2048_EINVAL, "lanes: a required buffer is NULL");
-    if (rng_mode == G2048_RNG_PCG64 && (!L->rng_state || !L->rng_inc || !L->rng_buf))
-        return fail(G2048_EINVAL, "lanes: PCG64 mode needs rng_state / rng_inc / rng_buf");
+    if (!L || !L->board || !L->state || !L->seed) return fail(G2048_EINVAL, "lanes: a required buffer is NULL");
+    if (rng_mode == G2048_RNG_PCG64 && (!L->rng_state || !L->rng_inc || !L->rng_uint))
+        return fail(G2048_EINVAL, "lanes: PCG64 mode needs rng_state / rng_inc / rng_uint");
     if (rng_mode != G2048_RNG_PCG64 && rng_mode != G2048_RNG_PHILOX)
         return fail(G2048_EINVAL, "Unsupported rng_mode: " + std::to_string(rng_mode));
     return G2048_OK;
@@ -740,14 +745,11 @@ int check_lanes(const g2048_lanes* L, int rng_mode) {
 g2048_lanes shift_lanes(const g2048_lanes& L, int64_t off) {
     g2048_lanes r = L;
     r.board += off;
-    r.step_count += off;
-    r.score += off;
-    r.max_tile += off;
-    r.status += off;
+    r.state += off;
     r.seed += off;
     if (r.rng_state) r.rng_state += 2 * off;
     if (r.rng_inc) r.rng_inc += 2 * off;
-    if (r.rng_buf) r.rng_buf += off;
+    if (r.rng_uint) r.rng_uint += off;
     return r;
 }
 
@@ -928,6 +930,7 @@ int g2048_step(const g2048_lanes* lanes, const uint8_t* actions, const g2048_env
         if (a.out.merged) a.out.merged += off;
         if (a.out.prev_board) a.out.prev_board += off;
         if (a.out.reward64) a.out.reward64 += off;
+        if (a.out.score_add) a.out.score_add += off;
         a.rc = reward_cfg(*cfg);
         a.obs_scale = cfg->obs_log2_scale;
         a.auto_reset = auto_reset;
@@ -991,10 +994,9 @@ int g2048_move(const uint64_t* boards, const uint8_t* actions, uint64_t* out_boa
     return G2048_OK;
 }
 
-int g2048_sample(const float* logits, const int8_t* mask, const uint8_t* active, int greedy, int rng_mode,
+int g2048_sample(const float* logits, const int8_t* mask, const uint32_t* lane_state, int greedy, int rng_mode,
                  uint64_t* rng_state, uint64_t* rng_inc, uint64_t* rng_buf, uint64_t philox_key,
-                 const uint64_t* lane_seed, const uint32_t* counter, float* probs_out, uint8_t* actions, int64_t n,
-                 void* stream) {
+                 const uint64_t* lane_seed, float* probs_out, uint8_t* actions, int64_t n, void* stream) {
     if (n < 0) return fail(G2048_EINVAL, "n < 0");
     if (!logits || !actions) return fail(G2048_EINVAL, "logits / actions are required");
     if (!greedy && rng_mode == G2048_RNG_PCG64 && (!rng_state || !rng_inc || !rng_buf))
@@ -1003,11 +1005,10 @@ int g2048_sample(const float* logits, const int8_t* mask, const uint8_t* active,
         return fail(G2048_EINVAL, "Unsupported rng_mode: " + std::to_string(rng_mode));
     for (int64_t off = 0; off < n; off += kMaxLanesPerLaunch) {
         const uint32_t m = (uint32_t)(n - off < kMaxLanesPerLaunch ? n - off : kMaxLanesPerLaunch);
-        SampleArgs a{logits + 4 * off, mask ? mask + 4 * off : nullptr, active ? active + off : nullptr,
+        SampleArgs a{logits + 4 * off, mask ? mask + 4 * off : nullptr, lane_state ? lane_state + off : nullptr,
                      rng_state ? rng_state + 2 * off : nullptr, rng_inc ? rng_inc + 2 * off : nullptr,
                      rng_buf ? rng_buf + off : nullptr, philox_key, lane_seed ? lane_seed + off : nullptr,
-                     counter ? counter + off : nullptr, probs_out ? probs_out + 4 * off : nullptr, actions + off, m,
-                     greedy};
+                     probs_out ? probs_out + 4 * off : nullptr, actions + off, m, greedy};
         const int grid = grid_for(m, 256, 2048);
         if (rng_mode == G2048_RNG_PCG64) hipLaunchKernelGGL(sample_kernel<G2048_RNG_PCG64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
         else hipLaunchKernelGGL(sample_kernel<G2048_RNG_PHILOX>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);

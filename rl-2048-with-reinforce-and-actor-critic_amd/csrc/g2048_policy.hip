@@ -117,12 +117,11 @@ __global__ void __launch_bounds__(256) pack_kernel(PackArgs a) {
 struct PolArgs {
     const float* net;
     const uint64_t* boards;
-    const uint8_t* active;   // status (bit 0) or NULL
+    const uint32_t* lane_state;   // env lane state words (G2048_LS_ACTIVE, step count) or NULL
     const int32_t* lane_index;   // entry j -> lane lane_index[j] (NULL: lane j)
     uint64_t *rs, *inc, *buf;
     uint64_t key;
     const uint64_t* lane_seed;
-    const uint32_t* counter;
     float* probs_out;
     float* logits_out;
     uint8_t* actions;
@@ -272,7 +271,8 @@ __global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) policy_k
         const uint64_t b = a.boards[i];
         float lg[4];
         mlp_logits<NT1, NT2, ACT, OBS>(sm, w2q, b, a.obs_scale, lane, lg);
-        if (h == 0 && j < a.n && (!a.active || (a.active[i] & 1u))) {
+        const uint32_t ls = a.lane_state ? a.lane_state[i] : G2048_LS_ACTIVE;
+        if (h == 0 && j < a.n && (ls & G2048_LS_ACTIVE)) {
             if (a.logits_out) reinterpret_cast<float4*>(a.logits_out)[i] = make_float4(lg[0], lg[1], lg[2], lg[3]);
             const uint32_t mw = a.use_mask ? mask_word_of(b) : 0x01010101u;
             double u = 0.0;
@@ -288,7 +288,7 @@ __global__ void __launch_bounds__(kPolBlock, pol_waves_per_simd<NT1>()) policy_k
                     reinterpret_cast<ulonglong2*>(a.rs)[i] = make_ulonglong2(g.s_lo, g.s_hi);
                 } else {
                     const uint64_t sd = a.lane_seed ? a.lane_seed[i] : (uint64_t)i;
-                    U4 c{(uint32_t)sd, (uint32_t)(sd >> 32), a.counter ? a.counter[i] : 0u, 3u};
+                    U4 c{(uint32_t)sd, (uint32_t)(sd >> 32), ls & G2048_LS_STEP_MASK, 3u};
                     const U4 r = philox4x32(c, (uint32_t)a.key, (uint32_t)(a.key >> 32));
                     const uint64_t xx = ((uint64_t)r.x << 32) | r.y;
                     u = (double)(xx >> 11) * (1.0 / 9007199254740992.0);
@@ -647,6 +647,11 @@ struct GradArgs {
     float huber_delta;
     const float* target;     // [n]
     float* delta_out;        // [n] or NULL
+    float* v_out;            // [n] or NULL: V(s) of each sample (critic mode)
+    // column window: sample j's a1^T / d2^T column is col_off + j; groups of 32 processed: ngroups (columns
+    // col_off .. col_off + 32 ngroups - 1; those past n are written as zero-coefficient padding)
+    uint32_t col_off, ngroups;
+    int part_accum;          // add this launch's per-wave partials to `part` instead of overwriting it
 };
 
 template <int NT1, int NT2>
@@ -720,7 +725,7 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
 #pragma unroll
     for (int k = 0; k < 2 * NT2; k++) dw3acc[k] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
     const uint32_t waves = gridDim.x * (kPolBlock / 64);
-    const uint32_t groups = a.ld >> 5;
+    const uint32_t groups = a.ngroups;
 #if G2048_DIAG
     unsigned long long gph[6] = {0, 0, 0, 0, 0, 0};
     unsigned long long gtp = __builtin_amdgcn_s_memrealtime();
@@ -740,7 +745,8 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         // a compiler memory barrier per group: without it the net tensors' LDS reads (loop-invariant) are hoisted
         // out of the group loop into hundreds of registers
         asm volatile("" ::: "memory");
-        const uint32_t off = (j + 4u * (uint32_t)h * a.ld) * 4u;   // byte offset: column j, + acc_row's 4h rows
+        const uint32_t cj = a.col_off + j;                        // this sample's column
+        const uint32_t off = (cj + 4u * (uint32_t)h * a.ld) * 4u;  // byte offset: column cj, + acc_row's 4h rows
         uint32_t ld4 = a.ld * 4u;                                    // row stride in bytes (see col_store)
         const bool valid = j < a.n;
         const uint64_t b = valid ? a.boards[j] : 0ull;
@@ -787,7 +793,7 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
             }
         }
         lds_fence();
-        if (h == 0) col_store(ra1, H1p, ld4, j * 4u, 1.0f);   // the ones row: db2 comes out of the dW2 GEMM
+        if (h == 0) col_store(ra1, H1p, ld4, cj * 4u, 1.0f);  // the ones row: db2 comes out of the dW2 GEMM
         GRAD_PH(0);
         float h2[NT2][16];
         float lg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -858,6 +864,7 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
             g[0] = gd * cf;
             g[1] = g[2] = g[3] = 0.0f;
             if (valid && h == 0 && a.delta_out) a.delta_out[j] = tg - lg[0];
+            if (valid && h == 0 && a.v_out) a.v_out[j] = lg[0];
         }
         lds_fence();   // the previous group's reads of S.g are done
         if (h == 0) {
@@ -980,24 +987,31 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
     // ---- this wave's partial gradients
     const uint32_t wg = blockIdx.x * (kPolBlock / 64) + w;
     float* out = a.part + (size_t)wg * grad_part_floats(NT1, NT2);
+    const bool acc = a.part_accum != 0;   // this wave owns its row: a plain read-modify-write
     lds_fence();
 #pragma unroll
     for (int k = 0; k < 2 * NT1; k++)   // block k: h1 units 16k..16k+15; row 4 q16 + r = feature
 #pragma unroll
-        for (int r = 0; r < 4; r++) out[(4 * q16 + r) * H1p + 16 * k + l16] = dw1acc[k][r];
-    for (int k = lane; k < H1p; k += 64) out[16 * H1p + k] = S.db1[w][k];
+        for (int r = 0; r < 4; r++) {
+            float* p = out + (4 * q16 + r) * H1p + 16 * k + l16;
+            *p = (acc ? *p : 0.0f) + dw1acc[k][r];
+        }
+    for (int k = lane; k < H1p; k += 64) out[16 * H1p + k] = (acc ? out[16 * H1p + k] : 0.0f) + S.db1[w][k];
     if (q16 == 0) {                     // rows 0..3 = actions
 #pragma unroll
         for (int k = 0; k < 2 * NT2; k++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) out[17 * H1p + (16 * k + l16) * 4 + r] = dw3acc[k][r];
+            for (int r = 0; r < 4; r++) {
+                float* p = out + 17 * H1p + (16 * k + l16) * 4 + r;
+                *p = (acc ? *p : 0.0f) + dw3acc[k][r];
+            }
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         float v = h == 0 ? gsum[k] : 0.0f;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-        if (lane == 0) out[17 * H1p + 4 * H2p + k] = v;
+        if (lane == 0) out[17 * H1p + 4 * H2p + k] = (acc ? out[17 * H1p + 4 * H2p + k] : 0.0f) + v;
     }
 }
 
@@ -1103,11 +1117,11 @@ int g2048_policy_pack(const float* W1, const float* b1, const float* W2, const f
     return G2048_OK;
 }
 
-int g2048_policy(const float* packed, int h1, int h2, int activation, const uint64_t* boards, const uint8_t* active,
-                 const int32_t* lane_index, int obs_mode, float obs_scale, int use_mask, int greedy, int rng_mode, uint64_t* rng_state,
-                 const uint64_t* rng_inc, const uint64_t* rng_buf, uint64_t philox_key, const uint64_t* lane_seed,
-                 const uint32_t* counter, float* probs_out, float* logits_out, uint8_t* actions, int64_t n,
-                 void* stream) {
+int g2048_policy(const float* packed, int h1, int h2, int activation, const uint64_t* boards,
+                 const uint32_t* lane_state, const int32_t* lane_index, int obs_mode, float obs_scale, int use_mask,
+                 int greedy, int rng_mode, uint64_t* rng_state, const uint64_t* rng_inc, const uint64_t* rng_buf,
+                 uint64_t philox_key, const uint64_t* lane_seed, float* probs_out, float* logits_out,
+                 uint8_t* actions, int64_t n, void* stream) {
     if (n < 0 || n > (int64_t)0xFFFFFFE0) return pfail(G2048_EINVAL, "n out of range");
     if (n == 0) return G2048_OK;
     if (!packed || !boards || !actions) return pfail(G2048_EINVAL, "packed / boards / actions is NULL");
@@ -1122,14 +1136,13 @@ int g2048_policy(const float* packed, int h1, int h2, int activation, const uint
     PolArgs a;
     a.net = packed;
     a.boards = boards;
-    a.active = active;
+    a.lane_state = lane_state;
     a.lane_index = lane_index;
     a.rs = rng_state;
     a.inc = const_cast<uint64_t*>(rng_inc);
     a.buf = const_cast<uint64_t*>(rng_buf);
     a.key = philox_key;
     a.lane_seed = lane_seed;
-    a.counter = counter;
     a.probs_out = probs_out;
     a.logits_out = logits_out;
     a.actions = actions;
@@ -1194,10 +1207,13 @@ int g2048_actor_grad_waves(void) {
 // the actor and critic entry points share one kernel (GradArgs::critic selects the loss gradient)
 static int actor_or_critic_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
                          float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions,
-                         const float* coef, int64_t n, int64_t ld, float* a1t, float* d2t, float* partials,
-                         int64_t waves, void* stream, int critic, int huber, float huber_delta, const float* target,
-                         float* delta_out) {
+                         const float* coef, int64_t n, int64_t ld, int64_t col_off, int64_t ncols, float* a1t, float* d2t,
+                         float* partials, int accumulate, int64_t waves, void* stream, int critic, int huber,
+                         float huber_delta, const float* target, float* delta_out, float* v_out) {
     if (n < 0 || ld < n || (ld & 31) || ld > ((int64_t)1 << 21)) return pfail(G2048_EINVAL, "fused gradient: bad n / ld");
+    if (col_off < 0 || (col_off & 31) || ncols < n || (ncols & 31) || col_off + ncols > ld)
+        return pfail(G2048_EINVAL, "fused gradient: bad column window (col_off / ncols multiples of 32, n <= ncols, "
+                                   "col_off + ncols <= ld)");
     if (g2048_grad_packed_size(h1, h2) < 0) return pfail(G2048_EINVAL, "fused gradient: hidden sizes must be in 1..256");
     if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
         return pfail(G2048_EINVAL, "Unsupported activation");
@@ -1224,6 +1240,10 @@ static int actor_or_critic_grad(const float* packed, const float* grad_packed, i
     a.huber_delta = huber_delta;
     a.target = target;
     a.delta_out = delta_out;
+    a.v_out = v_out;
+    a.col_off = (uint32_t)col_off;
+    a.ngroups = (uint32_t)(ncols >> 5);
+    a.part_accum = accumulate;
     const int grid = (int)(waves / (kPolBlock / 64));   // one workgroup per CU; every wave writes its partial row
     const int nt1 = tiles_for(h1), nt2 = tiles_for(h2);
     hipStream_t s = (hipStream_t)stream;
@@ -1243,17 +1263,20 @@ int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int 
                      int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, void* stream) {
     if (n > 0 && !actions) return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
     return actor_or_critic_grad(packed, grad_packed, h1, h2, activation, obs_mode, obs_scale, use_mask, boards, actions,
-                                coef, n, ld, a1t, d2t, partials, waves, stream, 0, 0, 0.0f, nullptr, nullptr);
+                                coef, n, ld, 0, ld, a1t, d2t, partials, 0, waves, stream, 0, 0, 0.0f, nullptr, nullptr,
+                                nullptr);
 }
 
 int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
                       float obs_scale, int loss, float huber_delta, const uint64_t* boards, const float* target,
-                      const float* weight, float* delta_out, int64_t n, int64_t ld, float* a1t, float* d2t,
-                      float* partials, int64_t waves, void* stream) {
+                      const float* weight, float* delta_out, float* value_out, int64_t n, int64_t ld, int64_t col_off,
+                      int64_t ncols, float* a1t, float* d2t, float* partials, int accumulate, int64_t waves,
+                      void* stream) {
     if (loss != 0 && loss != 1) return pfail(G2048_EINVAL, "Unknown critic loss type");
     if (n > 0 && !target) return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
     return actor_or_critic_grad(packed, grad_packed, h1, h2, activation, obs_mode, obs_scale, 0, boards, nullptr, weight,
-                                n, ld, a1t, d2t, partials, waves, stream, 1, loss, huber_delta, target, delta_out);
+                                n, ld, col_off, ncols, a1t, d2t, partials, accumulate, waves, stream, 1, loss,
+                                huber_delta, target, delta_out, value_out);
 }
 
 int g2048_rollout(const float* packed, int h1, int h2, int activation, const g2048_env_cfg* cfg, int greedy,

@@ -97,7 +97,7 @@ class Game2048:
         # the vectorised env deactivates a lane once it is done; Game2048 keeps accepting steps (the
         # reference never stops a finished game), so re-activate it
         if flags & L.F_TERMINATED:
-            self._vec.status.fill_(L.S_ACTIVE)
+            self._vec.set_active()
         return bool(flags & L.F_CHANGED), self.state, decode_merged(merged), bool(flags & L.F_TERMINATED)
 
     def get_action_mask(self) -> list[int]:
@@ -163,7 +163,7 @@ class Game2048Env:
         truncated = bool(flags & L.F_TRUNCATED)
         invalid = bool(flags & L.F_INVALID)
         if terminated or truncated:
-            self._vec.status.fill_(L.S_ACTIVE)  # the reference env keeps stepping after the end if asked to
+            self._vec.set_active()  # the reference env keeps stepping after the end if asked to
         info = {"score": self._score, "raw_state": self.state, "merged": decode_merged(merged),
                 "invalid_action": invalid, "step_index": self._step_count}
         return self._obs(obs, mask), float(reward), terminated, truncated, info

@@ -73,12 +73,16 @@ class VecGame2048Env:
     rng="philox": Philox4x32-10 keyed by (philox_key, lane seed, step) -- same distribution, no RNG state traffic.
     auto_reset: a lane that terminates/truncates restarts in the same call with seed += reset_stride.
     lane_offset: global index of lane 0 (for sharding a global board batch across ranks).
+    track_score: keep Game2048.score per lane (info["score"]) from the step's score increment (one small torch op
+    per step); off for pure throughput runs.
+    Lane state lives in one uint32 word per lane (include/g2048.h G2048_LS_*): ``step_count``, ``max_tile``,
+    ``status`` and ``active`` are views computed from it.
     """
 
     def __init__(self, num_envs: int, config: Game2048EnvConfig | None = None, device=None, rng: str = "pcg64",
                  auto_reset: bool = False, reset_stride: int | None = None, philox_key: int = 0x2048,
                  lane_offset: int = 0, record_merged: bool = False, record_prev_board: bool = False,
-                 record_reward64: bool = False):
+                 record_reward64: bool = False, track_score: bool = True):
         if num_envs <= 0:
             raise ValueError("num_envs must be positive")
         self.config = config or Game2048EnvConfig()
@@ -97,15 +101,14 @@ class VecGame2048Env:
         z = lambda dt, *s: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
         # lane state (g2048_lanes)
         self.board = z(torch.int64, n)
-        self.step_count = z(torch.int32, n)
-        self.score = z(torch.int32, n)
-        self.max_tile = z(torch.uint8, n)
-        self.status = z(torch.uint8, n)
+        self.state = z(torch.int32, n)                   # G2048_LS_* word (uint32 bits in an int32 tensor)
         self.seed = z(torch.int64, n)
         pcg = self.rng_mode == L.RNG_PCG64
         self.rng_state = z(torch.int64, 2 * n) if pcg else None
         self.rng_inc = z(torch.int64, 2 * n) if pcg else None
-        self.rng_buf = z(torch.int64, n) if pcg else None
+        self.rng_uint = z(torch.int32, n) if pcg else None
+        self.score = z(torch.int64, n) if track_score else None
+        self._score_add = z(torch.int32, n) if track_score else None
         # outputs (g2048_step_out)
         self.reward = z(torch.float32, n)
         # the fp64 reward (the Python float src/env.py:261 returns); off by default: +8 B per board-step
@@ -116,10 +119,10 @@ class VecGame2048Env:
         self.obs = z(torch.float32, n, self.obs_width)
         self.merged = z(torch.int32, n) if record_merged else None
         self.prev_board = z(torch.int64, n) if record_prev_board else None
-        self._lanes = L.Lanes(*[L.ptr(t) for t in (self.board, self.step_count, self.score, self.max_tile, self.status,
-                                                   self.seed, self.rng_state, self.rng_inc, self.rng_buf)])
+        self._lanes = L.Lanes(*[L.ptr(t) for t in (self.board, self.state, self.seed, self.rng_state, self.rng_inc,
+                                                   self.rng_uint)])
         self._out = L.StepOut(L.ptr(self.reward), L.ptr(self.flags), L.ptr(self.mask), L.ptr(self.obs),
-                              L.ptr(self.merged), L.ptr(self.prev_board), L.ptr(self.reward64))
+                              L.ptr(self.merged), L.ptr(self.prev_board), L.ptr(self.reward64), L.ptr(self._score_add))
         self._lib = L.lib()
         self._stream = L.stream_handle(self.device)
 
@@ -141,6 +144,11 @@ class VecGame2048Env:
             L.check(self._lib.g2048_reset(ctypes.byref(self._lanes), L.ptr(seeds), L.ptr(m), ctypes.byref(self._cfg),
                                           self.rng_mode, self.philox_key, L.ptr(self.mask), L.ptr(self.obs), self.n,
                                           L.stream_handle(self.device)))
+        if self.score is not None:
+            if m is None:
+                self.score.zero_()
+            else:
+                self.score.masked_fill_(m != 0, 0)
         return self._obs_view(), {"score": self.score, "board": self.board}
 
     def step_into(self, actions: torch.Tensor, reward: torch.Tensor | None = None, flags: torch.Tensor | None = None,
@@ -157,13 +165,16 @@ class VecGame2048Env:
                             L.ptr(flags if flags is not None else self.flags), L.ptr(self.mask),
                             L.ptr(self.obs) if write_obs else None,
                             L.ptr(self.merged), L.ptr(prev_board if prev_board is not None else self.prev_board),
-                            L.ptr(reward64 if reward64 is not None else self.reward64))
+                            L.ptr(reward64 if reward64 is not None else self.reward64), L.ptr(self._score_add))
         if torch.cuda.current_device() != self.device.index:
             with torch.cuda.device(self.device):
                 return self.step_into(actions, reward, flags, prev_board, write_obs, reward64)
         L.check(self._lib.g2048_step(ctypes.byref(self._lanes), L.ptr(actions), ctypes.byref(self._cfg),
                                      ctypes.byref(out), self.rng_mode, self.philox_key, int(self.auto_reset),
                                      self.reset_stride, self.n, L.stream_handle(self.device)))
+        if self.score is not None:   # Game2048.score += sum(merged); an auto-reset lane starts its new game at 0
+            fl = flags if flags is not None else self.flags
+            self.score.add_(self._score_add).masked_fill_((fl & L.F_RESET) != 0, 0)
 
     def step(self, actions):
         """Game2048Env.step (src/env.py:264-302) for every lane.  actions: int tensor/sequence of n in 0..3.
@@ -187,14 +198,52 @@ class VecGame2048Env:
         rew = self.reward64 if self.reward64 is not None else self.reward
         return (self._obs_view(), rew, (f & L.F_TERMINATED) != 0, (f & L.F_TRUNCATED) != 0, info)
 
+    # ---- views of the lane state word
+    @property
+    def step_count(self) -> torch.Tensor:
+        """Game2048Env._step_count per lane (int32)."""
+        return self.state & L.LS_STEP_MASK
+
+    @property
+    def max_tile(self) -> torch.Tensor:
+        """log2(Game2048Env.max_tile_seen) per lane (int32)."""
+        return (self.state >> L.LS_MAXT_SHIFT) & 31
+
+    @property
+    def status(self) -> torch.Tensor:
+        """1 where the lane is in an episode, else 0 (uint8)."""
+        return ((self.state & L.LS_ACTIVE) != 0).to(torch.uint8)
+
     @property
     def active(self) -> torch.Tensor:
-        return (self.status & L.S_ACTIVE) != 0
+        return (self.state & L.LS_ACTIVE) != 0
+
+    def set_active(self, lanes: torch.Tensor | None = None) -> None:
+        """Mark lanes (all, or a bool mask) as in-episode again (the single-board drop-ins keep stepping a finished
+        game, as the reference allows)."""
+        on = self.state | L.LS_ACTIVE
+        if lanes is None:
+            self.state.copy_(on)
+        else:
+            self.state.copy_(torch.where(lanes, on, self.state))
+
+    def set_lane_state(self, step_count=None, max_tile_exp=None, active=None) -> None:
+        """Overwrite fields of every lane's state word (synthetic workloads / tests)."""
+        st = self.state
+        if step_count is not None:
+            st = (st & ~L.LS_STEP_MASK) | (torch.as_tensor(step_count, device=self.device).to(torch.int32) & L.LS_STEP_MASK)
+        if max_tile_exp is not None:
+            st = (st & ~(31 << L.LS_MAXT_SHIFT)) | ((torch.as_tensor(max_tile_exp, device=self.device).to(torch.int32)
+                                                     & 31) << L.LS_MAXT_SHIFT)
+        if active is not None:
+            a = torch.as_tensor(active, device=self.device).to(torch.bool)
+            st = torch.where(a, st | L.LS_ACTIVE, st & ~L.LS_ACTIVE)
+        self.state.copy_(st)
 
     @property
     def max_tile_seen(self) -> torch.Tensor:
         """Game2048Env.max_tile_seen per lane (4 at reset; raised by merges >= 8, src/env.py:238-250)."""
-        return torch.ones_like(self.max_tile, dtype=torch.int64) << self.max_tile.to(torch.int64)
+        return torch.ones_like(self.state, dtype=torch.int64) << self.max_tile.to(torch.int64)
 
     def boards_exponents(self) -> torch.Tensor:
         """[n,4,4] int64 exponents (0 = empty) of the current boards."""

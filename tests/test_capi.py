@@ -79,6 +79,14 @@ def test_argument_validation_without_gpu(L):
     out = L.StepOut()
     rc = lib.g2048_step(ctypes.byref(lanes), None, ctypes.byref(cfg), ctypes.byref(out), 0, 0, 0, 0, 1, None)
     assert rc == L.G2048_EINVAL and b"reward mode" in lib.g2048_last_error()
+    cfg.reward_mode, cfg.max_steps = 0, L.MAX_STEPS_LIMIT + 1      # the 20-bit lane step count
+    rc = lib.g2048_step(ctypes.byref(lanes), None, ctypes.byref(cfg), ctypes.byref(out), 0, 0, 0, 0, 1, None)
+    assert rc == L.G2048_EINVAL and b"max_steps" in lib.g2048_last_error()
+    from rl2048_amd.config import Game2048EnvConfig, env_cfg_struct
+
+    with pytest.raises(ValueError, match="max_steps"):
+        env_cfg_struct(Game2048EnvConfig(max_steps=1 << 20))
+    assert env_cfg_struct(Game2048EnvConfig(max_steps=L.MAX_STEPS_LIMIT)).max_steps == L.MAX_STEPS_LIMIT
     with pytest.raises(ValueError):
         L.check(L.G2048_EINVAL)
     # fused policy: shape / mode validation (no launch)
@@ -89,7 +97,7 @@ def test_argument_validation_without_gpu(L):
     assert b"obs width" in lib.g2048_last_error()
     assert lib.g2048_policy_pack(p, p, p, p, p, p, 16, 32, 32, p, 10, None) == L.G2048_EINVAL
     args = [p, 32, 32, L.ACT_RELU, p, None, None, L.OBS_ONEHOT, 1.0, 1, 0, L.RNG_PHILOX, None, None, None, 0, None,
-            None, None, None, p, 4, None]
+            None, None, p, 4, None]
     assert lib.g2048_policy(*args) == L.G2048_EINVAL and b"obs_mode" in lib.g2048_last_error()
     args[7], args[3] = L.OBS_LOG2, 7
     assert lib.g2048_policy(*args) == L.G2048_EINVAL and b"activation" in lib.g2048_last_error()
@@ -106,8 +114,13 @@ def test_argument_validation_without_gpu(L):
     assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL   # ld < n
     gargs[12], gargs[5] = 64, L.OBS_ONEHOT
     assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL and b"obs_mode" in lib.g2048_last_error()
-    cargs = [p, p, 32, 32, L.ACT_RELU, L.OBS_LOG2, 1.0, 2, 1.0, p, p, p, None, 40, 64, p, p, p, 1024, None]
+    cargs = [p, p, 32, 32, L.ACT_RELU, L.OBS_LOG2, 1.0, 2, 1.0, p, p, p, None, None, 40, 128, 0, 64, p, p, p, 0, 1024,
+             None]
     assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"critic loss" in lib.g2048_last_error()
+    cargs[7] = 0
+    for col_off, ncols in ((16, 64), (0, 32), (96, 64), (-32, 64)):   # unaligned, < n, past ld, negative
+        cargs[16], cargs[17] = col_off, ncols
+        assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"column window" in lib.g2048_last_error()
 
 
 def test_config_validation_messages():

@@ -268,7 +268,7 @@ def test_sample_given_identical_probs(lib, golden_dir):
     refs = [O.PCG64(x) for x in seeds]
     for rep in range(3):
         lib.check(L.g2048_sample(lg.data_ptr(), mk.data_ptr(), None, 0, 0, st.data_ptr(), inc.data_ptr(),
-                                 buf.data_ptr(), 0, None, None, probs.data_ptr(), acts.data_ptr(), n, s))
+                                 buf.data_ptr(), 0, None, probs.data_ptr(), acts.data_ptr(), n, s))
         p = probs.cpu().numpy()
         a = acts.cpu().numpy()
         lgm = np.where(mask.astype(bool), logits, np.float32(-1e9))
@@ -278,7 +278,7 @@ def test_sample_given_identical_probs(lib, golden_dir):
         for i in range(n):
             assert a[i] == refs[i].choice4(p[i]), (rep, i)
     # greedy: argmax(probs * mask)
-    lib.check(L.g2048_sample(lg.data_ptr(), mk.data_ptr(), None, 1, 0, None, None, None, 0, None, None, None,
+    lib.check(L.g2048_sample(lg.data_ptr(), mk.data_ptr(), None, 1, 0, None, None, None, 0, None, None,
                              acts.data_ptr(), n, s))
     np.testing.assert_array_equal(acts.cpu().numpy(), np.argmax(p * mask, axis=1))
     del d

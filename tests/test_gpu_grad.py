@@ -170,3 +170,39 @@ def test_fused_critic_grad_ragged_chunks(chunk, act):
     for which in ("critic", "actor"):
         for i, (a, b) in enumerate(zip(grads[True][which], grads[False][which])):
             assert _rel(a, b) < tol, (which, i, _rel(a, b))
+
+
+@pytest.mark.parametrize("aug", [False, True])
+@pytest.mark.parametrize("act", ["Sigmoid", "ReLU"])
+def test_fused_critic_rows_mode(act, aug):
+    """The per-time-row critic pass (ReinforceAgent._critic_grad_rows: rows last-first, each launch's V(s) serving as
+    the previous row's V(s'), one column buffer, accumulated partials) forced on a small batch -- hundreds of
+    rows, most of them ragged, a column-buffer flush forced by a small chunk -- against the torch backprop: critic
+    and actor gradients and the TD errors (through the actor's advantages).  Sigmoid 1e-5; ReLU 5e-5 (fp32 ReLU
+    derivative flips, as in test_fused_critic_grad_ragged_chunks)."""
+    acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.97, use_critic=True, critic_loss_type="huber",
+                huber_delta=0.5, augmentation=aug)
+    grads = {}
+    batch = None
+    for mode in ("rows", "torch"):
+        ag = _agent((64, 96), act, obs_mode="log2", **acfg)
+        ag.use_fused_grad = mode == "rows"
+        ag.critic_rows_min_avg = 0
+        ag.grad_chunk_steps = 4096
+        if batch is None:
+            batch = ag.rollout_batch(list(range(100, 100 + 160)), list(range(900, 900 + 160)))
+        if mode == "rows":
+            assert ag._critic_by_rows(_steps_of(ag, batch))
+        ag.update_from_batch(batch)
+        torch.cuda.synchronize()
+        grads[mode] = {k: [g.cpu().numpy() for g in v] for k, v in ag.last_grads.items()}
+    tol = 1e-5 if act == "Sigmoid" else 5e-5
+    for which in ("critic", "actor"):
+        for i, (a, b) in enumerate(zip(grads["rows"][which], grads["torch"][which])):
+            assert _rel(a, b) < tol, (which, i, _rel(a, b))
+
+
+def _steps_of(agent, batch):
+    from rl2048_amd.agent import _Steps
+
+    return _Steps(agent, batch.lengths, batch.actions, batch.rewards, boards=batch.boards)

@@ -5,7 +5,7 @@
   under-fill the 32-unit tiles, both activations and both 16-wide obs modes;
 * choice: the fused kernel's probabilities and actions equal g2048_sample run on the fused kernel's own logits with
   the same RNG state (bit-exact), for PCG64 / Philox / greedy, with and without the action mask;
-* inactive lanes (status bit 0 clear) are left untouched; n not a multiple of the 32-board group.
+* inactive lanes (lane state word without G2048_LS_ACTIVE) are left untouched; n not a multiple of the 32-board group.
 """
 import ctypes
 
@@ -75,7 +75,7 @@ def test_fused_logits_match_gemm_path(h1, h2, act, obs):
     actions = torch.empty(n, dtype=torch.uint8, device=DEV)
     a = {"ReLU": L.ACT_RELU, "Sigmoid": L.ACT_SIGMOID}[act]
     L.check(lib.g2048_policy(L.ptr(packed), h1, h2, a, L.ptr(boards), None, None, code, 0.0625, 1, 1,
-                             L.RNG_PHILOX, None, None, None, 0, None, None, None, L.ptr(logits), L.ptr(actions), n,
+                             L.RNG_PHILOX, None, None, None, 0, None, None, L.ptr(logits), L.ptr(actions), n,
                              L.stream_handle(DEV)))
     torch.cuda.synchronize()
     scale = float(ref.abs().max()) + 1e-30
@@ -95,29 +95,31 @@ def test_fused_choice_equals_sample_kernel(rng, greedy, mask):
     p = _params(h1, h2, 9)
     packed = _pack(L, lib, p, h1, h2)
     seeds, st, inc, buf = _pcg(L, lib, n, 1234)
-    counter = torch.arange(n, dtype=torch.int32, device=DEV) * 3
-    status = torch.ones(n, dtype=torch.uint8, device=DEV)
-    status[::7] = 0                            # inactive lanes are left untouched
+    # env lane state words: the active bit and the step count (the Philox draw's counter)
+    status = torch.ones(n, dtype=torch.bool, device=DEV)
+    status[::7] = False                        # inactive lanes are left untouched
+    lane_state = (torch.arange(n, dtype=torch.int32, device=DEV) * 3) | torch.where(
+        status, torch.tensor(L.LS_ACTIVE, dtype=torch.int32, device=DEV), torch.tensor(0, dtype=torch.int32, device=DEV))
     rmode = L.RNG_PCG64 if rng == "pcg64" else L.RNG_PHILOX
     key = 0x1234ABCD5678
     st2 = st.clone()
     logits = torch.empty(n, 4, device=DEV)
     probs = torch.full((n, 4), -1.0, device=DEV)
     actions = torch.full((n,), 9, dtype=torch.uint8, device=DEV)
-    L.check(lib.g2048_policy(L.ptr(packed), h1, h2, L.ACT_RELU, L.ptr(boards), L.ptr(status), None, L.OBS_LOG2,
+    L.check(lib.g2048_policy(L.ptr(packed), h1, h2, L.ACT_RELU, L.ptr(boards), L.ptr(lane_state), None, L.OBS_LOG2,
                              0.0625, mask, greedy, rmode, L.ptr(st), L.ptr(inc), L.ptr(buf), key, L.ptr(seeds),
-                             L.ptr(counter), L.ptr(probs), L.ptr(logits), L.ptr(actions), n, L.stream_handle(DEV)))
+                             L.ptr(probs), L.ptr(logits), L.ptr(actions), n, L.stream_handle(DEV)))
     # the same choice on the fused kernel's own logits through g2048_sample
     mk = torch.empty(n, 4, dtype=torch.int8, device=DEV)
     x = torch.empty(n, 16, dtype=torch.float32, device=DEV)
     L.check(lib.g2048_obs(L.ptr(boards), L.OBS_LOG2, 0.0625, L.ptr(x), L.ptr(mk), n, L.stream_handle(DEV)))
     probs2 = torch.full((n, 4), -1.0, device=DEV)
     actions2 = torch.full((n,), 9, dtype=torch.uint8, device=DEV)
-    L.check(lib.g2048_sample(L.ptr(logits), L.ptr(mk) if mask else None, L.ptr(status), greedy, rmode, L.ptr(st2),
-                             L.ptr(inc), L.ptr(buf), key, L.ptr(seeds), L.ptr(counter), L.ptr(probs2),
+    L.check(lib.g2048_sample(L.ptr(logits), L.ptr(mk) if mask else None, L.ptr(lane_state), greedy, rmode,
+                             L.ptr(st2), L.ptr(inc), L.ptr(buf), key, L.ptr(seeds), L.ptr(probs2),
                              L.ptr(actions2), n, L.stream_handle(DEV)))
     torch.cuda.synchronize()
-    act = status.bool()
+    act = status
     assert torch.equal(actions, actions2)
     assert torch.equal(probs, probs2)
     assert torch.equal(st, st2)                # the PCG64 streams advanced identically
@@ -168,12 +170,12 @@ def test_lane_index_subset_equals_full_call():
     probs = torch.full((n, 4), -1.0, device=DEV)
     actions = torch.full((n,), 9, dtype=torch.uint8, device=DEV)
     L.check(lib.g2048_policy(L.ptr(packed), h1, h2, L.ACT_RELU, L.ptr(boards), None, L.ptr(idx), L.OBS_LOG2, 0.0625,
-                             1, 0, L.RNG_PCG64, L.ptr(st), L.ptr(inc), L.ptr(buf), 0, None, None, L.ptr(probs), None,
+                             1, 0, L.RNG_PCG64, L.ptr(st), L.ptr(inc), L.ptr(buf), 0, None, L.ptr(probs), None,
                              L.ptr(actions), idx.numel(), L.stream_handle(DEV)))
     probs_f = torch.empty(n, 4, device=DEV)
     actions_f = torch.empty(n, dtype=torch.uint8, device=DEV)
     L.check(lib.g2048_policy(L.ptr(packed), h1, h2, L.ACT_RELU, L.ptr(boards), None, None, L.OBS_LOG2, 0.0625, 1, 0,
-                             L.RNG_PCG64, L.ptr(st_full), L.ptr(inc), L.ptr(buf), 0, None, None, L.ptr(probs_f), None,
+                             L.RNG_PCG64, L.ptr(st_full), L.ptr(inc), L.ptr(buf), 0, None, L.ptr(probs_f), None,
                              L.ptr(actions_f), n, L.stream_handle(DEV)))
     torch.cuda.synchronize()
     m = torch.zeros(n, dtype=torch.bool, device=DEV)
