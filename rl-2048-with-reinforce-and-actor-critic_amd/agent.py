@@ -500,7 +500,7 @@ class ReinforceAgent:
             a1t[:, used:m].zero_()
             d2t[:, used:m].zero_()
             P = 1
-            while P < 64 and m // (2 * P) >= 8192:
+            while P < 128 and m // (2 * P) >= 8192:
                 P *= 2
             q = m // P
             big += torch.bmm(a1t[:, :m].view(H1p + 1, P, q).transpose(0, 1),
@@ -566,10 +566,11 @@ class ReinforceAgent:
                 if k:
                     b = self._symmetry_boards(b, k)
                 # split-K of the layer-2 weight gradient over P column blocks (a strided-batched fp32 GEMM; at most
-                # 64 blocks of >= 8192 samples: measured faster than 512 blocks of 2048, and the gradient's fp32
+                # 128 blocks of >= 8192 samples: 132 TFLOP/s at 2^20 columns against 121 at 64 blocks, 56 at 16 and
+                # 25 unsplit -- tools/dw2_gemm_probe.py, profiles/round2/dw2_gemm_probe.log; the gradient's fp32
                 # error at millions of samples is set by ReLU-derivative flips, not by this accumulation --
                 # tests/test_gpu_configs_at_size.py), blocks summed in fp32, chunks accumulated in fp64
-                P = max(1, min(64, m // 8192))
+                P = max(1, min(128, m // 8192))
                 ld = -(-m // (32 * P)) * 32 * P
                 q = ld // P
                 a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)

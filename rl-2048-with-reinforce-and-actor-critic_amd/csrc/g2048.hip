@@ -300,20 +300,24 @@ __device__ inline void load_lane(const StepArgs& a, uint32_t i, LaneIn& x) {
 
 // One lane of Game2048Env.step (src/env.py:264-302).  Returns the final board; wobs = this lane's obs/mask are
 // written by the wave; reset = the episode ended and an auto-reset is pending for this lane.
-template <int RNG, bool LIST>
+// XO (optional outputs, chosen by the launcher): 0 = none of prev_board / reward64 / score_add / merged (the
+// rollout and bench path: no null-pointer tests in the loop, whose uniform conditions the compiler otherwise keeps
+// as spilled 64-bit lane masks), 1 = any of the first three, 2 = the merged list too.
+template <int RNG, int XO>
 __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, const LineFn& lut,
                                      const CodeFn& code, bool& wobs, bool& reset, uint32_t& mbits) {
+    constexpr bool LIST = XO == 2, EXTRA = XO >= 1;
     const g2048_lanes& L = a.L;
     const uint64_t b = x.b;
-    if (a.out.prev_board) st(a.out.prev_board, i, b);
+    if (EXTRA && a.out.prev_board) st(a.out.prev_board, i, b);
     wobs = false;
     reset = false;
     if (!(x.st & G2048_LS_ACTIVE) || x.act > 3u) {
         st(a.out.reward, i, 0.0f);
-        if (a.out.reward64) st(a.out.reward64, i, 0.0);
+        if (EXTRA && a.out.reward64) st(a.out.reward64, i, 0.0);
         st(a.out.flags, i, (uint8_t)((x.st & G2048_LS_ACTIVE) ? G2048_F_BADACTION : G2048_F_INACTIVE));
-        if (a.out.merged) st(a.out.merged, i, 0u);
-        if (a.out.score_add) st(a.out.score_add, i, 0u);
+        if (LIST && a.out.merged) st(a.out.merged, i, 0u);
+        if (EXTRA && a.out.score_add) st(a.out.score_add, i, 0u);
         return b;
     }
     const uint32_t sc0 = x.st & G2048_LS_STEP_MASK;
@@ -344,9 +348,9 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
                         (trunc ? G2048_F_TRUNCATED : 0u) | (invalid ? G2048_F_INVALID : 0u) |
                         (s.overflow ? G2048_F_OVERFLOW : 0u);
     st(a.out.reward, i, (float)r);
-    if (a.out.reward64) st(a.out.reward64, i, r);
+    if (EXTRA && a.out.reward64) st(a.out.reward64, i, r);
     if (LIST && a.out.merged) st(a.out.merged, i, s.list);
-    if (a.out.score_add) st(a.out.score_add, i, s.score);
+    if (EXTRA && a.out.score_add) st(a.out.score_add, i, s.score);
     if ((done || trunc) && a.auto_reset) {
         reset = true;   // board / lane state / obs are written by reset_lane after the loop
         st(a.out.flags, i, (uint8_t)(fl | G2048_F_RESET));
@@ -364,16 +368,15 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
 }
 
 // One sweep of one wave: the step of board w0 + lane (inputs already in registers), its mask, the wave's obs.
-// One sweep of one wave: the step of board w0 + lane (inputs already in registers), its mask, the wave's obs.
 // A lane's first pending reset has its seed read here (`pseed`), so the read is long complete at the tail.
-template <int OBS, int RNG, bool LIST>
+template <int OBS, int RNG, int XO>
 __device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, LaneIn& x, const LineFn& lut,
                                       const CodeFn& code, uint64_t& pending, uint64_t& pseed, uint32_t k) {
     const uint32_t i = w0 + lane;
     bool wobs = false, reset = false;
     uint32_t mbits = 0;
     uint64_t b = 0;
-    if (i < a.n) b = step_lane<RNG, LIST>(a, i, x, lut, code, wobs, reset, mbits);
+    if (i < a.n) b = step_lane<RNG, XO>(a, i, x, lut, code, wobs, reset, mbits);
     if (reset) {
         if (!pending) {
             if constexpr (RNG == G2048_RNG_PCG64) pseed = ld(a.L.seed, i);
@@ -409,7 +412,7 @@ static_assert(kTabVec % kBlock == 0, "table fill: whole chunks per thread");
 // of a 1M-board step per CU cost one pass of one wave instead of one divergent pass in most of the 16 waves.
 // (A dynamic schedule -- chunks claimed with device-scope atomics -- measured slower on MI355X: under this
 // kernel's streaming load an atomic's return takes microseconds, and same-address atomics serialize.)
-template <int OBS, int RNG, bool LDS, bool LIST, int U>
+template <int OBS, int RNG, bool LDS, int XO, int U>
 __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     static_assert(U == 1, "one board per lane per sweep");
     __shared__ uint4 tab_lds[LDS ? kTabVec : 1];
@@ -448,15 +451,15 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     while (w0 < a.n) {                         // wave-uniform
         const uint32_t w2 = w1 + wstride;
         load_lane<RNG>(a, lane_at(w2), C);
-        sweep<OBS, RNG, LIST>(a, w0, lane, A, lut, code, pending, pseed, k);
+        sweep<OBS, RNG, XO>(a, w0, lane, A, lut, code, pending, pseed, k);
         if (w1 >= a.n) break;
         const uint32_t w3 = w2 + wstride;
         load_lane<RNG>(a, lane_at(w3), A);
-        sweep<OBS, RNG, LIST>(a, w1, lane, B, lut, code, pending, pseed, k + 1);
+        sweep<OBS, RNG, XO>(a, w1, lane, B, lut, code, pending, pseed, k + 1);
         if (w2 >= a.n) break;
         const uint32_t w4 = w3 + wstride;
         load_lane<RNG>(a, lane_at(w4), B);
-        sweep<OBS, RNG, LIST>(a, w2, lane, C, lut, code, pending, pseed, k + 2);
+        sweep<OBS, RNG, XO>(a, w2, lane, C, lut, code, pending, pseed, k + 2);
         w0 = w3;
         w1 = w4;
         k += 3;
@@ -715,6 +718,7 @@ RewardCfg reward_cfg(const g2048_env_cfg& c) {
     r.step_reward = c.step_reward;
     r.endgame_penalty = c.endgame_penalty;
     r.invalid_action_penalty = c.invalid_action_penalty;
+    r.terms = reward_terms(r);
     return r;
 }
 
@@ -758,9 +762,10 @@ g2048_lanes shift_lanes(const g2048_lanes& L, int64_t off) {
 constexpr int kStepU = 1;
 
 template <int OBS, int RNG, bool LDS, int U>
-void launch_step3(const StepArgs& a, int grid, bool list, hipStream_t s) {
-    if (list) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, true, U>), dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, false, U>), dim3(grid), dim3(kBlock), 0, s, a);
+void launch_step3(const StepArgs& a, int grid, int xo, hipStream_t s) {
+    if (xo == 2) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 2, U>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (xo == 1) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 1, U>), dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 0, U>), dim3(grid), dim3(kBlock), 0, s, a);
 }
 
 template <int OBS, int RNG, int kU>
@@ -773,9 +778,9 @@ void launch_step_u(const StepArgs& a, int cus, hipStream_t s) {
     int grid = grid_for((a.n + kU - 1) / kU, kBlock, lds ? cus : cus * 2);
     if (grid < min_blocks) grid = (int)min_blocks;
     if (G2048_DIAG && (a.diag & 8)) grid = grid_for(a.n, kBlock, 1 << 30);
-    const bool list = a.out.merged != nullptr;
-    if (lds) launch_step3<OBS, RNG, true, kU>(a, grid, list, s);
-    else launch_step3<OBS, RNG, false, kU>(a, grid, list, s);
+    const int xo = a.out.merged ? 2 : (a.out.prev_board || a.out.reward64 || a.out.score_add) ? 1 : 0;
+    if (lds) launch_step3<OBS, RNG, true, kU>(a, grid, xo, s);
+    else launch_step3<OBS, RNG, false, kU>(a, grid, xo, s);
 }
 
 template <int OBS, int RNG>

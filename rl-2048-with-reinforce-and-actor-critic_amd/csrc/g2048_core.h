@@ -544,30 +544,49 @@ G2048_HD uint64_t spawn_philox(uint64_t b, U4 r) {
 // ---------------------------------------------------------------------------------------------------------
 struct RewardCfg {
     int32_t reward_mode, bonus_mode, use_action_mask;
+    uint32_t terms;   // reward_terms(*this): set by whoever fills the fields
     double base_reward_scale, empty_tile_reward, merge_reward, bonus_scale, step_reward, endgame_penalty,
         invalid_action_penalty;
 };
 
+// The config's branch conditions as one integer word (bits kRw*).  env_reward tests these bits rather than the
+// fields: in the step kernel's loop the fp64 `!= 0.0` tests are VALU compares whose loop-invariant 64-bit results
+// the compiler hoists and spills to VGPR lanes (a v_readlane each per use); a bit test is one scalar instruction.
+constexpr uint32_t kRwInvalidPenalty = 1u, kRwLog2 = 2u, kRwEmpty = 4u, kRwMerge = 8u, kRwEndgame = 16u,
+                   kRwBonusRaw = 32u, kRwBonusLog2 = 64u;
+G2048_HD uint32_t reward_terms(const RewardCfg& c) {
+    return (c.use_action_mask ? 0u : kRwInvalidPenalty) | (c.reward_mode == 0 ? 0u : kRwLog2) |
+           (c.empty_tile_reward != 0.0 ? kRwEmpty : 0u) | (c.merge_reward != 0.0 ? kRwMerge : 0u) |
+           (c.endgame_penalty != 0.0 ? kRwEndgame : 0u) | (c.bonus_mode == 1 ? kRwBonusRaw : 0u) |
+           (c.bonus_mode == 2 ? kRwBonusLog2 : 0u);
+}
+
 G2048_HD double env_reward(const RewardCfg& c, const MoveSummary& s, uint64_t final_board, bool done, bool invalid,
                            uint32_t& max_tile_e) {
-    if (!c.use_action_mask && invalid) return c.invalid_action_penalty;
-    double r = c.reward_mode == 0 ? (double)s.score : (double)s.sum_e;
+    uint32_t t = c.terms;
+#ifdef __HIP_DEVICE_COMPILE__
+    // opaque per call: otherwise each bit test is hoisted out of the caller's loop as a 64-bit lane mask (it guards
+    // divergent code) and spilled like the fp64 compares were
+    asm volatile("" : "+s"(t));
+#endif
+    if ((t & kRwInvalidPenalty) && invalid) return c.invalid_action_penalty;
+    double r = (t & kRwLog2) ? (double)s.sum_e : (double)s.score;
     r *= c.base_reward_scale;
-    if (c.empty_tile_reward != 0.0) {
+    if (t & kRwEmpty) {
         const int ne = 16 - popc64(nz_bits(final_board));
         r += c.empty_tile_reward * (double)ne;
     }
-    if (c.merge_reward != 0.0) r += c.merge_reward * (double)s.count;
+    if (t & kRwMerge) r += c.merge_reward * (double)s.count;
     if (s.max_e >= 3u && s.max_e > max_tile_e) {
         double bonus = 0.0;
-        if (c.bonus_mode == 1) bonus = (double)(1u << s.max_e);
-        else if (c.bonus_mode == 2) bonus = (double)s.max_e;
+        if (t & kRwBonusRaw) bonus = (double)(1u << s.max_e);
+        else if (t & kRwBonusLog2) bonus = (double)s.max_e;
         max_tile_e = s.max_e;
         bonus *= c.bonus_scale;
         r += bonus;
     }
     r += c.step_reward;
-    if (done && c.endgame_penalty != 0.0) r += c.endgame_penalty;
+    if (done && (t & kRwEndgame)) r += c.endgame_penalty;
     return r;
 }
 

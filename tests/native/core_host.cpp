@@ -88,6 +88,7 @@ double ch_reward(int reward_mode, int bonus_mode, int use_mask, const double* sc
     c.reward_mode = reward_mode; c.bonus_mode = bonus_mode; c.use_action_mask = use_mask;
     c.base_reward_scale = scal[0]; c.empty_tile_reward = scal[1]; c.merge_reward = scal[2]; c.bonus_scale = scal[3];
     c.step_reward = scal[4]; c.endgame_penalty = scal[5]; c.invalid_action_penalty = scal[6];
+    c.terms = reward_terms(c);
     MoveSummary s{};
     s.count = count; s.sum_e = sum_e; s.score = score; s.max_e = max_e;
     return env_reward(c, s, final_board, done != 0, invalid != 0, *max_tile_e);

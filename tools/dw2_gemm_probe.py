@@ -1,0 +1,37 @@
+"""TOOL: the layer-2 weight-gradient GEMM of the fused update (a1t [257, m] x d2t [256, m]^T, m = 2^20 columns) --
+hipBLASLt strided-batched split-K over P column blocks in both operand orders, and a single addmm -- timed on one
+MI355X (ms per chunk, TFLOP/s).  Picks the variant agent._fused_grad uses."""
+import json
+import time
+
+import torch
+
+dev = torch.device("cuda", 0)
+m = 1 << 20
+H1, H2 = 257, 256
+a1t = torch.randn(H1, m, device=dev)
+d2t = torch.randn(H2, m, device=dev)
+flop = 2.0 * H1 * H2 * m
+
+
+def bench(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+res = {}
+for P in (8, 16, 32, 64, 128, 256):
+    q = m // P
+    res[f"bmm_a1d2_P{P}"] = bench(lambda: torch.bmm(a1t.view(H1, P, q).transpose(0, 1),
+                                                    d2t.view(H2, P, q).permute(1, 2, 0)).sum(0))
+    res[f"bmm_d2a1_P{P}"] = bench(lambda: torch.bmm(d2t.view(H2, P, q).transpose(0, 1),
+                                                    a1t.view(H1, P, q).permute(1, 2, 0)).sum(0))
+res["addmm"] = bench(lambda: a1t @ d2t.t())
+for k, v in sorted(res.items(), key=lambda kv: kv[1]):
+    print(json.dumps({"variant": k, "ms": round(v, 3), "tflops": round(flop / v / 1e9, 1)}))
