@@ -453,6 +453,10 @@ class ReinforceAgent:
 
     # the per-row critic pass pays ~7 small launches per time row; worth it from this many samples per row
     critic_rows_min_avg = 16384
+    # trailing rows below this many samples run as one "tail" launch with their own V(s') forward: a row launch
+    # costs at least one 32-sample group's latency (~115 us on MI355X) however few samples it has, while the tail
+    # pays ~1.5x the flops per sample (the extra forward) at full occupancy -- break-even near 28k samples
+    critic_tail_row_max = 24576
 
     def _critic_by_rows(self, steps: "_Steps") -> bool:
         if not self.use_critic_rows or steps.N == 0:
@@ -467,7 +471,9 @@ class ReinforceAgent:
         returns V(s) of its row (value_out) -- which is the V(s') the previous row's TD targets r + gamma V(s') m need
         (src/reinforce_agent.py:423-443: X_next = the next step's obs).  The launches fill one a1^T / d2^T column
         buffer (column window per row) and accumulate their per-wave partials; the layer-2 GEMM runs once per full
-        buffer.  Saves the ~141 kflop / sample V(s') forward of the chunked path."""
+        buffer.  Saves the ~141 kflop / sample V(s') forward of the chunked path.  The trailing short rows (fewer
+        than critic_tail_row_max samples each -- episodes have ended) run first as one launch with their own V(s')
+        forward, which then hands V(s) of its first row to the per-row chain."""
         c = self.agent_config
         loss = {"mse": 0, "huber": 1}[c.critic_loss_type]
         h1, h2, act = spec
@@ -487,9 +493,14 @@ class ReinforceAgent:
             starts[t] = starts[t - 1] + counts[t - 1]
         blk = 2048                                                         # 64 split-K blocks x 32 columns
         ld = -(-max(self.grad_chunk_steps, max(counts) + 32) // blk) * blk
+        # the tail: trailing rows t_tail.. with fewer than critic_tail_row_max samples each, at most ld - 32 in all
+        t_tail, tail_m = len(counts), 0
+        while t_tail > 0 and counts[t_tail - 1] < self.critic_tail_row_max and tail_m + counts[t_tail - 1] <= ld - 32:
+            t_tail -= 1
+            tail_m += counts[t_tail]
         a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
         d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
-        vout = torch.empty(max(counts), dtype=torch.float32, device=self.device)
+        vout = torch.empty(max(max(counts), tail_m), dtype=torch.float32, device=self.device)
         gamma = float(c.gamma)
 
         def flush(used: int) -> None:
@@ -506,10 +517,42 @@ class ReinforceAgent:
             big += torch.bmm(a1t[:, :m].view(H1p + 1, P, q).transpose(0, 1),
                              d2t[:, :m].view(H2p, P, q).permute(1, 2, 0)).sum(0)
 
+        def grad_launch(s0: int, cnt: int, tgt: torch.Tensor, k: int) -> None:
+            nonlocal col
+            b = flat[steps.vidx[s0:s0 + cnt]].contiguous()
+            if k:
+                b = self._symmetry_boards(b, k)
+            ncols = -(-cnt // 32) * 32
+            if col + ncols > ld:
+                flush(col)
+                col = 0
+            L.check(self._lib.g2048_critic_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, loss,
+                                                float(c.huber_delta), L.ptr(b), L.ptr(tgt), L.ptr(step_w[s0:s0 + cnt]),
+                                                L.ptr(deltas[k, s0:s0 + cnt]), L.ptr(vout), cnt, ld, col, ncols,
+                                                L.ptr(a1t), L.ptr(d2t), L.ptr(part), 1, waves, self._stream))
+            col += ncols
+
         col = 0
         for k in range(K):
             vb = [torch.zeros(n, dtype=torch.float32, device=self.device) for _ in range(2)]
-            for t in range(len(counts) - 1, -1, -1):
+            if tail_m:
+                # the tail rows in one launch: V(s') by the fused forward (the successor is the same lane's next
+                # row, flat index + n), then V(s) of row t_tail hands over to the per-row chain below
+                s0 = starts[t_tail]
+                fi, hn = steps.vidx[s0:s0 + tail_m], steps.has_next[s0:s0 + tail_m]
+                bn = flat[torch.where(hn, fi + n, fi)].contiguous()
+                if k:
+                    bn = self._symmetry_boards(bn, k)
+                lg = torch.empty(tail_m, 4, dtype=torch.float32, device=self.device)
+                dummy = torch.empty(tail_m, dtype=torch.uint8, device=self.device)
+                L.check(self._lib.g2048_policy(L.ptr(packed), h1, h2, act, L.ptr(bn), None, None, obs_code, scale, 0,
+                                               1, L.RNG_PCG64, None, None, None, 0, None, None, L.ptr(lg),
+                                               L.ptr(dummy), tail_m, self._stream))
+                tgt = (steps.rewards[s0:s0 + tail_m] + (gamma * lg[:, 0]) * hn.to(torch.float32)).contiguous()
+                grad_launch(s0, tail_m, tgt, k)
+                if t_tail > 0:
+                    vb[t_tail & 1].index_copy_(0, steps.lane[s0:s0 + counts[t_tail]], vout[:counts[t_tail]])
+            for t in range(t_tail - 1, -1, -1):
                 cnt = counts[t]
                 if cnt == 0:
                     continue
@@ -518,20 +561,8 @@ class ReinforceAgent:
                 hn = steps.has_next[s0:s0 + cnt]
                 vn = vb[(t + 1) & 1].index_select(0, lanes)
                 tgt = (steps.rewards[s0:s0 + cnt] + (gamma * vn) * hn.to(torch.float32)).contiguous()
-                b = flat[steps.vidx[s0:s0 + cnt]].contiguous()
-                if k:
-                    b = self._symmetry_boards(b, k)
-                ncols = -(-cnt // 32) * 32
-                if col + ncols > ld:
-                    flush(col)
-                    col = 0
-                L.check(self._lib.g2048_critic_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, loss,
-                                                    float(c.huber_delta), L.ptr(b), L.ptr(tgt),
-                                                    L.ptr(step_w[s0:s0 + cnt]), L.ptr(deltas[k, s0:s0 + cnt]),
-                                                    L.ptr(vout), cnt, ld, col, ncols, L.ptr(a1t), L.ptr(d2t),
-                                                    L.ptr(part), 1, waves, self._stream))
+                grad_launch(s0, cnt, tgt, k)
                 vb[t & 1].index_copy_(0, lanes, vout[:cnt])
-                col += ncols
         flush(col)
         small = part.sum(0, dtype=torch.float64).to(torch.float32)
         big = big.to(torch.float32)

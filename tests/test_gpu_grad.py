@@ -172,14 +172,16 @@ def test_fused_critic_grad_ragged_chunks(chunk, act):
             assert _rel(a, b) < tol, (which, i, _rel(a, b))
 
 
-@pytest.mark.parametrize("aug", [False, True])
+@pytest.mark.parametrize("aug,tail", [(False, 0), (True, 0), (False, 64), (True, 100000)])
 @pytest.mark.parametrize("act", ["Sigmoid", "ReLU"])
-def test_fused_critic_rows_mode(act, aug):
+def test_fused_critic_rows_mode(act, aug, tail):
     """The per-time-row critic pass (ReinforceAgent._critic_grad_rows: rows last-first, each launch's V(s) serving as
     the previous row's V(s'), one column buffer, accumulated partials) forced on a small batch -- hundreds of
     rows, most of them ragged, a column-buffer flush forced by a small chunk -- against the torch backprop: critic
-    and actor gradients and the TD errors (through the actor's advantages).  Sigmoid 1e-5; ReLU 5e-5 (fp32 ReLU
-    derivative flips, as in test_fused_critic_grad_ragged_chunks)."""
+    and actor gradients and the TD errors (through the actor's advantages).  `tail`: rows below that many samples
+    run as the one tail launch with its own V(s') forward (0: none; 64: the later rows, handing over to the chain;
+    100000: all rows, capped by the column buffer).  Sigmoid 1e-5; ReLU 5e-5 (fp32 ReLU derivative flips, as in
+    test_fused_critic_grad_ragged_chunks)."""
     acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.97, use_critic=True, critic_loss_type="huber",
                 huber_delta=0.5, augmentation=aug)
     grads = {}
@@ -188,6 +190,7 @@ def test_fused_critic_rows_mode(act, aug):
         ag = _agent((64, 96), act, obs_mode="log2", **acfg)
         ag.use_fused_grad = mode == "rows"
         ag.critic_rows_min_avg = 0
+        ag.critic_tail_row_max = tail
         ag.grad_chunk_steps = 4096
         if batch is None:
             batch = ag.rollout_batch(list(range(100, 100 + 160)), list(range(900, 900 + 160)))
