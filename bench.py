@@ -49,9 +49,9 @@ SURVEY_RNG_BYTES = {"pcg64": 88, "philox": 30}
 SURVEY_OBS_BYTES = {"none": 0, "raw": 64, "log2": 64, "onehot": 1092}
 # LAYOUT bytes: what this build's structure-of-arrays lane layout actually moves per board-step (reads / writes):
 #   board 8/8, action 1/-, lane state word (step count, max tile, active, PCG64 buffer flag) 4/4, reward -/4,
-#   flags -/1, mask -/4;  PCG64: rng_state 16/16, rng_inc 16/-, rng_uint 4/4;  Philox: lane seed 8/-
-#   obs: log2/raw -/64, onehot -/1088
-CORE_R, CORE_W = 8 + 1 + 4, 8 + 4 + 4 + 1 + 4
+#   flags -/1, action mask -/1 (packed: g2048_step_out.mask_bits);  PCG64: rng_state 16/16, rng_inc 16/-,
+#   rng_uint 4/4;  Philox: lane seed 8/-;  obs: log2/raw -/64, onehot -/1088
+CORE_R, CORE_W = 8 + 1 + 4, 8 + 4 + 4 + 1 + 1
 RNG_BYTES = {"pcg64": (36, 20), "philox": (8, 0)}
 OBS_BYTES = {"none": 0, "raw": 64, "log2": 64, "onehot": 1088}
 
@@ -114,7 +114,8 @@ def make_env(torch, args, B, lane_offset, device):
     cfg = Game2048EnvConfig(obs_mode="log2" if args.obs == "none" else args.obs, obs_log2_scale=0.0625,
                             reward_mode="log2", base_reward_scale=0.5, max_steps=1024)
     env = VecGame2048Env(B, cfg, device=device, rng=args.rng, auto_reset=not args.no_auto_reset,
-                         reset_stride=B * max(args.gpus, 1), lane_offset=lane_offset, track_score=False)
+                         reset_stride=B * max(args.gpus, 1), lane_offset=lane_offset, track_score=False,
+                         packed_mask=True)
     if args.obs == "none":
         env._out.obs = None
     # per-lane episode seeds (PCG64: default_rng(seed) streams) via g2048_reset, then the random-state boards
@@ -486,7 +487,7 @@ def main():
         "warmup": W, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
         "config": {"workload": f"g2048_step over {B:,} random-state boards per GPU (configs[2] batch): "
-                               f"slide/merge + {args.rng} spawn + fp64 reward + done/trunc + auto-reset + mask + "
+                               f"slide/merge + {args.rng} spawn + fp64 reward + done/trunc + auto-reset + action mask (packed) + "
                                f"{args.obs} obs, uniform random actions incl. invalid",
                    "boards_per_gpu": B, "global_boards": B * world, "rng": args.rng, "obs": args.obs,
                    "parallelism": f"dp{world} (board shards, no data-path collective)"},

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 7
+#define G2048_ABI_VERSION 8
 
 /* status codes */
 #define G2048_OK 0
@@ -113,6 +113,8 @@ typedef struct g2048_step_out {
     double* reward64;      /* [n] the same reward in fp64 -- the Python float src/env.py:261 returns (may be NULL) */
     uint32_t* score_add;   /* [n] sum of this step's merged tiles: Game2048.score's increment (src/game2048.py:54);
                               the caller keeps the running score when it needs one (may be NULL) */
+    uint8_t* mask_bits;    /* [n] the same action mask packed: bit a set = action a changes the board (may be NULL;
+                              1 B per board-step instead of the 4 of `mask`) */
 } g2048_step_out;
 
 /* ---------------------------------------------------------------------------------------------------- */

@@ -20,7 +20,7 @@ LIB_PATH = SHIPPED_LIB
 SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
 SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # include/g2048.h constants
 OBS_NONE, OBS_RAW, OBS_LOG2, OBS_ONEHOT = -1, 0, 1, 2
@@ -63,7 +63,7 @@ class Lanes(ctypes.Structure):
 
 class StepOut(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in ("reward", "flags", "mask", "obs", "merged", "prev_board",
-                                                         "reward64", "score_add")]
+                                                         "reward64", "score_add", "mask_bits")]
 
 
 _lib = None

@@ -277,6 +277,7 @@ __device__ inline void reset_lane(const StepArgs& a, uint32_t i, uint64_t prev_s
     st(L.state, i, fresh_state(g));
     if constexpr (RNG == G2048_RNG_PCG64) store_pcg(L, i, g, true);
     if (a.out.mask) st(reinterpret_cast<uint32_t*>(a.out.mask), i, mask_word(action_mask(b)));
+    if (a.out.mask_bits) st(a.out.mask_bits, i, (uint8_t)action_mask(b));
     if constexpr (OBS != G2048_OBS_NONE)
         if (a.out.obs) write_obs_lane<OBS>(a.out.obs, i, b, a.obs_scale);
 }
@@ -302,11 +303,12 @@ __device__ inline void load_lane(const StepArgs& a, uint32_t i, LaneIn& x) {
 // written by the wave; reset = the episode ended and an auto-reset is pending for this lane.
 // XO (optional outputs, chosen by the launcher): 0 = none of prev_board / reward64 / score_add / merged (the
 // rollout and bench path: no null-pointer tests in the loop, whose uniform conditions the compiler otherwise keeps
-// as spilled 64-bit lane masks), 1 = any of the first three, 2 = the merged list too.
+// as spilled 64-bit lane masks), 1 = any of the first three, 2 = the merged list too; 3 = as 0 with the action
+// mask written packed (mask_bits) instead of as int8[4].
 template <int RNG, int XO>
 __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, const LineFn& lut,
                                      const CodeFn& code, bool& wobs, bool& reset, uint32_t& mbits) {
-    constexpr bool LIST = XO == 2, EXTRA = XO >= 1;
+    constexpr bool LIST = XO == 2, EXTRA = XO == 1 || XO == 2;
     const g2048_lanes& L = a.L;
     const uint64_t b = x.b;
     if (EXTRA && a.out.prev_board) st(a.out.prev_board, i, b);
@@ -384,7 +386,12 @@ __device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, 
         }
         pending |= 1ull << k;
     }
-    if (wobs && a.out.mask) st(reinterpret_cast<uint32_t*>(a.out.mask), i, mask_word(mbits));
+    if constexpr (XO == 3) {
+        if (wobs) st(a.out.mask_bits, i, (uint8_t)mbits);
+    } else {
+        if (wobs && a.out.mask) st(reinterpret_cast<uint32_t*>(a.out.mask), i, mask_word(mbits));
+        if (wobs && a.out.mask_bits) st(a.out.mask_bits, i, (uint8_t)mbits);
+    }
     if constexpr (OBS != G2048_OBS_NONE) {
         const uint64_t wm = __ballot(wobs);
         if (G2048_DIAG && (a.diag & 16)) return;
@@ -763,7 +770,8 @@ constexpr int kStepU = 1;
 
 template <int OBS, int RNG, bool LDS, int U>
 void launch_step3(const StepArgs& a, int grid, int xo, hipStream_t s) {
-    if (xo == 2) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 2, U>), dim3(grid), dim3(kBlock), 0, s, a);
+    if (xo == 3) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 3, U>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (xo == 2) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 2, U>), dim3(grid), dim3(kBlock), 0, s, a);
     else if (xo == 1) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 1, U>), dim3(grid), dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 0, U>), dim3(grid), dim3(kBlock), 0, s, a);
 }
@@ -778,7 +786,8 @@ void launch_step_u(const StepArgs& a, int cus, hipStream_t s) {
     int grid = grid_for((a.n + kU - 1) / kU, kBlock, lds ? cus : cus * 2);
     if (grid < min_blocks) grid = (int)min_blocks;
     if (G2048_DIAG && (a.diag & 8)) grid = grid_for(a.n, kBlock, 1 << 30);
-    const int xo = a.out.merged ? 2 : (a.out.prev_board || a.out.reward64 || a.out.score_add) ? 1 : 0;
+    int xo = a.out.merged ? 2 : (a.out.prev_board || a.out.reward64 || a.out.score_add) ? 1 : 0;
+    if (xo == 0 && a.out.mask_bits && !a.out.mask) xo = 3;
     if (lds) launch_step3<OBS, RNG, true, kU>(a, grid, xo, s);
     else launch_step3<OBS, RNG, false, kU>(a, grid, xo, s);
 }
@@ -936,6 +945,7 @@ int g2048_step(const g2048_lanes* lanes, const uint8_t* actions, const g2048_env
         if (a.out.prev_board) a.out.prev_board += off;
         if (a.out.reward64) a.out.reward64 += off;
         if (a.out.score_add) a.out.score_add += off;
+        if (a.out.mask_bits) a.out.mask_bits += off;
         a.rc = reward_cfg(*cfg);
         a.obs_scale = cfg->obs_log2_scale;
         a.auto_reset = auto_reset;

@@ -77,12 +77,14 @@ class VecGame2048Env:
     per step); off for pure throughput runs.
     Lane state lives in one uint32 word per lane (include/g2048.h G2048_LS_*): ``step_count``, ``max_tile``,
     ``status`` and ``active`` are views computed from it.
+    packed_mask: the steps write the action mask as one byte per lane (``mask_bits``, bit a = action a) instead
+    of int8[4] -- 3 B less per board-step; ``obs["action_mask"]`` is then unpacked from it on access.
     """
 
     def __init__(self, num_envs: int, config: Game2048EnvConfig | None = None, device=None, rng: str = "pcg64",
                  auto_reset: bool = False, reset_stride: int | None = None, philox_key: int = 0x2048,
                  lane_offset: int = 0, record_merged: bool = False, record_prev_board: bool = False,
-                 record_reward64: bool = False, track_score: bool = True):
+                 record_reward64: bool = False, track_score: bool = True, packed_mask: bool = False):
         if num_envs <= 0:
             raise ValueError("num_envs must be positive")
         self.config = config or Game2048EnvConfig()
@@ -114,23 +116,36 @@ class VecGame2048Env:
         # the fp64 reward (the Python float src/env.py:261 returns); off by default: +8 B per board-step
         self.reward64 = z(torch.float64, n) if record_reward64 else None
         self.flags = z(torch.uint8, n)
-        self.mask = z(torch.int8, n, 4)
+        self.mask = z(torch.int8, n, 4)                  # written by reset (and by steps unless packed_mask)
+        self.mask_bits = z(torch.uint8, n) if packed_mask else None
         self.obs_width = obs_width(self.config.obs_mode)
         self.obs = z(torch.float32, n, self.obs_width)
         self.merged = z(torch.int32, n) if record_merged else None
         self.prev_board = z(torch.int64, n) if record_prev_board else None
         self._lanes = L.Lanes(*[L.ptr(t) for t in (self.board, self.state, self.seed, self.rng_state, self.rng_inc,
                                                    self.rng_uint)])
-        self._out = L.StepOut(L.ptr(self.reward), L.ptr(self.flags), L.ptr(self.mask), L.ptr(self.obs),
-                              L.ptr(self.merged), L.ptr(self.prev_board), L.ptr(self.reward64), L.ptr(self._score_add))
+        self._out = L.StepOut(L.ptr(self.reward), L.ptr(self.flags), self._mask_ptr(), L.ptr(self.obs),
+                              L.ptr(self.merged), L.ptr(self.prev_board), L.ptr(self.reward64), L.ptr(self._score_add),
+                              L.ptr(self.mask_bits))
         self._lib = L.lib()
         self._stream = L.stream_handle(self.device)
 
     # ------------------------------------------------------------------------------------------------------
+    def _mask_ptr(self):
+        return None if self.mask_bits is not None else L.ptr(self.mask)
+
+    @property
+    def action_mask(self) -> torch.Tensor:
+        """int8 [n, 4]: the action mask of every lane's current board."""
+        if self.mask_bits is None:
+            return self.mask
+        bits = torch.tensor([1, 2, 4, 8], dtype=torch.uint8, device=self.device)
+        return ((self.mask_bits.unsqueeze(1) & bits) != 0).to(torch.int8)
+
     def _obs_view(self):
         board = self.obs.view(self.n, 4, 4, 17) if self.obs_width == 272 else self.obs.view(self.n, 4, 4)
         if self.config.use_action_mask:
-            return {"board": board, "action_mask": self.mask}
+            return {"board": board, "action_mask": self.action_mask}
         return board
 
     def reset(self, *, seed=None, options=None, mask: torch.Tensor | None = None):
@@ -149,6 +164,9 @@ class VecGame2048Env:
                 self.score.zero_()
             else:
                 self.score.masked_fill_(m != 0, 0)
+        if self.mask_bits is not None:   # reset writes the int8[4] form; keep the packed one current
+            w = torch.tensor([1, 2, 4, 8], dtype=torch.int32, device=self.device)
+            self.mask_bits.copy_(((self.mask != 0).to(torch.int32) * w).sum(1).to(torch.uint8))
         return self._obs_view(), {"score": self.score, "board": self.board}
 
     def step_into(self, actions: torch.Tensor, reward: torch.Tensor | None = None, flags: torch.Tensor | None = None,
@@ -162,10 +180,11 @@ class VecGame2048Env:
         out = self._out
         if reward is not None or flags is not None or prev_board is not None or not write_obs or reward64 is not None:
             out = L.StepOut(L.ptr(reward if reward is not None else self.reward),
-                            L.ptr(flags if flags is not None else self.flags), L.ptr(self.mask),
+                            L.ptr(flags if flags is not None else self.flags), self._mask_ptr(),
                             L.ptr(self.obs) if write_obs else None,
                             L.ptr(self.merged), L.ptr(prev_board if prev_board is not None else self.prev_board),
-                            L.ptr(reward64 if reward64 is not None else self.reward64), L.ptr(self._score_add))
+                            L.ptr(reward64 if reward64 is not None else self.reward64), L.ptr(self._score_add),
+                            L.ptr(self.mask_bits))
         if torch.cuda.current_device() != self.device.index:
             with torch.cuda.device(self.device):
                 return self.step_into(actions, reward, flags, prev_board, write_obs, reward64)

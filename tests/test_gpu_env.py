@@ -409,3 +409,40 @@ def test_philox_mode_distribution():
             assert ((mv >> (4 * cell)) & 15) == 0
         else:
             assert diff == 0
+
+
+@pytest.mark.parametrize("n", [64, 200_000])
+@pytest.mark.parametrize("extra", [None, "reward64", "both_masks"])
+def test_packed_mask_matches_int8_mask(n, extra):
+    """g2048_step_out.mask_bits (one byte per lane, bit a = action a) carries exactly the int8[4] mask, through
+    the packed-only kernel variant (XO 3), the variant with optional outputs (reward64) and with both mask forms
+    requested in one launch; boards / rewards / flags equal the unpacked env's, auto-resets included (their mask is
+    written by the deferred reset pass)."""
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+    from rl2048_amd import _lib as L
+
+    cfg = Game2048EnvConfig(obs_mode="log2", max_steps=40)
+    rec64 = extra == "reward64"
+    envs = [VecGame2048Env(n, cfg, device=DEV, auto_reset=True, record_reward64=rec64, packed_mask=p)
+            for p in (False, True)]
+    for e in envs:
+        e.reset(seed=11)
+    if extra == "both_masks":
+        e = envs[1]
+        e._out = L.StepOut(L.ptr(e.reward), L.ptr(e.flags), L.ptr(e.mask), L.ptr(e.obs), None, None, None, None,
+                           L.ptr(e.mask_bits))
+    assert torch.equal(envs[1].action_mask, envs[0].mask)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    resets = 0
+    for t in range(100):
+        a = torch.randint(0, 4, (n,), device=DEV, dtype=torch.uint8, generator=g)
+        for e in envs:
+            e.step_into(a)
+        assert torch.equal(envs[0].board, envs[1].board) and torch.equal(envs[0].flags, envs[1].flags)
+        assert torch.equal(envs[0].reward, envs[1].reward)
+        assert torch.equal(envs[1].action_mask, envs[0].mask), t
+        if extra == "both_masks":
+            assert torch.equal(envs[1].mask, envs[0].mask)
+        resets += int(((envs[0].flags & L.F_RESET) != 0).sum())
+    assert resets > 0

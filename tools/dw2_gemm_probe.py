@@ -26,6 +26,19 @@ def bench(fn, reps=20):
 
 
 res = {}
+import sys
+if "--rows" in sys.argv:      # M = 256 (no ones row) against 257, and the db2 row as a separate column sum
+    a1s = a1t[:256]
+    for P in (64, 128, 256):
+        q = m // P
+        res[f"bmm_M257_P{P}"] = bench(lambda: torch.bmm(a1t.view(H1, P, q).transpose(0, 1),
+                                                        d2t.view(H2, P, q).permute(1, 2, 0)).sum(0))
+        res[f"bmm_M256_P{P}"] = bench(lambda: torch.bmm(a1s.reshape(256, P, q).transpose(0, 1),
+                                                        d2t.view(H2, P, q).permute(1, 2, 0)).sum(0))
+    res["d2_rowsum"] = bench(lambda: d2t.sum(1))
+    for k, v in sorted(res.items(), key=lambda kv: kv[1]):
+        print(json.dumps({"variant": k, "ms": round(v, 3)}))
+    sys.exit(0)
 for P in (8, 16, 32, 64, 128, 256):
     q = m // P
     res[f"bmm_a1d2_P{P}"] = bench(lambda: torch.bmm(a1t.view(H1, P, q).transpose(0, 1),
