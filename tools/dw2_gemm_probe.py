@@ -2,6 +2,7 @@
 hipBLASLt strided-batched split-K over P column blocks in both operand orders, and a single addmm -- timed on one
 MI355X (ms per chunk, TFLOP/s).  Picks the variant agent._fused_grad uses."""
 import json
+import sys
 import time
 
 import torch
@@ -26,7 +27,18 @@ def bench(fn, reps=20):
 
 
 res = {}
-import sys
+if "--sample-major" in sys.argv:   # a1 / d2 stored [sample][unit] (the kernel's column stores as 16-B runs)
+    a1s = torch.randn(m, H1, device=dev)
+    d2s = torch.randn(m, H2, device=dev)
+    for P in (64, 128, 256):
+        q = m // P
+        res[f"unit_major_P{P}"] = bench(lambda: torch.bmm(a1t.view(H1, P, q).transpose(0, 1),
+                                                          d2t.view(H2, P, q).permute(1, 2, 0)).sum(0))
+        res[f"sample_major_P{P}"] = bench(lambda: torch.bmm(a1s.view(P, q, H1).transpose(1, 2),
+                                                            d2s.view(P, q, H2)).sum(0))
+    for k, v in sorted(res.items(), key=lambda kv: kv[1]):
+        print(json.dumps({"variant": k, "ms": round(v, 3), "tflops": round(flop / v / 1e9, 1)}))
+    sys.exit(0)
 if "--rows" in sys.argv:      # M = 256 (no ones row) against 257, and the db2 row as a separate column sum
     a1s = a1t[:256]
     for P in (64, 128, 256):
