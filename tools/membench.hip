@@ -69,6 +69,18 @@ __global__ void __launch_bounds__(256) stream_copy(const float4* __restrict__ sr
         dst[i] = src[i];
 }
 
+// write-only stream (the one-hot obs bound): float4 stores, plain or non-temporal
+template <bool NT>
+__global__ void __launch_bounds__(256) stream_fill(float4* __restrict__ dst, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4 v = {0.f, 1.f, 0.f, (float)(i & 7)};
+        f4* p = reinterpret_cast<f4*>(dst) + i;
+        if constexpr (NT) __builtin_nontemporal_store(v, p);
+        else *p = v;
+    }
+}
+
 template <int W>
 void launch_twin(Bufs* a, int coop, int grid, int block, int lds, void* stream) {
     if (coop) hipLaunchKernelGGL((twin<true, W>), dim3(grid), dim3(block), lds, (hipStream_t)stream, *a);
@@ -88,5 +100,11 @@ extern "C" int mb_twin(Bufs* a, int coop, int grid, int block, int work, int lds
 
 extern "C" int mb_copy(const void* src, void* dst, size_t n16, int grid, void* stream) {
     hipLaunchKernelGGL(stream_copy, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float4*)src, (float4*)dst, n16);
+    return (int)hipGetLastError();
+}
+
+extern "C" int mb_fill(void* dst, size_t n16, int grid, int nt, void* stream) {
+    if (nt) hipLaunchKernelGGL(stream_fill<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (float4*)dst, n16);
+    else hipLaunchKernelGGL(stream_fill<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (float4*)dst, n16);
     return (int)hipGetLastError();
 }

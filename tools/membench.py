@@ -60,6 +60,14 @@ def main():
                                       ctypes.c_size_t(nb // 16), 4096, ctypes.c_void_p(stream)))
         out.append(dict(variant=f"float4 copy {mb} MiB", us=us, GBs=2 * nb / us / 1e3))
         del src, dst
+    nb = 1088 * n                                     # the one-hot obs of one 1M-board step
+    dst = z(torch.uint8, nb)
+    for nt in (0, 1):
+        for grid in (1024, 4096, 16384):
+            us = timeit(lambda: L.mb_fill(ctypes.c_void_p(dst.data_ptr()), ctypes.c_size_t(nb // 16), grid, nt,
+                                          ctypes.c_void_p(stream)))
+            out.append(dict(variant=f"float4 fill {nb >> 20} MiB nt={nt} grid={grid}", us=us, GBs=nb / us / 1e3))
+    del dst
     for o in out:
         print(json.dumps(o), flush=True)
 
