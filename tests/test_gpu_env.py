@@ -1,7 +1,6 @@
 """GPU parity of the env hot path (libg2048.so through its C ABI) against the reference's golden fixtures and
 the CPU oracle.  Bit-exact for boards / flags / masks / obs / merged lists / spawn streams; rewards equal the
 oracle's fp64 reward rounded once to fp32 (the kernel computes in fp64 and stores fp32)."""
-import ctypes
 import os
 
 import numpy as np

@@ -7,7 +7,6 @@
   the same RNG state (bit-exact), for PCG64 / Philox / greedy, with and without the action mask;
 * inactive lanes (lane state word without G2048_LS_ACTIVE) are left untouched; n not a multiple of the 32-board group.
 """
-import ctypes
 
 import numpy as np
 import pytest
