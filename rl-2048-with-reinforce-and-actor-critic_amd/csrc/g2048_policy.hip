@@ -366,35 +366,48 @@ struct RollSmem {
     uint32_t claim[32];
 };
 
-// One workgroup (one per CU) = 32 episode slots; its 4 waves split every step's MLP: wave w computes the layer-1
-// tiles and the layer-2 output tiles congruent to w mod 4 (a quarter of the MFMAs), exchanging the layer-1
+// One workgroup = 32 episode slots, TWO workgroups per CU; its 4 waves split every step's MLP: wave w computes the
+// layer-1 tiles and the layer-2 output tiles congruent to w mod 4 (a quarter of the MFMAs), exchanging the layer-1
 // activations and the partial logits through LDS (two barriers per step), so a step takes about a quarter of the
-// one-wave latency.  Each wave's quarter of the layer-2 weights (<= 2 output tiles x NT1 x 16 fragments = 256
-// floats per lane) is loaded ONCE into registers (the accumulator file: MFMA A operands may be AGPRs), so the
-// steady state reads no weights from memory at all.  Every wave then holds the same logits and runs the same
-// choice and env step on the same slot state (so no per-slot state is broadcast); wave 0 writes the trajectory
-// and claims episodes for the workgroup.
+// one-wave latency.  Each wave streams its quarter of the layer-2 weight fragments from L2 every step (the next k-tile
+// in flight; the first issued before layer 1), which leaves the registers for a second workgroup per CU: the
+// two workgroups' steps interleave on every SIMD, so one's MFMAs run while the other's env step, layer 1 and
+// barriers do (one workgroup per CU with the weights resident in registers left the MFMAs idle for those phases).
+// Every wave holds the same logits and runs the same choice and env step on the same slot state (so no per-slot
+// state is broadcast); wave 0 writes the trajectory and claims episodes for the workgroup.
+constexpr int kRollBlocksPerCU = 2;
+
 template <int NT1, int NT2, int ACT, int OBS>
-__global__ void __launch_bounds__(kPolBlock, 1) rollout_kernel(RolloutArgs a) {
+__global__ void __launch_bounds__(kPolBlock, kRollBlocksPerCU) rollout_kernel(RolloutArgs a) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
     __shared__ RollSmem<NT1, NT2> S;
     S.net.load(a.net);
-    const float4* __restrict__ w2q = reinterpret_cast<const float4*>(a.net + NetSmem<NT1, NT2>::L.w2f) + lane;
     const GLine lut{reinterpret_cast<const uint16_t*>(a.tab)};
     const GCode code{a.tab + 2 * 65536};
+    // this wave's layer-2 fragment stream: output tiles o = w + 4 k2 (those < NT2), k-tiles tt; stream index
+    // i = k2 * NT1 + tt; the index past the end re-reads the first k-tile (unused)
+    constexpr int kOwn = (NT2 + 3) / 4;
+    // Loads through a buffer resource: this lane's voffset (lane * 16) plus a scalar k-tile offset -- 64-bit
+    // per-fragment addresses were hoisted out of the step loop (128 registers) and spilled.
+    const int ws = __builtin_amdgcn_readfirstlane(w);
+    const int nown = (NT2 - ws + 3) / 4;                  // own output tiles (0 when w >= NT2)
+    const int nkt = nown * NT1;
+    const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.net + NetSmem<NT1, NT2>::L.w2f), 0, NT2 * NT1 * 1024 * 4, 0x00020000);
+    const uint32_t fvo = (uint32_t)lane * 16u;
+    const auto frag = [&](int i, float4 f[4]) {
+        const int ii = i < nkt ? i : 0;
+        const int o = ws + 4 * (ii / NT1), tt = ii % NT1;
+        const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(((o < NT2 ? o : 0) * NT1 + tt) * 4096));
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rw2, (int)fvo, (int)(base + 1024u * q), 0);
+            f[q] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+        }
+    };
     // episode claims for the slots that need one (identical `need` in all waves): wave 0 takes them with one
     // atomic and publishes them; every wave must call this together (it contains barriers)
-    // this wave's layer-2 fragments, loaded once: output tiles o = w + 4 k2
-    constexpr int kOwn = (NT2 + 3) / 4;
-    float4 wf[kOwn][NT1][4];
-#pragma unroll
-    for (int k2 = 0; k2 < kOwn; k2++) {
-        const int o = w + 4 * k2 < NT2 ? w + 4 * k2 : 0;
-#pragma unroll
-        for (int tt = 0; tt < NT1; tt++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) wf[k2][tt][q] = w2q[((o * NT1 + tt) * 4 + q) * 64];
-    }
     const auto claim = [&](bool need, uint32_t cur) -> uint32_t {
         if (w == 0) {
             const uint64_t bal = __ballot(need && h == 0);
@@ -446,6 +459,8 @@ __global__ void __launch_bounds__(kPolBlock, 1) rollout_kernel(RolloutArgs a) {
     } while (0)
 #endif
     while (__ballot(ep < a.n)) {                         // block-uniform (all waves hold the same slot state)
+        float4 fa[4];                                     // layer-2 k-tile 0, in flight through layer 1
+        frag(0, fa);
         // ---- layer 1: this wave's tiles -> LDS
         float x[8];
 #pragma unroll
@@ -468,24 +483,31 @@ __global__ void __launch_bounds__(kPolBlock, 1) rollout_kernel(RolloutArgs a) {
         }
         __syncthreads();
         ROLL_PH(0);
-        // ---- layer 2: this wave's output tiles (B from LDS, A resident in registers), folded into partial logits
+        // ---- layer 2: this wave's output tiles (B from LDS, A streamed), folded into partial logits
         float lgp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int k2 = 0; k2 < kOwn; k2++) {
-            const int o = w + 4 * k2;
+            const int o = ws + 4 * k2;
             if (o >= NT2) continue;                         // wave-uniform
+            // a compiler memory barrier: otherwise the layer-1 activations' LDS reads (the same for every own
+            // tile) are kept from the first tile for the next, 128 registers, which spill at 2 waves per SIMD
+            asm volatile("" ::: "memory");
             floatx16 acc = {};
 #pragma unroll
             for (int tt = 0; tt < NT1; tt++) {
+                asm volatile("" ::: "memory");              // (the same per k-tile: its 4 LDS reads stay here)
+                float4 fb[4];                               // k-tile i + 1 of the stream
+                frag(k2 * NT1 + tt + 1, fb);
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const float4 hb = S.h1f[tt][q][lane];
-                    const float4 fa = wf[k2][tt][q];
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.x, hb.x, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.y, hb.y, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.z, hb.z, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.w, hb.w, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, hb.x, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, hb.y, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, hb.z, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, hb.w, acc, 0, 0, 0);
                 }
+#pragma unroll
+                for (int q = 0; q < 4; q++) fa[q] = fb[q];
             }
             const float4* bb = reinterpret_cast<const float4*>(S.net.b2p() + (o * 2 + h) * 16);
             const float4* w3 = reinterpret_cast<const float4*>(S.net.w3p() + (o * 2 + h) * 64);
@@ -1330,7 +1352,7 @@ int g2048_rollout(const float* packed, int h1, int h2, int activation, const g20
     a.cap = (uint32_t)cap;
     const int nt1 = tiles_for(h1), nt2 = tiles_for(h2);
     int64_t grid = (n + 31) / 32;                  // one workgroup per 32 episode slots
-    if (grid > cus) grid = cus;                    // persistent (one per CU); the slots refill from the queue
+    if (grid > kRollBlocksPerCU * cus) grid = kRollBlocksPerCU * cus;   // persistent; the slots refill from the queue
     hipStream_t s = (hipStream_t)stream;
     switch (nt1) {
         case 1: launch_roll_nt2<1>(a, nt2, activation, cfg->obs_mode, (int)grid, s); break;
