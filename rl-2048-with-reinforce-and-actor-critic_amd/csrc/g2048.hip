@@ -57,6 +57,11 @@ int fail(int code, const std::string& msg) {
 #define G2048_DIAG 0
 #endif
 
+// Step-kernel prefetch ring: 3 register buffers (loads two sweeps ahead) or 4 (three sweeps ahead).
+#ifndef G2048_STEP_DEPTH
+#define G2048_STEP_DEPTH 3
+#endif
+
 #if G2048_DIAG
 // per-workgroup phase timestamps of the last step launch (s_memrealtime, 100 MHz): entry, tables filled,
 // main loop done, reset list built, end
@@ -433,6 +438,11 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     uint32_t w0 = w_first, w1 = w_first + wstride;
     load_lane<RNG>(a, lane_at(w0), A);
     load_lane<RNG>(a, lane_at(w1), B);
+#if G2048_STEP_DEPTH == 4
+    LaneIn D;
+    uint32_t w2 = w1 + wstride;
+    load_lane<RNG>(a, lane_at(w2), C);
+#endif
     const uint8_t* tab = a.tab;
     if constexpr (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(a.tab);
@@ -455,6 +465,29 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     const CodeFn code{tab + 2 * kLines};
     uint64_t pending = 0, pseed = 0;
     uint32_t k = 0;
+#if G2048_STEP_DEPTH == 4
+    while (w0 < a.n) {                         // wave-uniform; loads three sweeps ahead
+        const uint32_t w3 = w2 + wstride;
+        load_lane<RNG>(a, lane_at(w3), D);
+        sweep<OBS, RNG, XO>(a, w0, lane, A, lut, code, pending, pseed, k);
+        if (w1 >= a.n) break;
+        const uint32_t w4 = w3 + wstride;
+        load_lane<RNG>(a, lane_at(w4), A);
+        sweep<OBS, RNG, XO>(a, w1, lane, B, lut, code, pending, pseed, k + 1);
+        if (w2 >= a.n) break;
+        const uint32_t w5 = w4 + wstride;
+        load_lane<RNG>(a, lane_at(w5), B);
+        sweep<OBS, RNG, XO>(a, w2, lane, C, lut, code, pending, pseed, k + 2);
+        if (w3 >= a.n) break;
+        const uint32_t w6 = w5 + wstride;
+        load_lane<RNG>(a, lane_at(w6), C);
+        sweep<OBS, RNG, XO>(a, w3, lane, D, lut, code, pending, pseed, k + 3);
+        w0 = w4;
+        w1 = w5;
+        w2 = w6;
+        k += 4;
+    }
+#else
     while (w0 < a.n) {                         // wave-uniform
         const uint32_t w2 = w1 + wstride;
         load_lane<RNG>(a, lane_at(w2), C);
@@ -471,6 +504,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
         w1 = w4;
         k += 3;
     }
+#endif
     if (G2048_DIAG && (a.diag & 2)) pending = 0;
     if constexpr (LDS) {
         uint32_t* cnt = reinterpret_cast<uint32_t*>(tab_lds);
