@@ -62,6 +62,12 @@ int fail(int code, const std::string& msg) {
 #define G2048_STEP_DEPTH 3
 #endif
 
+// Step-kernel move: 0 = the two LDS row tables (board_move_coded), 1 = table-free (board_move_alu: no LDS tables,
+// no table fill; the LDS then holds only the deferred-reset list).
+#ifndef G2048_STEP_ALU
+#define G2048_STEP_ALU 0
+#endif
+
 #if G2048_DIAG
 // per-workgroup phase timestamps of the last step launch (s_memrealtime, 100 MHz): entry, tables filled,
 // main loop done, reset list built, end
@@ -339,7 +345,11 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
         s = MoveSummary{0, 0, 0, 0, 0, 0};
         m = b ^ ((uint64_t)x.act << 60);
     } else {
+#if G2048_STEP_ALU
+        m = board_move_alu<LIST>(b, x.act, s);
+#else
         m = board_move_coded<LIST>(b, x.act, lut, code, s);
+#endif
     }
     const bool changed = m != b;
     if (changed && !(G2048_DIAG && (a.diag & 4))) {
@@ -405,8 +415,14 @@ __device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, 
 }
 
 // LDS reuse after the last sweep: the block's reset list (counter, lane indices, previous seeds)
-constexpr int kResetCap = (kTabBytes - 16) / 12;
-static_assert(16 + kResetCap * 4 + kResetCap * 8 <= kTabBytes, "reset list fits the table area");
+#if G2048_STEP_ALU
+constexpr int kStepLdsBytes = 24576;        // the reset list only
+#else
+constexpr int kStepLdsBytes = kTabBytes;    // the row tables, then (after the last sweep) the reset list
+#endif
+constexpr int kStepLdsVec = kStepLdsBytes / 16;
+constexpr int kResetCap = (kStepLdsBytes - 16) / 12;
+static_assert(16 + kResetCap * 4 + kResetCap * 8 <= kStepLdsBytes, "reset list fits the LDS area");
 static_assert(kTabVec % kBlock == 0, "table fill: whole chunks per thread");
 
 // Persistent over the board array, one board per lane per sweep (wave g of W takes the chunks of 64 boards
@@ -427,7 +443,7 @@ static_assert(kTabVec % kBlock == 0, "table fill: whole chunks per thread");
 template <int OBS, int RNG, bool LDS, int XO, int U>
 __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     static_assert(U == 1, "one board per lane per sweep");
-    __shared__ uint4 tab_lds[LDS ? kTabVec : 1];
+    __shared__ uint4 tab_lds[LDS ? kStepLdsVec : 1];
     const int lane = threadIdx.x & 63;
     const uint32_t w_first = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
     const uint32_t wstride = gridDim.x * kBlock;
@@ -446,7 +462,7 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     const uint8_t* tab = a.tab;
     if constexpr (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(a.tab);
-        if (!(G2048_DIAG && (a.diag & 1))) {
+        if (!G2048_STEP_ALU && !(G2048_DIAG && (a.diag & 1))) {
             constexpr uint32_t kChunks = kTabVec / kBlock;
             const uint32_t rot = blockIdx.x % kChunks;
 #pragma unroll

@@ -302,6 +302,73 @@ G2048_HD uint64_t board_move_coded(uint64_t b, uint32_t a, const Lut& lut, const
     return g;
 }
 
+// _row_move_left (src/game2048.py:120-137) of one line without a table: one left-to-right pass holding the pending
+// (not yet placed) tile, which either merges with the next equal tile or is placed at the write position.  Returns
+// the new line (a 15+15 merge saturates at 15); e0 / e1 = the merged exponents in position order (16 = saturated).
+G2048_HD uint32_t line_move_alu(uint32_t o, uint32_t& e0, uint32_t& e1) {
+    uint32_t out = 0u, sh = 0u, pend = o & 15u;
+    e0 = 0u;
+    e1 = 0u;
+#pragma unroll
+    for (int k = 1; k < 4; k++) {
+        const uint32_t v = bfe32(o, 4u * k, 4u);
+        const bool nz = v != 0u;
+        const bool mg = nz && v == pend;
+        const uint32_t emit = mg ? (v == 15u ? 15u : v + 1u) : (nz ? pend : 0u);
+        out |= emit << sh;
+        sh += emit != 0u ? 4u : 0u;
+        e1 = (mg && e0 != 0u) ? v + 1u : e1;
+        e0 = (mg && e0 == 0u) ? v + 1u : e0;
+        pend = mg ? 0u : (nz ? v : pend);
+    }
+    return out | (pend << sh);
+}
+
+// Game2048._move (src/game2048.py:158-165) with line_move_alu: the same result, summary and merged-list order as
+// board_move_coded, and no table (no LDS, no table fill).
+template <bool WANT_LIST>
+G2048_HD uint64_t board_move_alu(uint64_t b, uint32_t a, MoveSummary& s) {
+    const uint64_t mvert = 0ull - (uint64_t)((a == 0u) | (a == 2u));
+    const uint64_t mrev = 0ull - (uint64_t)((a == 1u) | (a == 2u));
+    const bool back = (a == 0u) | (a == 1u);
+    uint64_t f = b ^ ((b ^ transpose(b)) & mvert);
+    f ^= (f ^ reverse_rows(f)) & mrev;
+    uint32_t e0[4], e1[4];
+    uint64_t g = 0;
+    uint32_t sum_e = 0, score = 0, max_e = 0, count = 0, list = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t nw = line_move_alu((uint32_t)(f >> (16 * j)) & 0xFFFFu, e0[j], e1[j]);
+        g |= (uint64_t)nw << (16 * j);
+        score += ((1u << e0[j]) & ~1u) + ((1u << e1[j]) & ~1u);
+        sum_e += e0[j] + e1[j];
+        max_e = max_e > e0[j] ? max_e : e0[j];
+        max_e = max_e > e1[j] ? max_e : e1[j];
+    }
+    if (WANT_LIST) {
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            const uint32_t x0 = back ? e0[3 - jj] : e0[jj], x1 = back ? e1[3 - jj] : e1[jj];
+            const uint32_t n0 = x0 != 0u, n1 = x1 != 0u;
+            if (n0) list |= ((x0 - 1u) & 15u) << (4u * (count & 7u));
+            if (n1) list |= ((x1 - 1u) & 15u) << (4u * ((count + n0) & 7u));
+            count += n0 + n1;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) count += (e0[j] != 0u) + (e1[j] != 0u);
+    }
+    s.count = count;
+    s.sum_e = sum_e;
+    s.score = score;
+    s.max_e = max_e;
+    s.overflow = max_e >> 4;
+    s.list = list;
+    g ^= (g ^ reverse_rows(g)) & mrev;
+    g ^= (g ^ transpose(g)) & mvert;
+    return g;
+}
+
 // nz / equal-neighbour masks of a board, shared by is_done and action_mask
 struct BoardBits {
     uint64_t nz, z, eqh, eqv;

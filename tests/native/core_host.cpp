@@ -52,6 +52,41 @@ uint64_t ch_board_move_coded_nolist(uint64_t b, uint32_t a, uint32_t* list, uint
     *list = s.list; *count = s.count; *score = s.score; *sum_e = s.sum_e; *max_e = s.max_e; *overflow = s.overflow;
     return m;
 }
+uint64_t ch_board_move_alu(uint64_t b, uint32_t a, uint32_t* list, uint32_t* count, uint32_t* score,
+                           uint32_t* sum_e, uint32_t* max_e, uint32_t* overflow) {
+    MoveSummary s;
+    uint64_t m = board_move_alu<true>(b, a, s);
+    *list = s.list; *count = s.count; *score = s.score; *sum_e = s.sum_e; *max_e = s.max_e; *overflow = s.overflow;
+    return m;
+}
+// board_move_alu (list and no-list) against board_move_coded on every line value in every line slot of a board
+// (the other three lines random) under all four actions, plus `n` random boards: the number of mismatches
+int64_t ch_check_alu(int64_t n, uint64_t seed) {
+    ensure_lut();
+    int64_t bad = 0;
+    uint64_t x = seed | 1ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    auto same = [](const MoveSummary& p, const MoveSummary& q, bool list) {
+        return p.count == q.count && p.sum_e == q.sum_e && p.score == q.score && p.max_e == q.max_e &&
+               p.overflow == q.overflow && (!list || p.list == q.list);
+    };
+    auto check = [&](uint64_t b) {
+        for (uint32_t a = 0; a < 4; a++) {
+            MoveSummary s0, s1, s2;
+            const uint64_t m0 = board_move_coded<true>(b, a, HostLut{}, HostCode{}, s0);
+            const uint64_t m1 = board_move_alu<true>(b, a, s1);
+            const uint64_t m2 = board_move_alu<false>(b, a, s2);
+            if (m0 != m1 || m0 != m2 || !same(s0, s1, true) || !same(s0, s2, false)) bad++;
+        }
+    };
+    for (uint32_t r = 0; r < 65536u; r++)
+        for (int slot = 0; slot < 4; slot++) {
+            const uint64_t other = rnd() & ~(0xFFFFull << (16 * slot));
+            check(other | ((uint64_t)r << (16 * slot)));
+        }
+    for (int64_t i = 0; i < n; i++) check(rnd());
+    return bad;
+}
 uint32_t ch_bits_mask(uint64_t b) { return bits_mask(board_bits(b)); }
 int ch_bits_done(uint64_t b) { return bits_done(board_bits(b)) ? 1 : 0; }
 uint32_t ch_action_mask(uint64_t b) { return action_mask(b); }

@@ -37,6 +37,10 @@ def ch():
     L.ch_philox.argtypes = [u32p, u32p, u32p]
     L.ch_spawn_philox.restype = ctypes.c_uint64
     L.ch_spawn_philox.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
+    L.ch_board_move_alu.restype = ctypes.c_uint64
+    L.ch_board_move_alu.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [u32p] * 6
+    L.ch_check_alu.restype = ctypes.c_int64
+    L.ch_check_alu.argtypes = [ctypes.c_int64, ctypes.c_uint64]
     L.ch_bits_mask.restype = ctypes.c_uint32
     L.ch_bits_mask.argtypes = [ctypes.c_uint64]
     L.ch_bits_done.argtypes = [ctypes.c_uint64]
@@ -61,7 +65,8 @@ def ch():
 
 def _move(ch, b, a, coded=False):
     vals = [ctypes.c_uint32() for _ in range(6)]
-    fn = {False: ch.ch_board_move, True: ch.ch_board_move_coded, "nolist": ch.ch_board_move_coded_nolist}[coded]
+    fn = {False: ch.ch_board_move, True: ch.ch_board_move_coded, "nolist": ch.ch_board_move_coded_nolist,
+          "alu": ch.ch_board_move_alu}[coded]
     m = fn(b, a, *[ctypes.byref(v) for v in vals])
     lst, cnt, score, sum_e, max_e, ovf = [v.value for v in vals]
     if coded == "nolist":
@@ -77,7 +82,7 @@ def _rand_boards(rng, n, p_empty=0.375, hi=15):
     return [O.pack_exponents(x) for x in e]
 
 
-@pytest.mark.parametrize("coded", [False, True, "nolist"])
+@pytest.mark.parametrize("coded", [False, True, "nolist", "alu"])
 def test_board_move_vs_oracle(ch, coded):
     rng = np.random.default_rng(3)
     boards = _rand_boards(rng, 3000) + _rand_boards(rng, 2000, p_empty=0.0, hi=4) + _rand_boards(rng, 1000, 0.7)
@@ -97,6 +102,12 @@ def test_board_move_vs_oracle(ch, coded):
             if ok:
                 assert m == ob, (hex(b), a)
             assert (m != b) == ochanged
+
+
+def test_board_move_alu_equals_table_move(ch):
+    """The table-free move (line_move_alu) against the two-table move: every 16-bit line in every line slot under
+    all four actions (boards, merge summaries and merged lists equal), plus 200k random boards."""
+    assert ch.ch_check_alu(200_000, 0x2048) == 0
 
 
 def test_mask_done_vs_oracle(ch):
