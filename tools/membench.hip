@@ -69,6 +69,15 @@ __global__ void __launch_bounds__(256) stream_copy(const float4* __restrict__ sr
         dst[i] = src[i];
 }
 
+// read one float4, write two (the step kernel's 1:2 read:write byte mix): dst[2i], dst[2i+1] from src[i]
+__global__ void __launch_bounds__(256) stream_rw12(const float4* __restrict__ src, float4* __restrict__ dst, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const float4 v = src[i];
+        dst[i] = v;
+        dst[n + i] = make_float4(v.w, v.z, v.y, v.x);
+    }
+}
+
 // write-only stream (the one-hot obs bound): float4 stores, plain or non-temporal
 template <bool NT>
 __global__ void __launch_bounds__(256) stream_fill(float4* __restrict__ dst, size_t n) {
@@ -103,6 +112,10 @@ extern "C" int mb_copy(const void* src, void* dst, size_t n16, int grid, void* s
     return (int)hipGetLastError();
 }
 
+extern "C" int mb_rw12(const void* src, void* dst, size_t n16, int grid, void* stream) {
+    hipLaunchKernelGGL(stream_rw12, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float4*)src, (float4*)dst, n16);
+    return (int)hipGetLastError();
+}
 extern "C" int mb_fill(void* dst, size_t n16, int grid, int nt, void* stream) {
     if (nt) hipLaunchKernelGGL(stream_fill<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (float4*)dst, n16);
     else hipLaunchKernelGGL(stream_fill<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (float4*)dst, n16);

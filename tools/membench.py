@@ -49,6 +49,28 @@ def main():
         return s.elapsed_time(e) / reps * 1e3  # us
 
     out = []
+    if "--stream-sweep" in sys.argv:
+        # plain streams at the step kernel's traffic per launch (166.8 MB at 1M boards, x8 at 8M), back to back
+        # like the bench: a 1:1 copy and a 1:2 read:write stream (the step's byte mix), grid 4096 x 256
+        for boards in (1 << 20, 1 << 21, 1 << 22, 1 << 23):
+            total = 159 * boards
+            nb = (total // 2) & ~15
+            src, dst = z(torch.uint8, nb), z(torch.uint8, nb)
+            us = timeit(lambda: L.mb_copy(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                                          ctypes.c_size_t(nb // 16), 4096, ctypes.c_void_p(stream)))
+            out.append(dict(variant=f"float4 copy, {boards} boards' traffic ({2 * nb >> 20} MiB)", us=us,
+                            GBs=2 * nb / us / 1e3))
+            del src, dst
+            nr = (total // 3) & ~15
+            src, dst = z(torch.uint8, nr), z(torch.uint8, 2 * nr)
+            us = timeit(lambda: L.mb_rw12(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                                          ctypes.c_size_t(nr // 16), 4096, ctypes.c_void_p(stream)))
+            out.append(dict(variant=f"float4 read 1 : write 2, {boards} boards' traffic ({3 * nr >> 20} MiB)", us=us,
+                            GBs=3 * nr / us / 1e3))
+            del src, dst
+        for o in out:
+            print(json.dumps(o), flush=True)
+        return
     for work in (0, 16, 32, 64):
         for grid, block, lds in ((256, 1024, 160 * 1024), (256, 1024, 0), (1024, 1024, 0), (4096, 256, 0)):
             us = timeit(lambda: L.mb_twin(ctypes.byref(b), 1, grid, block, work, lds, ctypes.c_void_p(stream)))
