@@ -26,6 +26,13 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+// grad_kernel column stores: 0 = each phase stores its own columns (a1^T after layer 1, d2^T after d2); 1 = spread
+// over the MFMA loops that follow (the a1^T values as the layer-2 loop reads them, the d2^T values through the d1
+// loop), a few per k-tile, so the column writes drain under the MFMAs instead of stalling on the VMEM queue;
+// 2 = only the d2^T stores spread.
+#ifndef G2048_GRAD_SPREAD
+#define G2048_GRAD_SPREAD 2
+#endif
 #ifndef G2048_DIAG
 #define G2048_DIAG 0
 #endif
@@ -807,10 +814,12 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                     const float4 hv = make_float4(activate<ACT>(acc[4 * q + 0] + bv.x), activate<ACT>(acc[4 * q + 1] + bv.y),
                                                   activate<ACT>(acc[4 * q + 2] + bv.z), activate<ACT>(acc[4 * q + 3] + bv.w));
                     h1f[(t * 4 + q) * 64 + lane] = hv;
-                    col_store(ra1, 32 * t + acc_row(4 * q + 0, 0), ld4, off, hv.x);
-                    col_store(ra1, 32 * t + acc_row(4 * q + 1, 0), ld4, off, hv.y);
-                    col_store(ra1, 32 * t + acc_row(4 * q + 2, 0), ld4, off, hv.z);
-                    col_store(ra1, 32 * t + acc_row(4 * q + 3, 0), ld4, off, hv.w);
+                    if (G2048_GRAD_SPREAD != 1 && G2048_GRAD_SPREAD != 3) {
+                        col_store(ra1, 32 * t + acc_row(4 * q + 0, 0), ld4, off, hv.x);
+                        col_store(ra1, 32 * t + acc_row(4 * q + 1, 0), ld4, off, hv.y);
+                        col_store(ra1, 32 * t + acc_row(4 * q + 2, 0), ld4, off, hv.z);
+                        col_store(ra1, 32 * t + acc_row(4 * q + 3, 0), ld4, off, hv.w);
+                    }
                 }
             }
         }
@@ -834,6 +843,17 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, hb.y, acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, hb.z, acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, hb.w, acc, 0, 0, 0);
+                    if (G2048_GRAD_SPREAD == 1 || G2048_GRAD_SPREAD == 3) {
+                        // a1 value v = 4q + c of tile t goes out at output tile (v * NT2) / 16 (mode 1) or with the
+                        // first output tile (mode 3)
+                        const float hv[4] = {hb.x, hb.y, hb.z, hb.w};
+#pragma unroll
+                        for (int c = 0; c < 4; c++)
+                            if ((G2048_GRAD_SPREAD == 3 ? 0 : ((4 * q + c) * NT2) / 16) == o) {
+                                opaque_sgpr(ld4);
+                                col_store(ra1, 32 * t + acc_row(4 * q + c, 0), ld4, off, hv[c]);
+                            }
+                    }
                 }
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
@@ -934,7 +954,7 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                 dh = fmaf(g[2], wv.z, dh);
                 dh = fmaf(g[3], wv.w, dh);
                 h2[o][r] = dh * activation_derivative<ACT>(h2[o][r]);
-                col_store(rd2, 32 * o + acc_row(r, 0), ld4, off, h2[o][r]);
+                if (!G2048_GRAD_SPREAD) col_store(rd2, 32 * o + acc_row(r, 0), ld4, off, h2[o][r]);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -972,6 +992,14 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].y, h2[t2][4 * q + 1], acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].z, h2[t2][4 * q + 2], acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].w, h2[t2][4 * q + 3], acc, 0, 0, 0);
+                }
+                if (G2048_GRAD_SPREAD) {   // d2 value r of tile t2 goes out at input tile (r * NT1) / 16
+#pragma unroll
+                    for (int r = 0; r < 16; r++)
+                        if ((r * NT1) / 16 == o1) {
+                            opaque_sgpr(ld4);
+                            col_store(rd2, 32 * t2 + acc_row(r, 0), ld4, off, h2[t2][r]);
+                        }
                 }
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
