@@ -26,12 +26,14 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-// grad_kernel column stores: 0 = each phase stores its own columns (a1^T after layer 1, d2^T after d2); 1 = spread
-// over the MFMA loops that follow (the a1^T values as the layer-2 loop reads them, the d2^T values through the d1
-// loop), a few per k-tile, so the column writes drain under the MFMAs instead of stalling on the VMEM queue;
-// 2 = only the d2^T stores spread.
+// grad_kernel column stores.  0 = each phase stores its own columns (a1^T after layer 1, d2^T after d2): with one
+// wave per SIMD the wave then stalls on the VMEM queue (vmcnt caps outstanding ops at 63) while 128 stores per
+// lane drain.  The other modes issue them inside the MFMA loops that follow, so they drain under the MFMAs:
+// 2 = the d2^T values through the d1 loop (2 per k-tile; they are its B operand, already in registers);
+// 3 (default) = that, and the a1^T values as the first output tile of the layer-2 loop reads them from LDS;
+// 1 = as 3 with the a1^T stores spread over every output tile -- measured: the compiler spills 122 VGPRs.
 #ifndef G2048_GRAD_SPREAD
-#define G2048_GRAD_SPREAD 2
+#define G2048_GRAD_SPREAD 3
 #endif
 #ifndef G2048_DIAG
 #define G2048_DIAG 0
