@@ -338,6 +338,7 @@ def train_iteration_dp(torch, device, episodes_per_rank: int, rank: int, world: 
         barrier()
         t0 = time.perf_counter()
         batch = agent.rollout_batch(es, ps)
+        batch.shard_sizes = (E,) * world
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         agent.update_from_batch(batch)
@@ -363,7 +364,7 @@ def train_iteration_dp(torch, device, episodes_per_rank: int, rank: int, world: 
         dist.all_reduce(steps)
         res.update(rollout_s=float(t[0]), update_s=float(t[1]), iteration_s=float(t[2]), env_steps=int(steps[0]))
         ar_ms = float(t[3])
-    backend = dist.get_backend() if world > 1 else "none (1 rank)"
+    backend = dist.get_backend() if dist.is_initialized() else "none (1 rank)"
     return {"episodes": E * world, "episodes_per_gpu": E, **res,
             "env_steps_per_s": res["env_steps"] / res["iteration_s"],
             "grad_allreduce_ms": ar_ms, "grad_allreduce_bytes": 4 * (n_par + 1), "backend": str(backend),

@@ -77,6 +77,9 @@ class TrajectoryBatch:
     max_tile: torch.Tensor     # [n] int64 (Game2048Env.max_tile_seen at the end of the episode)
     final_boards: torch.Tensor  # [n] int64
     probs: torch.Tensor | None = None  # [T, n, 4] policy probabilities used for each draw (record_probs=True)
+    # data parallel: the episode count of every rank's shard of the global batch (dp.shard_sizes), set by whoever
+    # sharded it; lets the rank-weight all-gather run without a host synchronisation
+    shard_sizes: tuple[int, ...] | None = None
 
     @property
     def n(self) -> int:
@@ -216,6 +219,11 @@ class ReinforceAgent:
         # ... and the fused critic per time row, V(s') taken from the next row's pass (large batches)
         self.use_critic_rows = True
         self.grad_chunk_steps = 1 << 20
+        # diagnostics (tests): called as grad_probe(slot, k, sample_idx, a1t_cols, d2t_cols) with the column buffers
+        # of every fused-gradient launch before they are reused -- sample_idx indexes the batch's valid steps
+        # (time-major), a1t_cols [H1p + 1, m] holds the layer-1 activations the kernel computed, d2t_cols [H2p, m]
+        # its layer-2 deltas -- so a checker can evaluate the formula under the kernel's own activation pattern
+        self.grad_probe: Callable | None = None
         self._pack_cache: dict[str, list] = {}
         self._params_version = 0
         self._vec_cache: dict = {}
@@ -503,10 +511,25 @@ class ReinforceAgent:
         vout = torch.empty(max(max(counts), tail_m), dtype=torch.float32, device=self.device)
         gamma = float(c.gamma)
 
+        small = torch.zeros(pf, dtype=torch.float64, device=self.device)
+        launched: list[tuple[int, int, int, int]] = []     # (k, s0, cnt, column) of the launches in the buffer
+
+        def fold() -> None:
+            # the per-wave partials accumulate in fp32 across row launches; fold them into fp64 every so often
+            nonlocal small
+            small += part.sum(0, dtype=torch.float64)
+            part.zero_()
+
         def flush(used: int) -> None:
             nonlocal big
             if used == 0:
                 return
+            if self.grad_probe is not None:
+                for k_, s0_, cnt_, c0 in launched:
+                    self.grad_probe("critic", k_, torch.arange(s0_, s0_ + cnt_, device=self.device),
+                                    a1t[:, c0:c0 + cnt_], d2t[:, c0:c0 + cnt_])
+            launched.clear()
+            fold()
             m = -(-used // blk) * blk
             a1t[:, used:m].zero_()
             d2t[:, used:m].zero_()
@@ -518,7 +541,7 @@ class ReinforceAgent:
                              d2t[:, :m].view(H2p, P, q).permute(1, 2, 0)).sum(0)
 
         def grad_launch(s0: int, cnt: int, tgt: torch.Tensor, k: int) -> None:
-            nonlocal col
+            nonlocal col, since_fold
             b = flat[steps.vidx[s0:s0 + cnt]].contiguous()
             if k:
                 b = self._symmetry_boards(b, k)
@@ -530,9 +553,15 @@ class ReinforceAgent:
                                                 float(c.huber_delta), L.ptr(b), L.ptr(tgt), L.ptr(step_w[s0:s0 + cnt]),
                                                 L.ptr(deltas[k, s0:s0 + cnt]), L.ptr(vout), cnt, ld, col, ncols,
                                                 L.ptr(a1t), L.ptr(d2t), L.ptr(part), 1, waves, self._stream))
+            launched.append((k, s0, cnt, col))
             col += ncols
+            since_fold += 1
+            if since_fold == 64:
+                fold()
+                since_fold = 0
 
         col = 0
+        since_fold = 0
         for k in range(K):
             vb = [torch.zeros(n, dtype=torch.float32, device=self.device) for _ in range(2)]
             if tail_m:
@@ -564,7 +593,7 @@ class ReinforceAgent:
                 grad_launch(s0, cnt, tgt, k)
                 vb[t & 1].index_copy_(0, lanes, vout[:cnt])
         flush(col)
-        small = part.sum(0, dtype=torch.float64).to(torch.float32)
+        small = small.to(torch.float32)
         big = big.to(torch.float32)
         gW[0] += small[:16 * H1p].view(16, H1p)[:, :h1]
         gb[0] += small[16 * H1p:17 * H1p][:h1]
@@ -607,6 +636,8 @@ class ReinforceAgent:
                 a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
                 d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
                 launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale)
+                if self.grad_probe is not None:
+                    self.grad_probe(slot, k, sel, a1t[:, :m], d2t[:, :m])
                 big += torch.bmm(a1t.view(H1p + 1, P, q).transpose(0, 1), d2t.view(H2p, P, q).permute(1, 2, 0)).sum(0)
                 small += part.sum(0)
         big, small = big.to(torch.float32), small.to(torch.float32)
@@ -858,9 +889,10 @@ class ReinforceAgent:
         return out
 
     # ============================================================================================ weights & baselines
-    def _compute_episode_rank_weights(self, totals: torch.Tensor) -> torch.Tensor:
-        """src/reinforce_agent.py:681-716 on the global batch (dp.rank_weights)."""
-        return dp.rank_weights(totals, self.agent_config.reward_rank_weights)
+    def _compute_episode_rank_weights(self, totals: torch.Tensor, sizes=None) -> torch.Tensor:
+        """src/reinforce_agent.py:681-716 on the global batch (dp.rank_weights; `sizes` = every rank's episode
+        count when known, else one host-synchronising size exchange under data parallelism)."""
+        return dp.rank_weights(totals, self.agent_config.reward_rank_weights, sizes=sizes)
 
     def _advantages(self, values: torch.Tensor, lane: torch.Tensor, n_lanes: int, step_rank_w: torch.Tensor) -> torch.Tensor:
         """_compute_advantages (src/reinforce_agent.py:276-325) + _compute_weighted_stats (:864-881) over flat
@@ -963,14 +995,14 @@ class ReinforceAgent:
     def update_from_batch(self, batch: TrajectoryBatch) -> dict:
         """update_batch on a device TrajectoryBatch (the hot path: no host round trip)."""
         steps = _Steps(self, batch.lengths, batch.actions, batch.rewards, boards=batch.boards)
-        return self._update(steps, batch.total_reward)
+        return self._update(steps, batch.total_reward, batch.shard_sizes)
 
     def _chunks(self, N: int, size: int | None = None):
         size = size or self.chunk_steps
         for s in range(0, N, size):
             yield torch.arange(s, min(N, s + size), device=self.device)
 
-    def _update(self, steps: _Steps, totals: torch.Tensor) -> dict:
+    def _update(self, steps: _Steps, totals: torch.Tensor, shard_sizes=None) -> dict:
         """update_batch (src/reinforce_agent.py:357-620) on a batch of valid steps.  Per-step weights are
         rank_w / T_i; the 1 / n_traj factor is applied after the gradient all-reduce (dp.reduce_gradients_), so the
         data-parallel update needs ONE gradient collective and nothing synchronises the host before the final
@@ -978,7 +1010,7 @@ class ReinforceAgent:
         c = self.agent_config
         n_local = steps.n
         K = 8 if c.augmentation else 1
-        rank_w = self._compute_episode_rank_weights(totals)               # [n_local]
+        rank_w = self._compute_episode_rank_weights(totals, shard_sizes)  # [n_local]
         lane = steps.lane
         lens_f = steps.lengths.to(torch.float64)
         step_w = (rank_w[lane].double() / lens_f[lane]).to(torch.float32)   # rank_w / T_i (1 / n: after the reduce)

@@ -7,9 +7,13 @@ global statistics before the gradient pass:
                        clipping (src/reinforce_agent.py:558-561); the 1 / n_traj weight is applied after it
   * baseline sums   -> 'batch' / 'batch_norm' only: one all-reduce of 3 fp64 scalars (:864-881)
   * episode totals  -> reward_rank_weights only: an all-gather (global reward ranks, :681-716)
-None of them synchronises the host.  The fused buffer is 0.3-1.1 MB for the reference configs: latency-bound on
-xGMI, so a single bucket is the right size (no bucketing / overlap needed at this size).  These helpers are
-device-agnostic (gloo on CPU in the tests, RCCL on the GPUs).
+None of them synchronises the host when the caller passes the shard sizes of the global batch (``sizes``: the
+episode count of every rank's shard, known to whoever sharded the batch -- shard_sizes()); without them
+gather_varlen first exchanges the sizes, which costs one host synchronisation.  The fused buffer is 0.3-1.1 MB for
+the reference configs: latency-bound on xGMI, so a single bucket is the right size (no bucketing / overlap needed
+at this size).  These helpers are device-agnostic (gloo on CPU in the tests, RCCL on the GPUs).  Whenever a
+process group is initialised -- world size 1 included -- the collectives run through it, so a one-rank RCCL group
+exercises the device-backend path on one GPU.
 """
 from __future__ import annotations
 
@@ -18,7 +22,8 @@ import torch.distributed as dist
 
 
 def active(group=None) -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    """A process group is initialised (any world size): the collectives go through it."""
+    return dist.is_available() and dist.is_initialized()
 
 
 def world(group=None) -> tuple[int, int]:
@@ -27,21 +32,41 @@ def world(group=None) -> tuple[int, int]:
     return dist.get_rank(group), dist.get_world_size(group)
 
 
+def shard_bounds(n: int, rank: int, ws: int) -> tuple[int, int]:
+    """Episodes [lo, hi) of rank `rank` when a global batch of n episodes is split into ws contiguous shards of
+    ceil(n / ws) (the last ones shorter or empty)."""
+    per = (n + ws - 1) // ws
+    lo = min(rank * per, n)
+    return lo, min(lo + per, n)
+
+
+def shard_sizes(n: int, ws: int) -> tuple[int, ...]:
+    """The episode count of every rank's shard (shard_bounds) -- host-known, so the collectives need no size
+    exchange."""
+    return tuple(hi - lo for lo, hi in (shard_bounds(n, r, ws) for r in range(ws)))
+
+
 def all_reduce_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
     if active(group):
         dist.all_reduce(t, group=group)
     return t
 
 
-def gather_varlen(x: torch.Tensor, group=None) -> tuple[torch.Tensor, int]:
-    """Concatenate a 1-D tensor of per-rank length across ranks (rank order).  Returns (all, my offset)."""
+def gather_varlen(x: torch.Tensor, group=None, sizes=None) -> tuple[torch.Tensor, int]:
+    """Concatenate a 1-D tensor of per-rank length across ranks (rank order).  Returns (all, my offset).
+    sizes: every rank's length (host-known, e.g. shard_sizes) -- then no host synchronisation; None exchanges
+    the lengths first (one all-gather read back on the host)."""
     if not active(group):
         return x, 0
     rank, ws = world(group)
-    n = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
-    sizes = [torch.zeros_like(n) for _ in range(ws)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
+    if sizes is None:
+        n = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
+        parts_n = [torch.zeros_like(n) for _ in range(ws)]
+        dist.all_gather(parts_n, n, group=group)
+        sizes = [int(s) for s in torch.cat(parts_n).tolist()]      # the one host synchronisation
+    sizes = [int(s) for s in sizes]
+    if len(sizes) != ws or sizes[rank] != x.numel():
+        raise ValueError(f"gather_varlen: sizes {sizes} do not match world size {ws} / this rank's {x.numel()}")
     padded = torch.zeros(max(sizes), dtype=x.dtype, device=x.device)
     padded[: x.numel()] = x
     parts = [torch.zeros_like(padded) for _ in range(ws)]
@@ -61,16 +86,16 @@ def fused_all_reduce_(tensors: list[torch.Tensor], group=None) -> None:
         off += t.numel()
 
 
-def rank_weights(totals: torch.Tensor, conf, group=None) -> torch.Tensor:
+def rank_weights(totals: torch.Tensor, conf, group=None, sizes=None) -> torch.Tensor:
     """_compute_episode_rank_weights (src/reinforce_agent.py:681-716) over the GLOBAL batch; returns this rank's
     slice.  Episode ranks come from a stable sort of the fp64 totals (the Python floats the reference sorts,
     :701); exact ties keep episode order, where the reference's default numpy sort leaves their order
     machine-dependent.  Weights are fp32 as in the reference: conf[bin] / mean, the mean an fp32 division of the
-    (exact) weight sum by n.  No host synchronisation."""
+    (exact) weight sum by n.  No host synchronisation when `sizes` (every rank's episode count) is given."""
     n_local = totals.numel()
     if conf is None or len(conf) == 0:
         return torch.ones(n_local, dtype=torch.float32, device=totals.device)
-    all_tot, offset = gather_varlen(totals.to(torch.float64), group)
+    all_tot, offset = gather_varlen(totals.to(torch.float64), group, sizes)
     n = all_tot.numel()
     confs = torch.tensor(list(conf), dtype=torch.float32, device=totals.device)
     order = torch.argsort(all_tot, stable=True)
@@ -101,24 +126,42 @@ def batch_mean_std(values: torch.Tensor, weights: torch.Tensor, group=None) -> t
     return torch.where(ok, mean, torch.zeros_like(mean)), torch.where(ok, torch.sqrt(var), torch.ones_like(var))
 
 
+# the episode count travels in the fp32 gradient buffer as base-2^16 digits: each digit sum is exact in fp32 for
+# up to 256 ranks (256 * 65535 < 2^24), and counts up to 2^48 are representable
+_COUNT_DIGITS = 3
+
+
+def _count_digits(n: int) -> list[float]:
+    n = int(n)
+    if n < 0 or n >= 1 << (16 * _COUNT_DIGITS):
+        raise ValueError(f"episode count {n} out of range")
+    return [float((n >> (16 * d)) & 0xFFFF) for d in range(_COUNT_DIGITS)]
+
+
 def reduce_gradients_(tensors: list[torch.Tensor], n_local: int, group=None) -> None:
     """Finish the gradients of update_batch across ranks with ONE collective: every rank accumulated its
     episodes' sum of rank_w / T_i-weighted per-step gradients; the flat fp32 buffer of all of them (actor +
-    critic) plus this rank's episode count is all-reduced, and each gradient is divided by the global count --
-    the 1 / n_traj of src/reinforce_agent.py:467, :533 -- on the device (no host synchronisation).  The count
-    travels as an fp32 element: exact up to 2^24 episodes per update.  Single process: just the division."""
+    critic) plus this rank's episode count (as exact base-2^16 digits) is all-reduced, the global count is rebuilt
+    exactly in fp64 on the device, and every gradient is multiplied by fp32(1 / count) -- the 1 / n_traj of
+    src/reinforce_agent.py:467, :533 (n_traj = 8 n with augmentation).  No host synchronisation.  Without a process
+    group: the same multiply by fp32(1 / n_local)."""
     if not tensors:
         return
     if not active(group):
-        inv = 1.0 / max(int(n_local), 1)
+        inv = torch.tensor(1.0 / max(int(n_local), 1), dtype=torch.float64).to(torch.float32).item()
         for t in tensors:
             t.mul_(inv)
         return
+    dev, dt = tensors[0].device, tensors[0].dtype
     flat = torch.cat([t.reshape(-1) for t in tensors] +
-                     [torch.full((1,), float(n_local), dtype=tensors[0].dtype, device=tensors[0].device)])
+                     [torch.tensor(_count_digits(n_local), dtype=dt, device=dev)])
     dist.all_reduce(flat, group=group)
-    flat[:-1].div_(flat[-1].clamp(min=1.0))
+    digits = flat[-_COUNT_DIGITS:].double()
+    scale = torch.tensor([float(1 << (16 * d)) for d in range(_COUNT_DIGITS)], dtype=torch.float64, device=dev)
+    count = (digits * scale).sum().clamp(min=1.0)
+    grads = flat[:-_COUNT_DIGITS]
+    grads.mul_((1.0 / count).to(dt))
     off = 0
     for t in tensors:
-        t.copy_(flat[off: off + t.numel()].view_as(t))
+        t.copy_(grads[off: off + t.numel()].view_as(t))
         off += t.numel()

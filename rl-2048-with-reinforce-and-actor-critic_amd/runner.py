@@ -198,14 +198,12 @@ def create_training_run_dir() -> tuple[Path, str]:
 
 def _shard(n: int) -> tuple[int, int]:
     rank, world = dp.world()
-    per = (n + world - 1) // world
-    lo = min(rank * per, n)
-    return lo, min(lo + per, n)
+    return dp.shard_bounds(n, rank, world)
 
 
 def _global_episode_stats(batch) -> tuple[np.ndarray, np.ndarray]:
-    tot, _ = dp.gather_varlen(batch.total_reward.to(torch.float64))
-    mt, _ = dp.gather_varlen(batch.max_tile.to(torch.float64))
+    tot, _ = dp.gather_varlen(batch.total_reward.to(torch.float64), sizes=batch.shard_sizes)
+    mt, _ = dp.gather_varlen(batch.max_tile.to(torch.float64), sizes=batch.shard_sizes)
     return tot.cpu().numpy(), mt.cpu().numpy().astype(np.int64)
 
 
@@ -259,6 +257,7 @@ def training_loop(agent: ReinforceAgent, env_config, mlp_config, agent_config, t
     while nb <= 0 or step < nb:
         env_seeds, pol_seeds = env_stream.take_array(bs), pol_stream.take_array(bs)
         batch = agent.rollout_batch(env_seeds[lo:hi], pol_seeds[lo:hi])
+        batch.shard_sizes = dp.shard_sizes(bs, dp.world()[1])
         step += 1
         totals, max_tiles = _global_episode_stats(batch)
         r32 = totals.astype(np.float32)
@@ -313,6 +312,7 @@ def evaluation_loop(agent: ReinforceAgent, eval_cfg: Dict[str, Any], chunk: int 
         e, p = env_seeds[s:s + chunk], pol_seeds[s:s + chunk]
         lo, hi = _shard(len(e))
         b = agent.rollout_batch(e[lo:hi], p[lo:hi], use_greedy=greedy)
+        b.shard_sizes = dp.shard_sizes(len(e), dp.world()[1])
         t, m = _global_episode_stats(b)
         totals.append(t)
         tiles.append(m)

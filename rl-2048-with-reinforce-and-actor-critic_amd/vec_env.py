@@ -164,9 +164,15 @@ class VecGame2048Env:
                 self.score.zero_()
             else:
                 self.score.masked_fill_(m != 0, 0)
-        if self.mask_bits is not None:   # reset writes the int8[4] form; keep the packed one current
+        if self.mask_bits is not None:
+            # reset writes the int8[4] form for the lanes it resets; steps write only the packed form, so
+            # self.mask is stale on every other lane: repack the reset lanes only
             w = torch.tensor([1, 2, 4, 8], dtype=torch.int32, device=self.device)
-            self.mask_bits.copy_(((self.mask != 0).to(torch.int32) * w).sum(1).to(torch.uint8))
+            packed = ((self.mask != 0).to(torch.int32) * w).sum(1).to(torch.uint8)
+            if m is None:
+                self.mask_bits.copy_(packed)
+            else:
+                self.mask_bits.copy_(torch.where(m != 0, packed, self.mask_bits))
         return self._obs_view(), {"score": self.score, "board": self.board}
 
     def step_into(self, actions: torch.Tensor, reward: torch.Tensor | None = None, flags: torch.Tensor | None = None,

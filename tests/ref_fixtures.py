@@ -137,3 +137,38 @@ def rel(a, b) -> float:
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30)) if b.size else 0.0
+
+
+def adam_state(agent, critic: bool = False):
+    """Copies of the agent's Adam moments ([W..., b...] order, as the gradients) and step counter."""
+    if critic:
+        mW, vW, mB, vB, t = agent._adam_m_W_c, agent._adam_v_W_c, agent._adam_m_B_c, agent._adam_v_B_c, agent._adam_t_c
+    else:
+        mW, vW, mB, vB, t = agent._adam_m_W, agent._adam_v_W, agent._adam_m_B, agent._adam_v_B, agent._adam_t
+    host = lambda ts: [x.detach().cpu().numpy().astype(np.float64) for x in ts]  # noqa: E731
+    return host(mW) + host(mB), host(vW) + host(vB), int(t)
+
+
+def assert_adam_step_exact(after, before, grads, state, lr, sign, b1, b2, max_norm, what="") -> None:
+    """One Adam update (src/reinforce_agent.py:719-770, after clip_grads_global_norm :835-861) checked on the exact
+    basis: the parameter step taken equals the fp64 evaluation of the Adam formula -- clip coefficient, moments
+    with bias correction, eps outside the sqrt -- applied to OUR pre-clip gradient (held to the exact value of the
+    reference's formula by assert_grad_parity) and our previous moments, on every element, within the fp32
+    rounding of the step and of the parameter.  (Elements whose gradient is rounding noise take a step of either
+    sign of up to ~lr; compared with the reference's own noise they cannot be matched, compared with the formula
+    they can.)"""
+    m0, v0, t = state
+    g = [np.asarray(x, np.float64) for x in grads]
+    norm = float(np.sqrt(sum(float(np.sum(x * x)) for x in g)))
+    coef = min(1.0, max_norm / max(norm, 1e-8))
+    t1 = t + 1
+    bc1, bc2 = 1.0 - b1 ** t1, 1.0 - b2 ** t1
+    for k, (a, b, gi, m, v) in enumerate(zip(after, before, g, m0, v0)):
+        a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+        gc = gi * coef
+        mn = b1 * m + (1.0 - b1) * gc
+        vn = b2 * v + (1.0 - b2) * gc * gc
+        step = sign * lr * (mn / bc1) / (np.sqrt(vn / bc2) + 1e-8)
+        tol = 1e-6 * lr + 2.0 ** -23 * np.abs(b) + 1e-5 * np.abs(step)
+        bad = np.abs((a - b) - step) > tol
+        assert not bad.any(), (what, k, int(bad.sum()), (a - b)[bad][:5], step[bad][:5])

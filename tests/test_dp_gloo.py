@@ -46,8 +46,15 @@ def _worker(rank, world, port, q):
         # reduce_gradients_: sum over ranks / global episode count (6 + 7), one collective
         h = [torch.full((2, 2), float(rank + 1) * 13.0), torch.ones(3) * (rank + 1) * 26.0]
         dp.reduce_gradients_(h, sizes[rank])
+        # the same gathers with the shard sizes known host-side (no size exchange)
+        w_local2 = dp.rank_weights(mine, conf, sizes=sizes)
+        allg2, o2 = dp.gather_varlen(mine, sizes=sizes)
+        # the count path alone, augmented episode counts (8 n) far above 2^24 whose fp32 sum would round
+        big = [8 * 8_388_608 + 3, 8 * 1_000_001][rank]
+        c = [torch.full((5,), float(rank + 1))]
+        dp.reduce_gradients_(c, big)
         q.put((rank, w_local.numpy(), allg.numpy(), o, float(mean), float(std), [t.numpy() for t in g],
-               [t.numpy() for t in h]))
+               [t.numpy() for t in h], w_local2.numpy(), allg2.numpy(), o2, c[0].numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -88,6 +95,12 @@ def test_dp_collectives_equal_single_process():
         np.testing.assert_array_equal(res[r][6][1], np.arange(4) * 3.0)
         np.testing.assert_allclose(res[r][7][0], np.full((2, 2), 3.0), rtol=1e-7)     # (13 + 26) / 13
         np.testing.assert_allclose(res[r][7][1], np.full(3, 6.0), rtol=1e-7)          # (26 + 52) / 13
+        np.testing.assert_array_equal(res[r][8], res[r][1])
+        np.testing.assert_array_equal(res[r][9], totals)
+        assert res[r][10] == res[r][3]
+        # (1 + 2) * fp32(1 / (67,108,867 + 8,000,008)): the global count is exact
+        inv = np.float32(1.0 / (8 * 8_388_608 + 3 + 8 * 1_000_001))
+        np.testing.assert_array_equal(res[r][11], np.full(5, np.float32(3.0) * inv, dtype=np.float32))
 
 
 def test_rank_weights_match_reference_formula():
@@ -118,3 +131,24 @@ def test_batch_mean_std_single(n):
     got = [float(x) for x in dp.batch_mean_std(torch.tensor(v), torch.tensor(w))]
     ref = AO.OracleAgent.weighted_stats(v.astype(np.float64), w.astype(np.float64))
     assert abs(got[0] - float(ref[0])) < 1e-9 * max(1.0, abs(float(ref[0]))) and abs(got[1] - float(ref[1])) < 1e-9
+
+
+def test_shard_sizes_partition():
+    from rl2048_amd import dp
+
+    for n in (0, 1, 7, 8, 1 << 20, 4_194_304):
+        for ws in (1, 2, 3, 8):
+            sz = dp.shard_sizes(n, ws)
+            assert sum(sz) == n and len(sz) == ws
+            assert [dp.shard_bounds(n, r, ws) for r in range(ws)] == [
+                (sum(sz[:r]), sum(sz[:r + 1])) for r in range(ws)]
+
+
+def test_reduce_gradients_single_process_scale():
+    """No process group: the gradients are multiplied by fp32(1 / n), the same factor the all-reduce path uses."""
+    from rl2048_amd import dp
+
+    n = 8 * 8_388_608 + 3
+    t = [torch.full((4,), 3.0)]
+    dp.reduce_gradients_(t, n)
+    np.testing.assert_array_equal(t[0].numpy(), np.full(4, np.float32(3.0) * np.float32(1.0 / n), dtype=np.float32))

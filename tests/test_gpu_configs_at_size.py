@@ -12,16 +12,18 @@
   (oracle/g2048_oracle.c, pinned by Random123's known answers), spawn-distribution KAT over every lane.
 (configs[3], 8-way RCCL, needs the 8-GPU node: tests/test_dp_gloo.py covers its exchange on CPU.)
 
-Gradient tolerance (normwise-relative: max abs error / max abs value per tensor) against fp64 evaluations of the
-formula: the plain fp32 path within 1e-5 of the fp64 value computed with that path's own ReLU patterns; the fused
-and plain paths within 2e-4 of the plain fp64 value -- at millions of samples fp32 rounding of pre-activations
-next to 0 flips ReLU derivatives (see _run_config), so no fp32 evaluation, the reference's included, sits within
-1e-5 of the fp64 value there; the measured errors are printed.
+Gradient tolerance: 1e-5 normwise-relative (max abs error / max abs value per tensor) against the exact fp64 value
+of the formula under the ReLU activation pattern each fp32 path computed (tests/exact_grad.py): the fused kernels'
+pattern is read from their own column buffers (ReinforceAgent.grad_probe), the plain hipBLASLt path's recomputed
+on its own chunks.  At millions of samples fp32 rounding of pre-activations next to 0 flips ReLU derivatives, in
+every fp32 evaluation (the reference's included) on different samples; the errors against fp64 with fp64's own
+pattern are printed beside.
 """
 import numpy as np
 import pytest
 import torch
 
+import exact_grad as EG
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -65,6 +67,8 @@ def _replay_sampled(batch, env_seeds, pol_seeds, k, seed):
         total = 0.0
         Ti = int(lens[i])
         assert 0 < Ti <= T
+        if j % 50 == 49:
+            print(f"  replayed {j + 1} / {len(idx)} episodes", flush=True)
         for t in range(Ti):
             assert boards[t, j] == O.pack_exponents(O.values_to_exponents(env.board)), (i, t)
             assert pol.choice4(probs[t, j]) == acts[t, j], (i, t)
@@ -76,107 +80,6 @@ def _replay_sampled(batch, env_seeds, pol_seeds, k, seed):
     return idx
 
 
-def _fp64_net(params):
-    return [w.double() for w in params["W"]], [b.double() for b in params["b"]]
-
-
-def _fwd64(W, b, x, masks=None):
-    """fp64 forward; masks = the ReLU patterns (z1 > 0, z2 > 0) to impose (those of an fp32 forward), or None."""
-    z1 = x @ W[0] + b[0]
-    if masks is not None:
-        z1 = torch.where(masks[0], z1.abs().clamp_min(1e-300), -z1.abs())
-    a1 = torch.relu(z1)
-    z2 = a1 @ W[1] + b[1]
-    if masks is not None:
-        z2 = torch.where(masks[1], z2.abs().clamp_min(1e-300), -z2.abs())
-    a2 = torch.relu(z2)
-    return z1, a1, z2, a2, a2 @ W[2] + b[2]
-
-
-def _fp32_masks(params, x32):
-    """ReLU patterns of the plain fp32 forward (mlp_forward_kept: hipBLASLt GEMMs with the bias + ReLU epilogue)."""
-    from rl2048_amd.mlp import mlp_forward_kept
-
-    _, acts = mlp_forward_kept(params, x32, "ReLU")
-    return acts[1] > 0, acts[2] > 0
-
-
-def _bwd64(W, x, z1, a1, z2, a2, g, acc):
-    """_backpropagation (src/reinforce_agent.py:639-678) summed over rows, fp64, into acc = [dW1..3, db1..3]."""
-    acc[2] += a2.t() @ g
-    acc[5] += g.sum(0)
-    d2 = (g @ W[2].t()) * (z2 > 0)
-    acc[1] += a1.t() @ d2
-    acc[4] += d2.sum(0)
-    d1 = (d2 @ W[1].t()) * (z1 > 0)
-    acc[0] += x.t() @ d1
-    acc[3] += d1.sum(0)
-
-
-def _exact_update_grads(agent, batch, chunk=1 << 20, fp32_masks=False):
-    """fp64 evaluation of update_batch's pre-clip gradients (src/reinforce_agent.py:357-555) on a device batch:
-    returns / TD errors, batch-baseline advantages (weights all 1), rank_w / (T_i n) step weights, manual backprop.
-    Independent of the product's kernels (torch fp64 GEMMs; obs from g2048_obs, whose values are pinned).
-    fp32_masks=True imposes the ReLU patterns of the plain fp32 forward (everything else fp64): the exact value
-    of the formula given the activation pattern an fp32 evaluation sees."""
-    c = agent.agent_config
-    T, n = batch.boards.shape
-    lens = batch.lengths.to(torch.int64)
-    valid = torch.arange(T, device=DEV).unsqueeze(1) < lens.unsqueeze(0)
-    vidx = valid.reshape(-1).nonzero().squeeze(1)
-    lane, t = vidx % n, vidx // n
-    has_next = (t + 1) < lens[lane]
-    w_step = 1.0 / (lens[lane].double() * n)
-    R64 = batch.rewards.double()
-    W, b = _fp64_net(agent.params)
-    out = {}
-    if c.use_critic:
-        Wc, bc = _fp64_net(agent.critic_params)
-        accc = [torch.zeros_like(p) for p in Wc + bc]
-        delta = torch.empty(vidx.numel(), dtype=torch.float64, device=DEV)
-        flat = batch.boards.reshape(-1)
-        for s in range(0, vidx.numel(), chunk):
-            sl = slice(s, min(s + chunk, vidx.numel()))
-            x32 = agent._obs_from_boards(flat[vidx[sl]].contiguous())[0]
-            x = x32.double()
-            hn = has_next[sl]
-            nxt = torch.where(hn, vidx[sl] + n, vidx[sl])
-            xn32 = agent._obs_from_boards(flat[nxt].contiguous())[0]
-            mk_c = _fp32_masks(agent.critic_params, x32) if fp32_masks else None
-            mk_n = _fp32_masks(agent.critic_params, xn32) if fp32_masks else None
-            z1, a1, z2, a2, v = _fwd64(Wc, bc, x, mk_c)
-            vn = _fwd64(Wc, bc, xn32.double(), mk_n)[4][:, 0]
-            r32 = R64.reshape(-1)[vidx[sl]].float().double()          # np.array(rewards, float32) (:420)
-            tgt = r32 + c.gamma * vn * hn.double()
-            delta[sl] = tgt - v[:, 0]
-            _bwd64(Wc, x, z1, a1, z2, a2, ((v[:, 0] - tgt) * w_step[sl]).unsqueeze(1), accc)
-        out["critic"] = accc
-        values = delta.float().double()                                   # td_errors.astype(float32) (:447)
-    else:
-        G = torch.zeros(n, dtype=torch.float64, device=DEV)
-        Gt = torch.empty(T, n, dtype=torch.float64, device=DEV)
-        for tt in reversed(range(T)):                                     # compute_returns (:255-273)
-            G = R64[tt] + c.gamma * G
-            Gt[tt] = G
-        values = Gt.float().double().reshape(-1)[vidx]                   # returns stored as float32
-    assert c.baseline_mode == "batch" and not c.reward_rank_weights
-    adv = values - values.mean()                                          # _compute_advantages "batch" (:314-316)
-    acc = [torch.zeros_like(p) for p in W + b]
-    flat = batch.boards.reshape(-1)
-    acts = batch.actions.reshape(-1)
-    for s in range(0, vidx.numel(), chunk):
-        sl = slice(s, min(s + chunk, vidx.numel()))
-        x32, mk = agent._obs_from_boards(flat[vidx[sl]].contiguous())
-        x = x32.double()
-        z1, a1, z2, a2, lg = _fwd64(W, b, x, _fp32_masks(agent.params, x32) if fp32_masks else None)
-        lg = torch.where(mk.bool(), lg, torch.full_like(lg, -1e9))
-        p = torch.softmax(lg, dim=1)
-        oh = torch.nn.functional.one_hot(acts[vidx[sl]].long(), 4).double()
-        _bwd64(W, x, z1, a1, z2, a2, (oh - p) * (adv[sl] * w_step[sl]).unsqueeze(1), acc)
-    out["actor"] = acc
-    return out
-
-
 def _check_probs_fp64(agent, batch, idx):
     """The probabilities the rollout drew from vs an fp64 forward + masked softmax of the same boards."""
     it = torch.tensor(idx, device=DEV)
@@ -184,8 +87,8 @@ def _check_probs_fp64(agent, batch, idx):
     b = batch.boards[:, it]
     valid = torch.arange(batch.T, device=DEV).unsqueeze(1) < lens.unsqueeze(0)
     x, mk = agent._obs_from_boards(b[valid].contiguous())
-    W, bb = _fp64_net(agent.params)
-    lg = _fwd64(W, bb, x.double())[4]
+    W, bb = [w.double() for w in agent.params["W"]], [v.double() for v in agent.params["b"]]
+    lg = EG.fwd64(W, bb, x.double())[4]
     p = torch.softmax(torch.where(mk.bool(), lg, torch.full_like(lg, -1e9)), dim=1)
     assert float((batch.probs[:, it][valid].double() - p).abs().max()) < 2e-6
 
@@ -197,36 +100,44 @@ def _run_config(episodes, critic, k_sample):
     es, ps = SeedStream(3).take_array(episodes), SeedStream(7).take_array(episodes)
     batch = agent.rollout_batch(es, ps, record_probs=True)
     assert batch.n == episodes
+    print(f"\nrollout of {episodes} episodes done; replaying {k_sample} in the oracle", flush=True)
     idx = _replay_sampled(batch, es, ps, k_sample, seed=episodes)
     _check_probs_fp64(agent, batch, idx)
-    N = int(batch.lengths.sum())
-    exact = _exact_update_grads(agent, batch)
-    exact_m = _exact_update_grads(agent, batch, fp32_masks=True)
+    print("replay and probabilities ok", flush=True)
     batch.probs = None
-    # the same update through the plain fp32 GEMM path (hipBLASLt, mlp_backward_): the yardstick for how far an
-    # fp32 evaluation of the formula lands from the exact value at this N
+    N = int(batch.lengths.sum())
+    params0 = EG.snapshot(agent)
+    # the fused update, recording the ReLU pattern its kernels used (from their own a1^T / d2^T columns)
+    probe = EG.PatternProbe(1, N, DEV)
+    agent.grad_probe = probe
+    stats = agent.update_from_batch(batch)
+    agent.grad_probe = None
+    nets = ("actor", "critic") if critic else ("actor",)
+    assert all(probe.complete(w) for w in nets)
+    # the same update through the plain fp32 GEMM path (hipBLASLt, mlp_backward_)
     plain = _agent(baseline_mode="batch", gamma=0.99, use_critic=critic)
     plain.use_fused_grad = False
     plain.update_from_batch(batch)
-    stats = agent.update_from_batch(batch)
-    errs, errs_plain, errs_plain_m = {}, {}, {}
-    for which in ("actor", "critic") if critic else ("actor",):
-        for j, (g, gp, e, em) in enumerate(zip(agent.last_grads[which], plain.last_grads[which], exact[which],
-                                               exact_m[which])):
-            errs[f"{which}{j}"] = _rel(g, e)
-            errs_plain[f"{which}{j}"] = _rel(gp, e)
-            errs_plain_m[f"{which}{j}"] = _rel(gp, em)
+    exact_f = EG.exact_update_grads(agent, batch, patterns=probe, params=params0)
+    errs = EG.grad_errors(agent.last_grads, exact_f)
+    del exact_f, probe
+    exact_p = EG.exact_update_grads(plain, batch, patterns="plain", params=params0)
+    errs_plain = EG.grad_errors(plain.last_grads, exact_p)
+    del exact_p
+    exact = EG.exact_update_grads(agent, batch, params=params0)       # plain fp64, no imposed pattern
+    errs_free = EG.grad_errors(agent.last_grads, exact)
+    errs_free_plain = EG.grad_errors(plain.last_grads, exact)
+    for which in nets:
         en = float(torch.sqrt(sum((e ** 2).sum() for e in exact[which])))
         assert abs(stats[f"{which}_grad_norm"] - en) <= 1e-5 * en, (which, stats[f"{which}_grad_norm"], en)
     fmt = lambda d: ", ".join(f"{k}={v:.2e}" for k, v in d.items())  # noqa: E731
-    print(f"\n{episodes} episodes, {N} steps: error vs fp64 -- fused {fmt(errs)} | plain fp32 GEMM path "
-          f"{fmt(errs_plain)} | plain vs fp64 with the plain path's ReLU patterns {fmt(errs_plain_m)}")
-    # Given the activation pattern an fp32 forward sees, the fp32 evaluation is within the north star's 1e-5 of the
-    # exact value; what remains of the fused / plain error against fp64 is ReLU derivatives flipped by fp32 rounding
-    # of pre-activations within ~1e-7 of 0 (~1e-6 of the unit-samples), different samples in each fp32 path.
-    assert all(v < 1e-5 for v in errs_plain_m.values()), errs_plain_m
-    for k in errs:
-        assert errs[k] < 2e-4 and errs_plain[k] < 2e-4, (k, errs[k], errs_plain[k])
+    print(f"\n{episodes} episodes, {N} steps: fused vs fp64 under the fused kernels' ReLU pattern {fmt(errs)} | "
+          f"plain fp32 GEMM path vs fp64 under its pattern {fmt(errs_plain)} | vs fp64 with fp64's own pattern: "
+          f"fused {fmt(errs_free)}, plain {fmt(errs_free_plain)}")
+    # the north star's 1e-5, for both fp32 paths, each against the exact value of the formula under the activation
+    # pattern that path computed (module docstring)
+    assert all(v < 1e-5 for v in errs.values()), errs
+    assert all(v < 1e-5 for v in errs_plain.values()), errs_plain
     return N
 
 

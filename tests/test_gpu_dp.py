@@ -86,3 +86,169 @@ def test_two_rank_update_equals_single_process():
         assert abs(res[rank][3] - stats["actor_grad_norm"]) <= 1e-5 * stats["actor_grad_norm"]
     for a, b in zip(res[0][1], res[1][1]):   # replicas stay identical
         np.testing.assert_array_equal(a, b)
+
+
+# ------------------------------------------------------------------------------------------ configs[3] shard
+# configs[3]: 4,194,304 boards sharded 8 ways -> 524,288 episodes per rank, the runner-default 16-256-256-4 ReLU
+# net, actor-critic (critic MSE, per-row fused critic pass), batch baseline, SGD.  Two ranks on cuda:0 each play
+# one such shard of a 1,048,576-episode global batch (runner.py:581-663's loop shape: env seed stream, policy seed
+# stream per global episode); their data-parallel update must equal the single-process update on the
+# concatenated batch.
+C3_E = 1 << 19
+C3_ACFG = dict(baseline_mode="batch", optimizer="sgd", use_critic=True, critic_loss_type="mse", gamma=0.99,
+               learning_rate=1e-4, critic_learning_rate=1e-5)
+
+
+def _c3_agent():
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from rl2048_amd import Game2048EnvConfig
+    from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
+    from rl2048_amd.mlp import MLPConfig
+
+    return ReinforceAgent(Game2048EnvConfig(), MLPConfig(hidden_sizes=[256, 256], activation="ReLU",
+                                                         init_distribution="HeNormal"),
+                          ReinforceAgentConfig(**C3_ACFG), device="cuda:0")
+
+
+def _c3_seeds(lo, hi):
+    es = np.arange(1000 + lo, 1000 + hi, dtype=np.int64)
+    return es, es + (1 << 40)
+
+
+def _c3_result(agent, stats):
+    return ({k: [g.cpu().numpy() for g in v] for k, v in agent.last_grads.items()},
+            [t.cpu().numpy() for t in agent.params["W"] + agent.params["b"] + agent.critic_params["W"] +
+             agent.critic_params["b"]], stats)
+
+
+def _c3_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rl2048_amd import dp
+
+        agent = _c3_agent()
+        lo, hi = dp.shard_bounds(world * C3_E, rank, world)
+        batch = agent.rollout_batch(*_c3_seeds(lo, hi))
+        batch.shard_sizes = dp.shard_sizes(world * C3_E, world)
+        assert agent._critic_by_rows(_steps(agent, batch))          # the per-row critic pass at this size
+        stats = agent.update_from_batch(batch)
+        q.put((rank, int(batch.lengths.sum())) + _c3_result(agent, stats))
+    finally:
+        dist.destroy_process_group()
+
+
+def _steps(agent, batch):
+    from rl2048_amd.agent import _Steps
+
+    return _Steps(agent, batch.lengths, batch.actions, batch.rewards, boards=batch.boards)
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def test_configs3_shard_two_ranks_equal_single_process():
+    """2 ranks x 524,288 episodes (configs[3]'s per-GPU shard) == 1 process x 1,048,576 episodes: pre-clip actor and
+    critic gradients within 1e-5 normwise-relative, norms within 1e-5, parameters after SGD within fp32 rounding.
+    The fused kernels compute every sample's forward identically wherever it lands (same ReLU pattern), so the
+    difference is summation order; the single-process path itself is held to the exact fp64 value of the formula
+    at this size by tests/test_gpu_configs_at_size.py."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_c3_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r = q.get(timeout=600)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    agent = _c3_agent()
+    batch = agent.rollout_batch(*_c3_seeds(0, 2 * C3_E))
+    n_steps = int(batch.lengths.sum())
+    assert n_steps == res[0][1] + res[1][1] and n_steps > 100_000_000, (n_steps, res[0][1], res[1][1])
+    stats = agent.update_from_batch(batch)
+    grads, params, _ = _c3_result(agent, stats)
+    for rank in (0, 1):
+        g_r, p_r, st_r = res[rank][2], res[rank][3], res[rank][4]
+        for which in ("actor", "critic"):
+            for j, (a, b) in enumerate(zip(g_r[which], grads[which])):
+                assert _rel(a, b) < 1e-5, (rank, which, j, _rel(a, b))
+            assert abs(st_r[f"{which}_grad_norm"] - stats[f"{which}_grad_norm"]) <= 1e-5 * stats[f"{which}_grad_norm"]
+        for a, b in zip(p_r, params):
+            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+    for a, b in zip(res[0][3], res[1][3]):   # replicas stay identical
+        np.testing.assert_array_equal(a, b)
+
+
+# ------------------------------------------------------------------------------------------ RCCL
+def _rccl_worker(port, q):
+    import sys
+
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    import bench
+    from rl2048_amd import dp
+
+    def run():
+        agent = _agent()   # actor-critic, batch_norm baseline, rank weights, Adam
+        es, ps = _seeds()
+        b = agent.rollout_batch(es, ps)
+        st = agent.update_from_batch(b)
+        return ([t.cpu().numpy() for t in agent.params["W"] + agent.params["b"] + agent.critic_params["W"] +
+                 agent.critic_params["b"]], st)
+
+    ref = run()                                  # no process group: the single-process path
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        assert dp.active() and dist.get_backend() == "nccl"
+        got = run()                              # every collective of the update through RCCL
+        sizes = dp.gather_varlen(torch.arange(5, dtype=torch.float64, device=dev), sizes=(5,))[0].cpu().numpy()
+        c = [torch.full((3,), 2.0, device=dev)]
+        dp.reduce_gradients_(c, 8 * 8_388_608 + 3)
+        train = bench.train_iteration_dp(torch, dev, 1 << 14, 0, 1)
+        q.put((ref, got, sizes, c[0].cpu().numpy(), train))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_world_size_one_runs_the_update_and_bench_leg():
+    """A one-rank RCCL ("nccl") process group on cuda:0: update_from_batch runs its rank-weight all-gather, batch
+    statistics all-reduce and fused gradient all-reduce through RCCL and gives exactly the single-process update;
+    the exact-count path and bench.py's train_iteration_dp leg run on RCCL too."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(port, q))
+    p.start()
+    ref, got, sizes, c, train = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    for a, b in zip(got[0], ref[0]):
+        np.testing.assert_array_equal(a, b)
+    assert got[1] == ref[1]
+    np.testing.assert_array_equal(sizes, np.arange(5, dtype=np.float64))
+    np.testing.assert_array_equal(c, np.full(3, np.float32(2.0) * np.float32(1.0 / (8 * 8_388_608 + 3))))
+    assert train["backend"] == "nccl" and train["env_steps"] > 0 and "error" not in train

@@ -444,4 +444,12 @@ def test_packed_mask_matches_int8_mask(n, extra):
         if extra == "both_masks":
             assert torch.equal(envs[1].mask, envs[0].mask)
         resets += int(((envs[0].flags & L.F_RESET) != 0).sum())
+        if t % 25 == 24:
+            # a partial reset: the packed mask of the lanes NOT reset must keep their stepped value (the int8
+            # buffer of the packed env is stale on those lanes)
+            sel = torch.randint(0, 2, (n,), device=DEV, dtype=torch.uint8, generator=g)
+            for e in envs:
+                e.reset(seed=1000 + t, mask=sel)
+            assert torch.equal(envs[0].board, envs[1].board)
+            assert torch.equal(envs[1].action_mask, envs[0].mask), ("partial reset", t)
     assert resets > 0

@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 import torch
 
+import exact_grad as EG
 from oracle import agent_oracle as AO
 
 pytestmark = pytest.mark.gpu
@@ -93,9 +94,10 @@ def test_fused_critic_grad_matches_batched_backprop(case):
 
 @pytest.mark.parametrize("critic", [False, True], ids=["actor", "actor_critic"])
 def test_fused_grad_one_large_chunk_split_k(critic):
-    """One chunk of > 2^17 samples (the default chunk size, so a single launch): the layer-2 weight gradient then runs
-    as a split-K batched GEMM over P = m // 2048 > 64 column blocks of a1^T / d2^T (the small-batch cases above use
-    P = 2), and the kernel's column buffers are wide (ld > 2^17).  Gradients within 1e-5 of the torch backprop."""
+    """One chunk of > 17 x 8192 samples (below the default chunk size, so a single launch): the layer-2 weight
+    gradient then runs as a split-K batched GEMM over P = max(1, min(128, m // 8192)) >= 17 column blocks of
+    a1^T / d2^T (the small-batch cases above use P = 1), and the kernel's column buffers are wide (ld > 2^17).
+    Gradients within 1e-5 of the torch backprop."""
     acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.99)
     if critic:
         acfg.update(use_critic=True, critic_loss_type="mse")
@@ -141,35 +143,53 @@ def test_update_matches_oracle_unmasked():
             np.testing.assert_allclose(a.cpu().numpy(), b, rtol=1e-5, atol=2e-7)
 
 
+def _check_fused_vs_plain(runs, act):
+    """runs: {"fused" | "plain": (agent, params before the update, PatternProbe or None)} after update_from_batch on
+    the same batch.  Sigmoid: fused within 1e-5 of the torch backprop (no pattern).  ReLU: each path within 1e-5 of
+    the exact fp64 value of the formula under the ReLU pattern it computed (tests/exact_grad.py) -- at ~1e5 samples
+    the two fp32 forwards round a few pre-activations next to 0 to opposite signs, so they are not compared with
+    each other there."""
+    (fa, fp0, probe), (pa, pp0, _) = runs["fused"], runs["plain"]
+    if act == "Sigmoid":
+        for which in ("critic", "actor"):
+            for i, (a, b) in enumerate(zip(fa.last_grads[which], pa.last_grads[which])):
+                assert _rel(a.cpu().numpy(), b.cpu().numpy()) < 1e-5, (which, i)
+        return
+    assert probe.complete("actor") and probe.complete("critic")
+    errs_f = EG.grad_errors(fa.last_grads, EG.exact_update_grads(fa, runs["batch"], patterns=probe, params=fp0))
+    errs_p = EG.grad_errors(pa.last_grads, EG.exact_update_grads(pa, runs["batch"], patterns="plain", params=pp0))
+    print("\nfused vs exact under its pattern", errs_f, "\nplain vs exact under its pattern", errs_p)
+    assert all(v < 1e-5 for v in errs_f.values()), errs_f
+    assert all(v < 1e-5 for v in errs_p.values()), errs_p
+
+
 @pytest.mark.parametrize("act", ["Sigmoid", "ReLU"])
 @pytest.mark.parametrize("chunk", [4096 + 17, 8192 * 17 + 5])
 def test_fused_critic_grad_ragged_chunks(chunk, act):
     """Regression for the round-1 hipErrorIllegalAddress seen after the 256x256 critic's V(s') launch
     ("Fault audit"): every chunk of the fused critic + actor gradient is ragged (m not a
     multiple of 32, so the last 32-sample group of each launch is partial), the last chunk is short, and the
-    second size makes the split-K layer-2 GEMM run P = 68 column blocks; the device stays healthy (a
-    synchronising copy after each update).  Gradients against the torch backprop: within 1e-5 for Sigmoid; for
-    ReLU within 5e-5, because at ~150k samples the two fp32 forwards flip a few ReLU derivatives of
-    pre-activations rounded next to 0 on different samples (tests/test_gpu_configs_at_size.py measures this
-    against fp64)."""
+    second size makes the split-K layer-2 GEMM run P = 17 column blocks; the device stays healthy (a
+    synchronising copy after each update).  Gradients: _check_fused_vs_plain (1e-5)."""
     acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.97, use_critic=True, critic_loss_type="mse")
-    grads = {}
+    runs = {}
     batch = None
-    for fused in (True, False):
+    for mode in ("fused", "plain"):
         ag = _agent((256, 256), act, **acfg)
-        ag.use_fused_grad = fused
+        ag.use_fused_grad = mode == "fused"
         if batch is None:
             batch = ag.rollout_batch(list(range(3000, 3000 + 1200)), list(range(7000, 7000 + 1200)))
+            runs["batch"] = batch
+        N = int(batch.lengths.sum())
         ag.grad_chunk_steps = chunk
+        probe = EG.PatternProbe(1, N, DEV) if mode == "fused" else None
+        ag.grad_probe = probe
+        p0 = EG.snapshot(ag)
         ag.update_from_batch(batch)
         torch.cuda.synchronize()
-        grads[fused] = {k: [g.cpu().numpy() for g in v] for k, v in ag.last_grads.items()}
-    N = int(batch.lengths.sum())
+        runs[mode] = (ag, p0, probe)
     assert N % chunk and (N % chunk) % 32 and N > chunk, (N, chunk)
-    tol = 1e-5 if act == "Sigmoid" else 5e-5
-    for which in ("critic", "actor"):
-        for i, (a, b) in enumerate(zip(grads[True][which], grads[False][which])):
-            assert _rel(a, b) < tol, (which, i, _rel(a, b))
+    _check_fused_vs_plain(runs, act)
 
 
 @pytest.mark.parametrize("aug,tail", [(False, 0), (True, 0), (False, 64), (True, 100000)])
@@ -180,29 +200,29 @@ def test_fused_critic_rows_mode(act, aug, tail):
     rows, most of them ragged, a column-buffer flush forced by a small chunk -- against the torch backprop: critic
     and actor gradients and the TD errors (through the actor's advantages).  `tail`: rows below that many samples
     run as the one tail launch with its own V(s') forward (0: none; 64: the later rows, handing over to the chain;
-    100000: all rows, capped by the column buffer).  Sigmoid 1e-5; ReLU 5e-5 (fp32 ReLU derivative flips, as in
-    test_fused_critic_grad_ragged_chunks)."""
+    100000: all rows, capped by the column buffer).  Gradients: _check_fused_vs_plain (1e-5)."""
     acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.97, use_critic=True, critic_loss_type="huber",
                 huber_delta=0.5, augmentation=aug)
-    grads = {}
+    runs = {}
     batch = None
-    for mode in ("rows", "torch"):
+    for mode in ("fused", "plain"):
         ag = _agent((64, 96), act, obs_mode="log2", **acfg)
-        ag.use_fused_grad = mode == "rows"
+        ag.use_fused_grad = mode == "fused"
         ag.critic_rows_min_avg = 0
         ag.critic_tail_row_max = tail
         ag.grad_chunk_steps = 4096
         if batch is None:
             batch = ag.rollout_batch(list(range(100, 100 + 160)), list(range(900, 900 + 160)))
-        if mode == "rows":
+            runs["batch"] = batch
+        if mode == "fused":
             assert ag._critic_by_rows(_steps_of(ag, batch))
+        probe = EG.PatternProbe(8 if aug else 1, int(batch.lengths.sum()), DEV) if mode == "fused" else None
+        ag.grad_probe = probe
+        p0 = EG.snapshot(ag)
         ag.update_from_batch(batch)
         torch.cuda.synchronize()
-        grads[mode] = {k: [g.cpu().numpy() for g in v] for k, v in ag.last_grads.items()}
-    tol = 1e-5 if act == "Sigmoid" else 5e-5
-    for which in ("critic", "actor"):
-        for i, (a, b) in enumerate(zip(grads["rows"][which], grads["torch"][which])):
-            assert _rel(a, b) < tol, (which, i, _rel(a, b))
+        runs[mode] = (ag, p0, probe)
+    _check_fused_vs_plain(runs, act)
 
 
 def _steps_of(agent, batch):

@@ -19,6 +19,7 @@ import numpy as np
 import pytest
 import torch
 
+import exact_grad as EG
 import ref_fixtures as RF
 from oracle import oracle as O
 
@@ -303,6 +304,8 @@ def test_update_matches_reference_update_batch(ci, path):
     lr = case["agent"].get("learning_rate", 1e-3)
     lr_c = case["agent"].get("critic_learning_rate", 1e-3)
     adam = case["agent"].get("optimizer", "sgd") == "adam"
+    b1, b2 = case["agent"].get("adam_beta1", 0.9), case["agent"].get("adam_beta2", 0.999)
+    mx = case["agent"].get("max_grad_norm", 1.0)
     noisy_a = noisy_c = None
     for u in range(case["updates"]):
         P = f"up{u}_"
@@ -316,6 +319,8 @@ def test_update_matches_reference_update_batch(ci, path):
         before = [p.cpu().numpy().copy() for p in agent.params["W"] + agent.params["b"]]
         cbefore = [p.cpu().numpy().copy() for p in agent.critic_params["W"] + agent.critic_params["b"]] if crit \
             else None
+        ast = RF.adam_state(agent) if adam else None
+        cst = RF.adam_state(agent, critic=True) if adam and crit else None
         if path == "device":
             stats = agent.update_from_batch(_batch_from_fixture(ci, u))
         else:
@@ -328,8 +333,11 @@ def test_update_matches_reference_update_batch(ci, path):
         nref = float(RF.arr(ci, P + "actor_norm"))
         RF.assert_norm_parity(stats["actor_grad_norm"], nref, lambda: exact()["actor"], (u, "actor norm"))
         ref, rb = RF.params_of(ci, P + "actor", L), _params_before(ci, u, L, "actor")
-        noisy_a = assert_step_matches([p.cpu().numpy() for p in agent.params["W"] + agent.params["b"]], before,
-                                      ref["W"] + ref["b"], rb["W"] + rb["b"], gref, noisy_a, lr, adam)
+        after = [p.cpu().numpy() for p in agent.params["W"] + agent.params["b"]]
+        noisy_a = assert_step_matches(after, before, ref["W"] + ref["b"], rb["W"] + rb["b"], gref, noisy_a, lr, adam)
+        if adam:
+            RF.assert_adam_step_exact(after, before, [g.cpu().numpy() for g in agent.last_grads["actor"]], ast, lr, 1.0,
+                                      b1, b2, mx, (u, "actor"))
         if crit:
             cref = [RF.arr(ci, P + f"critic_grad_{j}") for j in range(2 * L)]
             for j, (g, r) in enumerate(zip(agent.last_grads["critic"], cref)):
@@ -337,9 +345,12 @@ def test_update_matches_reference_update_batch(ci, path):
             cn = float(RF.arr(ci, P + "critic_norm"))
             RF.assert_norm_parity(stats["critic_grad_norm"], cn, lambda: exact()["critic"], (u, "critic norm"))
             ref, rb = RF.params_of(ci, P + "critic", L), _params_before(ci, u, L, "critic")
-            noisy_c = assert_step_matches(
-                [p.cpu().numpy() for p in agent.critic_params["W"] + agent.critic_params["b"]], cbefore,
-                ref["W"] + ref["b"], rb["W"] + rb["b"], cref, noisy_c, lr_c, adam)
+            cafter = [p.cpu().numpy() for p in agent.critic_params["W"] + agent.critic_params["b"]]
+            noisy_c = assert_step_matches(cafter, cbefore, ref["W"] + ref["b"], rb["W"] + rb["b"], cref, noisy_c, lr_c,
+                                          adam)
+            if adam:
+                RF.assert_adam_step_exact(cafter, cbefore, [g.cpu().numpy() for g in agent.last_grads["critic"]], cst,
+                                          lr_c, -1.0, b1, b2, mx, (u, "critic"))
 
 
 def test_returns_and_rank_weights_match_reference():
@@ -373,7 +384,32 @@ def test_runner_matches_reference_training_and_evaluation(tmp_path):
     try:
         R.apply_config_overrides_from_dict(conf)
         agent, ec, mc, ac, tc = R.build_training_components(DEV)
+        acfg = conf["agent"]
+        lr = acfg["learning_rate"]
+        update = agent.update_from_batch
+        checked = []
+
+        def checked_update(batch):
+            # every update on the exact basis: pre-clip gradients within 1e-5 of the fp64 formula under the fused
+            # kernels' ReLU pattern, and the Adam step == the fp64 Adam formula on those gradients
+            p0, st = EG.snapshot(agent), RF.adam_state(agent)
+            before = [p.cpu().numpy().copy() for p in agent.params["W"] + agent.params["b"]]
+            probe = EG.PatternProbe(1, int(batch.lengths.sum()), DEV)
+            agent.grad_probe = probe
+            stats = update(batch)
+            agent.grad_probe = None
+            errs = EG.grad_errors(agent.last_grads, EG.exact_update_grads(agent, batch, patterns=probe, params=p0))
+            assert all(v < 1e-5 for v in errs.values()), (len(checked), errs)
+            RF.assert_adam_step_exact([p.cpu().numpy() for p in agent.params["W"] + agent.params["b"]], before,
+                                      [g.cpu().numpy() for g in agent.last_grads["actor"]], st, lr, 1.0, 0.9, 0.999,
+                                      1.0, ("runner update", len(checked)))
+            checked.append(errs)
+            return stats
+
+        agent.update_from_batch = checked_update
         rows = R.training_loop(agent, ec, mc, ac, tc, tmp_path, "golden")
+        agent.update_from_batch = update
+        assert len(checked) == 3
         assert [r["batch"] for r in rows] == list(d["train_batch"])
         for k in ("avg_reward", "max_reward", "min_reward"):
             np.testing.assert_array_equal([r[k] for r in rows], d["train_" + k], err_msg=k)
@@ -381,9 +417,17 @@ def test_runner_matches_reference_training_and_evaluation(tmp_path):
         header = (tmp_path / "training_stats.csv").read_text().splitlines()[0].split(",")
         assert header == json.loads(str(d["train_csv_header"]))
         L = len(agent.params["W"])
+        # the final actor against the reference runner's: after 3 Adam updates, each verified above on the exact
+        # basis, the two can differ only by the steps of elements whose gradient is rounding noise (either sign,
+        # each at most ~lr in magnitude): every element within 3 such steps; the measured difference is printed
+        rels = []
         for j, p in enumerate(agent.params["W"] + agent.params["b"]):
             r = d[f"train_final_actor_{j}"]
-            assert RF.rel(p.cpu().numpy(), r) < 1e-4, j
+            diff = np.abs(p.cpu().numpy().astype(np.float64) - r)
+            assert diff.max() <= 3 * 2 * lr, (j, diff.max())
+            rels.append(RF.rel(p.cpu().numpy(), r))
+        print("\nrunner final actor vs the reference's (normwise per tensor):", rels, "per-update gradient errors:",
+              checked)
         for gi, greedy in enumerate((True, False)):
             s = R.evaluation_loop(agent, dict(conf["eval"], use_greedy=greedy))
             assert s["episodes"] == int(d[f"eval{gi}_episodes"])
