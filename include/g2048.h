@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 8
+#define G2048_ABI_VERSION 9
 
 /* status codes */
 #define G2048_OK 0
@@ -171,8 +171,9 @@ int g2048_sample(const float* logits, const int8_t* mask, const uint32_t* lane_s
                  const uint64_t* lane_seed, float* probs_out, uint8_t* actions, int64_t n, void* stream);
 
 /* Discounted returns per episode (ReinforceAgent.compute_returns src/reinforce_agent.py:255-273):
- * rewards / returns are time-major [T, n] fp32 (lane i's episode occupies rows 0..lengths[i]-1); the scan is
- * accumulated in fp64 like the reference's Python float and stored as fp32. */
+ * rewards [T, n] fp64 (the Python floats Game2048Env.step returns) and returns [T, n] fp32, both time-major (lane
+ * i's episode occupies rows 0..lengths[i]-1); the scan is accumulated in fp64 like the reference's Python float
+ * and stored as fp32. */
 int g2048_returns(const double* rewards, const int32_t* lengths, double gamma, float* returns, int64_t T,
                   int64_t n, void* stream);
 
@@ -248,6 +249,16 @@ int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int
                       const float* weight, float* delta_out, float* value_out, int64_t n, int64_t ld, int64_t col_off,
                       int64_t ncols, float* a1t, float* d2t, float* partials, int accumulate, int64_t waves,
                       void* stream);
+
+/* The layer-2 weight / bias gradient of the fused update (the a1 d2^T outer products of _backpropagation,
+ * src/reinforce_agent.py:639-678, summed over samples): over the columns [col0, col0 + ncols) of the column
+ * buffers g2048_actor_grad / g2048_critic_grad write -- a1t [H1p + 1][ld] (its last row is not read) and d2t
+ * [H2p][ld] -- partials[p] [H1p + 1][H2p] fp32 = sum over the columns [col0 + p cols_per_part, ...) of a1 d2^T
+ * (rows 0..H1p-1, dW2) and of d2 (row H1p, db2); the caller sums the nparts = ceil(ncols / cols_per_part) slabs.
+ * Columns must hold zeros in d2t where no sample is (padding).  ld, col0, ncols, cols_per_part multiples of 16.
+ * fp32-accurate: each operand split exactly into three bf16 planes, six plane products on the bf16 MFMA. */
+int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int64_t ld, int64_t col0, int64_t ncols,
+              int64_t cols_per_part, float* partials, int64_t nparts, void* stream);
 
 /* The whole batched rollout in one launch: ReinforceAgent.run_episode (src/reinforce_agent.py:195-252) for n
  * (env_seed, policy_seed) pairs -- select_action (the fused policy above) + Game2048Env.step until terminated or

@@ -18,9 +18,9 @@ REPO_ROOT = os.path.dirname(PKG_DIR)
 SHIPPED_LIB = os.path.join(PKG_DIR, "libg2048.so")
 LIB_PATH = SHIPPED_LIB
 SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
-SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip")]
+SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip"), os.path.join(PKG_DIR, "csrc", "g2048_dw2.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # include/g2048.h constants
 OBS_NONE, OBS_RAW, OBS_LOG2, OBS_ONEHOT = -1, 0, 1, 2
@@ -34,17 +34,58 @@ MAX_STEPS_LIMIT = 0x000FFFFF
 G2048_OK, G2048_EINVAL, G2048_EHIP, G2048_ENOINIT = 0, 1, 2, 3
 
 
-def build(verbose: bool = False) -> str:
-    """Compile libg2048.so for gfx950 in-tree (hipcc cross-compiles; no GPU needed)."""
-    # -ffp-contract=off: the fp64 reward keeps the reference's separately rounded multiply and add (no FMA)
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", "-I" + INCLUDE,
-           "-I" + os.path.dirname(SRC), "-o", SHIPPED_LIB] + SOURCES
+CSRC = os.path.join(PKG_DIR, "csrc")
+BUILD_DIR = os.path.join(PKG_DIR, "build")
+# -ffp-contract=off: the fp64 reward keeps the reference's separately rounded multiply and add (no FMA)
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC"]
+
+
+def _object_for(src: str, flags: list[str]) -> str:
+    """build/<tu>-<hash>.o: keyed by the TU, every header it may include and the flags (incremental builds)."""
+    import hashlib
+
+    h = hashlib.sha256(" ".join(flags).encode())
+    hdrs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc")))
+    for f in [src] + hdrs + [os.path.join(INCLUDE, "g2048.h")]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return os.path.join(BUILD_DIR, f"{os.path.splitext(os.path.basename(src))[0]}-{h.hexdigest()[:16]}.o")
+
+
+def build(verbose: bool = False, out: str | None = None, defines: tuple[str, ...] = (),
+          define_tus: tuple[str, ...] | None = None) -> str:
+    """Compile libg2048.so for gfx950 in-tree (hipcc cross-compiles; no GPU needed).  Every TU is compiled to an
+    object in parallel (cached under build/ by content hash), then linked.  out / defines (applied to the TUs
+    named in define_tus, default all): tools-only variant builds (e.g. the -DG2048_DIAG=1 timing build); the
+    product is the default."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    base_flags = HIPCC_FLAGS + ["-I" + INCLUDE, "-I" + CSRC]
+
+    def compile_one(src):
+        use_defs = define_tus is None or os.path.basename(src) in define_tus
+        flags = base_flags + ([f"-D{d}" for d in defines] if use_defs else [])
+        obj = _object_for(src, flags)
+        if not os.path.exists(obj):
+            tmp = obj + f".tmp{os.getpid()}"
+            cmd = ["hipcc"] + flags + ["-c", src, "-o", tmp]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+            os.replace(tmp, obj)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    target = out or SHIPPED_LIB
+    cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", target] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
+        raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
     if verbose:
         print(" ".join(cmd))
-    return SHIPPED_LIB
+    return target
 
 
 class EnvCfg(ctypes.Structure):
@@ -101,9 +142,11 @@ def _declare(L):
     L.g2048_actor_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, vp, vp, vp, i64, i64, vp, vp, vp, i64, vp]
     L.g2048_critic_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, f, vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, vp,
                                     vp, i32, i64, vp]
+    L.g2048_dw2.argtypes = [vp, vp, i32, i32, i64, i64, i64, i64, vp, i64, vp]
     for name in ("g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step", "g2048_obs", "g2048_move",
                  "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy",
-                 "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad"):
+                 "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad",
+                 "g2048_dw2"):
         getattr(L, name).restype = ctypes.c_int
 
 
@@ -111,7 +154,7 @@ EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g204
                     "g2048_step", "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries",
                     "g2048_policy_packed_size", "g2048_policy_pack", "g2048_policy", "g2048_rollout",
                     "g2048_grad_packed_size", "g2048_grad_partial_size", "g2048_grad_pack", "g2048_actor_grad_waves",
-                    "g2048_actor_grad", "g2048_critic_grad")
+                    "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2")
 
 
 def lib():

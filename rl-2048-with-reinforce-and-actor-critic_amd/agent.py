@@ -410,6 +410,24 @@ class ReinforceAgent:
             entry[1] = key
         return entry[0]
 
+    # columns per g2048_dw2 workgroup: one workgroup per CU at 2^20 columns, never fewer than this many columns each
+    dw2_min_cols_per_part = 2048
+
+    def _dw2(self, a1t: torch.Tensor, d2t: torch.Tensor, h1: int, h2: int, ncols: int) -> torch.Tensor:
+        """dW2 / db2 of the columns [0, ncols) of the fused kernels' column buffers (g2048_dw2: the a1 d2^T outer
+        products on the bf16 MFMA with three-plane fp32-accurate operands, split over workgroups); returns the fp64
+        sum of the workgroup slabs, [H1p + 1, H2p] (row H1p = db2)."""
+        H1p, H2p = _padded_units(h1), _padded_units(h2)
+        if ncols == 0:
+            return torch.zeros(H1p + 1, H2p, dtype=torch.float64, device=self.device)
+        cus = int(self._lib.g2048_actor_grad_waves()) // 4
+        cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * cus)) * 16)
+        nparts = -(-ncols // cpp)
+        part = torch.empty(nparts, H1p + 1, H2p, dtype=torch.float32, device=self.device)
+        L.check(self._lib.g2048_dw2(L.ptr(a1t), L.ptr(d2t), h1, h2, int(a1t.shape[1]), 0, ncols, cpp, L.ptr(part),
+                                    nparts, self._stream))
+        return part.sum(0, dtype=torch.float64)
+
     def _actor_grad_fused(self, steps: "_Steps", adv: torch.Tensor, step_w: torch.Tensor, K: int,
                           gW: list[torch.Tensor], gb: list[torch.Tensor], spec) -> None:
         """The actor branch of update_batch (src/reinforce_agent.py:502-555) for every valid step and symmetry k:
@@ -530,15 +548,7 @@ class ReinforceAgent:
                                     a1t[:, c0:c0 + cnt_], d2t[:, c0:c0 + cnt_])
             launched.clear()
             fold()
-            m = -(-used // blk) * blk
-            a1t[:, used:m].zero_()
-            d2t[:, used:m].zero_()
-            P = 1
-            while P < 128 and m // (2 * P) >= 8192:
-                P *= 2
-            q = m // P
-            big += torch.bmm(a1t[:, :m].view(H1p + 1, P, q).transpose(0, 1),
-                             d2t[:, :m].view(H2p, P, q).permute(1, 2, 0)).sum(0)
+            big += self._dw2(a1t, d2t, h1, h2, used)   # every column < used was written by a row launch
 
         def grad_launch(s0: int, cnt: int, tgt: torch.Tensor, k: int) -> None:
             nonlocal col, since_fold
@@ -625,20 +635,14 @@ class ReinforceAgent:
                 b = flat[steps.vidx[sel]].contiguous()
                 if k:
                     b = self._symmetry_boards(b, k)
-                # split-K of the layer-2 weight gradient over P column blocks (a strided-batched fp32 GEMM; at most
-                # 128 blocks of >= 8192 samples: 132 TFLOP/s at 2^20 columns against 121 at 64 blocks, 56 at 16 and
-                # 25 unsplit -- tools/dw2_gemm_probe.py, profiles/round2/dw2_gemm_probe.log; the gradient's fp32
-                # error at millions of samples is set by ReLU-derivative flips, not by this accumulation --
-                # tests/test_gpu_configs_at_size.py), blocks summed in fp32, chunks accumulated in fp64
-                P = max(1, min(128, m // 8192))
-                ld = -(-m // (32 * P)) * 32 * P
-                q = ld // P
+                # column buffers: the kernel writes every column < ld (those past m as zero-coefficient padding)
+                ld = -(-m // 32) * 32
                 a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
                 d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
                 launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale)
                 if self.grad_probe is not None:
                     self.grad_probe(slot, k, sel, a1t[:, :m], d2t[:, :m])
-                big += torch.bmm(a1t.view(H1p + 1, P, q).transpose(0, 1), d2t.view(H2p, P, q).permute(1, 2, 0)).sum(0)
+                big += self._dw2(a1t, d2t, h1, h2, ld)     # layer-2 weight + bias gradient, chunks summed in fp64
                 small += part.sum(0)
         big, small = big.to(torch.float32), small.to(torch.float32)
         gW[0] += small[:16 * H1p].view(16, H1p)[:, :h1]

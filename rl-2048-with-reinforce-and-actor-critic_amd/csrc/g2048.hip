@@ -57,16 +57,6 @@ int fail(int code, const std::string& msg) {
 #define G2048_DIAG 0
 #endif
 
-// Step-kernel prefetch ring: 3 register buffers (loads two sweeps ahead) or 4 (three sweeps ahead).
-#ifndef G2048_STEP_DEPTH
-#define G2048_STEP_DEPTH 3
-#endif
-
-// Step-kernel move: 0 = the two LDS row tables (board_move_coded), 1 = table-free (board_move_alu: no LDS tables,
-// no table fill; the LDS then holds only the deferred-reset list).
-#ifndef G2048_STEP_ALU
-#define G2048_STEP_ALU 0
-#endif
 
 #if G2048_DIAG
 // per-workgroup phase timestamps of the last step launch (s_memrealtime, 100 MHz): entry, tables filled,
@@ -103,13 +93,9 @@ __device__ __forceinline__ void st(T* p, uint32_t idx, T v) {
 
 // observation stores are non-temporal (streaming): measured on MI355X, onehot obs (1,088 B/board) 260 -> 241 us at
 // 1M boards and 1050 -> 908 us at 4M; log2 obs unchanged (tools/ab_nt.sh, profiles/round1/ab_nt.log)
-#ifndef G2048_OBS_NT
-#define G2048_OBS_NT 1
-#endif
-__device__ __forceinline__ void st_obs(float4* p, float4 v) {
+__device__ __forceinline__ void st_obs(float4* base, int q, float4 v) {
     typedef float f4v __attribute__((ext_vector_type(4)));
-    if constexpr (G2048_OBS_NT) __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
-    else *p = v;
+    __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(base + q));
 }
 
 struct LineFn {
@@ -154,7 +140,7 @@ __device__ inline void write_obs_wave(float* __restrict__ obs, uint32_t w0, uint
                 v.y = (j + 1 == p0 || j + 1 == p1) ? 1.0f : 0.0f;
                 v.z = (j + 2 == p0 || j + 2 == p1) ? 1.0f : 0.0f;
                 v.w = (j + 3 == p0 || j + 3 == p1) ? 1.0f : 0.0f;
-                st_obs(dst + q, v);
+                st_obs(dst, q, v);
             }
         }
     } else if constexpr (OBS == G2048_OBS_LOG2 || OBS == G2048_OBS_RAW) {
@@ -174,7 +160,7 @@ __device__ inline void write_obs_wave(float* __restrict__ obs, uint32_t w0, uint
                     if constexpr (OBS == G2048_OBS_LOG2) v[t] = (float)e * scale;
                     else v[t] = e ? (float)(1u << e) : 0.0f;
                 }
-                st_obs(dst + q, make_float4(v[0], v[1], v[2], v[3]));
+                st_obs(dst, q, make_float4(v[0], v[1], v[2], v[3]));
             }
         }
     }
@@ -345,11 +331,7 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
         s = MoveSummary{0, 0, 0, 0, 0, 0};
         m = b ^ ((uint64_t)x.act << 60);
     } else {
-#if G2048_STEP_ALU
-        m = board_move_alu<LIST>(b, x.act, s);
-#else
         m = board_move_coded<LIST>(b, x.act, lut, code, s);
-#endif
     }
     const bool changed = m != b;
     if (changed && !(G2048_DIAG && (a.diag & 4))) {
@@ -415,11 +397,7 @@ __device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, 
 }
 
 // LDS reuse after the last sweep: the block's reset list (counter, lane indices, previous seeds)
-#if G2048_STEP_ALU
-constexpr int kStepLdsBytes = 24576;        // the reset list only
-#else
 constexpr int kStepLdsBytes = kTabBytes;    // the row tables, then (after the last sweep) the reset list
-#endif
 constexpr int kStepLdsVec = kStepLdsBytes / 16;
 constexpr int kResetCap = (kStepLdsBytes - 16) / 12;
 static_assert(16 + kResetCap * 4 + kResetCap * 8 <= kStepLdsBytes, "reset list fits the LDS area");
@@ -454,15 +432,10 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     uint32_t w0 = w_first, w1 = w_first + wstride;
     load_lane<RNG>(a, lane_at(w0), A);
     load_lane<RNG>(a, lane_at(w1), B);
-#if G2048_STEP_DEPTH == 4
-    LaneIn D;
-    uint32_t w2 = w1 + wstride;
-    load_lane<RNG>(a, lane_at(w2), C);
-#endif
     const uint8_t* tab = a.tab;
     if constexpr (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(a.tab);
-        if (!G2048_STEP_ALU && !(G2048_DIAG && (a.diag & 1))) {
+        if (!(G2048_DIAG && (a.diag & 1))) {
             constexpr uint32_t kChunks = kTabVec / kBlock;
             const uint32_t rot = blockIdx.x % kChunks;
 #pragma unroll
@@ -481,29 +454,6 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     const CodeFn code{tab + 2 * kLines};
     uint64_t pending = 0, pseed = 0;
     uint32_t k = 0;
-#if G2048_STEP_DEPTH == 4
-    while (w0 < a.n) {                         // wave-uniform; loads three sweeps ahead
-        const uint32_t w3 = w2 + wstride;
-        load_lane<RNG>(a, lane_at(w3), D);
-        sweep<OBS, RNG, XO>(a, w0, lane, A, lut, code, pending, pseed, k);
-        if (w1 >= a.n) break;
-        const uint32_t w4 = w3 + wstride;
-        load_lane<RNG>(a, lane_at(w4), A);
-        sweep<OBS, RNG, XO>(a, w1, lane, B, lut, code, pending, pseed, k + 1);
-        if (w2 >= a.n) break;
-        const uint32_t w5 = w4 + wstride;
-        load_lane<RNG>(a, lane_at(w5), B);
-        sweep<OBS, RNG, XO>(a, w2, lane, C, lut, code, pending, pseed, k + 2);
-        if (w3 >= a.n) break;
-        const uint32_t w6 = w5 + wstride;
-        load_lane<RNG>(a, lane_at(w6), C);
-        sweep<OBS, RNG, XO>(a, w3, lane, D, lut, code, pending, pseed, k + 3);
-        w0 = w4;
-        w1 = w5;
-        w2 = w6;
-        k += 4;
-    }
-#else
     while (w0 < a.n) {                         // wave-uniform
         const uint32_t w2 = w1 + wstride;
         load_lane<RNG>(a, lane_at(w2), C);
@@ -520,7 +470,6 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
         w1 = w4;
         k += 3;
     }
-#endif
     if (G2048_DIAG && (a.diag & 2)) pending = 0;
     if constexpr (LDS) {
         uint32_t* cnt = reinterpret_cast<uint32_t*>(tab_lds);

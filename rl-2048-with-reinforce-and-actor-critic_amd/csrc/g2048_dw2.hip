@@ -1,0 +1,239 @@
+// g2048_dw2.hip -- the layer-2 weight / bias gradient of the fused update (part of libg2048.so).
+//
+// update_batch accumulates, per valid step, the outer product a1 d2^T into dW2 and d2 into db2
+// (src/reinforce_agent.py:536-555 -> _backpropagation :639-678).  The fused gradient kernels (g2048_policy.hip)
+// write every sample's a1 and d2 as columns of a1^T [H1p + 1][ld] and d2^T [H2p][ld]; this kernel sums
+// dW2 = a1^T d2 over a column range and db2 = the row sums of d2^T, split over workgroups (one fp32 partial
+// [H1p + 1][H2p] slab per workgroup, rows 0..H1p-1 = dW2, row H1p = db2; the caller sums the slabs in fp64).
+//
+// gfx950 design: the product is HBM-bound at 2 KiB of columns per sample only if the arithmetic runs faster than
+// the fp32 MFMA (64 FLOP/clk/SIMD would make it compute-bound at 2x the HBM time).  Every fp32 operand is split
+// exactly into three bf16 planes (x = x0 + x1 + x2, 8 significant bits each) and the six plane products of order
+// <= 2 run on v_mfma_f32_32x32x16_bf16 (16x the fp32 MFMA rate) into fp32 accumulators: fp32-accurate products
+// (the dropped terms are < 2^-24 |x y|), at 6 x 32 cycles per 32x32x16 step against 8 x 64 for fp32 MFMA.
+// Columns are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4), 16 samples per stage, 4 stages with two
+// in flight (counted vmcnt + raw barrier); the 16-B chunks of a staged row are XOR-swizzled by row so that the
+// fragment reads (ds_read_b128) are bank-conflict free.  One 256-thread workgroup per CU: the 4 waves own 2 x 2
+// blocks of the output tiles (4 x 4 tiles of 32 x 32, 256 accumulator registers each for a 256 x 256 layer).
+#include <hip/hip_runtime.h>
+
+#include "g2048.h"
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int kBK = 16;        // samples (columns) per stage = one 32x32x16 MFMA k-step
+constexpr int kStages = 4;     // LDS ring; two stages in flight while one is read
+constexpr int kThreads = 256;  // 4 waves
+
+__host__ __device__ inline int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// one LDS-DMA of 16 B per lane: lane l's 16 bytes land at lds_wave_base + 16 l (lds_wave_base wave-uniform).
+// Device-only body: the host pass of a template kernel that names the address-space-3 cast drops the kernel's
+// host stub without a diagnostic.
+__device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
+#else
+    (void)src;
+    (void)lds_wave_base;
+#endif
+}
+
+template <int NT1, int NT2>
+struct Dw2 {
+    static constexpr int H1 = 32 * NT1, H2 = 32 * NT2;
+    static constexpr int kRows = H1 + H2;               // staged rows: a1 rows, then d2 rows
+    static constexpr int kStageFloats = kRows * kBK;    // 64 B per staged row
+    static constexpr int kGlds = kRows / 16;            // 1 KiB LDS-DMA instructions per stage (16 rows each)
+    static constexpr int kGldsPerWave = (kGlds + 3) / 4;
+    static constexpr int TR = NT1 >= 2 ? NT1 / 2 : 1;   // row tiles per wave (2 x 2 wave grid)
+    static constexpr int TC = NT2 >= 2 ? NT2 / 2 : 1;   // column tiles per wave
+};
+
+struct Dw2Args {
+    const float* a1t;   // [H1p + 1][ld]
+    const float* d2t;   // [H2p][ld]
+    float* part;        // [nparts][H1p + 1][H2p]
+    uint32_t ld, col0, ncols, kb;   // column range [col0, col0 + ncols); workgroup p takes kb columns from col0 + p kb
+};
+
+// exact split of 8 fp32 values into three bf16 planes (round to nearest even at each step)
+__device__ __forceinline__ void split3(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const __bf16 h = (__bf16)v[j];
+        const float r = v[j] - (float)h;
+        const __bf16 m = (__bf16)r;
+        const float r2 = r - (float)m;
+        p0[j] = h;
+        p1[j] = m;
+        p2[j] = (__bf16)r2;
+    }
+}
+
+// 8 consecutive columns k = 8h .. 8h+7 of staged row `row` (two 16-B chunks, swizzled slot = chunk ^ ((row >> 2) & 3))
+__device__ __forceinline__ void read_frag(const float* stage, int row, int h, float (&v)[8]) {
+    const int f = (row >> 2) & 3;
+    const float4 x = *reinterpret_cast<const float4*>(stage + row * kBK + (((2 * h) ^ f) << 2));
+    const float4 y = *reinterpret_cast<const float4*>(stage + row * kBK + (((2 * h + 1) ^ f) << 2));
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+}
+
+template <int NT1, int NT2>
+__global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
+    using G = Dw2<NT1, NT2>;
+    __shared__ float S[kStages * G::kStageFloats];   // the only LDS object (see the glds / second-object rule)
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, r = lane & 31;
+    const int wr = w >> 1, wc = w & 1;
+    const uint32_t k_begin = a.col0 + blockIdx.x * a.kb;
+    const uint32_t k_end = min(k_begin + a.kb, a.col0 + a.ncols);
+    const int iters = k_end > k_begin ? (int)((k_end - k_begin) / kBK) : 0;
+
+    // this lane's LDS-DMA sources: instruction g (wave w issues g = w, w + 4, ...; past the end: the last one
+    // again, an identical rewrite) covers staged rows 16 g .. 16 g + 15; lane -> row 16 g + (lane >> 2), slot
+    // lane & 3, which holds the row's chunk (slot ^ ((row >> 2) & 3))
+    const float* src[G::kGldsPerWave];
+#pragma unroll
+    for (int i = 0; i < G::kGldsPerWave; i++) {
+        int g = w + 4 * i;
+        g = g < G::kGlds ? g : G::kGlds - 1;
+        const int row = 16 * g + (lane >> 2);
+        const int chunk = (lane & 3) ^ ((lane >> 4) & 3);
+        const float* base = row < G::H1 ? a.a1t + (size_t)row * a.ld : a.d2t + (size_t)(row - G::H1) * a.ld;
+        src[i] = base + k_begin + 4 * chunk;
+    }
+    const auto issue = [&](int stage_idx) {
+        float* dst = S + (stage_idx % kStages) * G::kStageFloats;
+#pragma unroll
+        for (int i = 0; i < G::kGldsPerWave; i++) {
+            int g = w + 4 * i;
+            g = g < G::kGlds ? g : G::kGlds - 1;
+            glds16(src[i] + (size_t)stage_idx * kBK, dst + 16 * g * kBK);
+        }
+    };
+
+    floatx16 acc[G::TR][G::TC];
+#pragma unroll
+    for (int i = 0; i < G::TR; i++)
+#pragma unroll
+        for (int j = 0; j < G::TC; j++) acc[i][j] = floatx16{};
+    const bool rows_mine = NT1 >= 2 || wr == 0, cols_mine = NT2 >= 2 || wc == 0;
+    float dsum = 0.0f;   // db2: thread t sums d2 row t
+
+    if (iters > 0) issue(0);
+    if (iters > 1) issue(1);
+    for (int it = 0; it < iters; it++) {
+        if (it + 2 < iters) {
+            issue(it + 2);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::kGldsPerWave) : "memory");
+        } else if (it + 1 < iters) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::kGldsPerWave) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const float* st = S + (it % kStages) * G::kStageFloats;
+        if (t < G::H2) {   // db2
+            const float* rowp = st + (G::H1 + t) * kBK;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const float4 x = *reinterpret_cast<const float4*>(rowp + 4 * c);
+                dsum += ((x.x + x.y) + x.z) + x.w;
+            }
+        }
+        if (rows_mine && cols_mine) {
+            bf16x8 a0[G::TR], a1[G::TR], a2[G::TR], b0[G::TC], b1[G::TC], b2[G::TC];
+#pragma unroll
+            for (int i = 0; i < G::TR; i++) {
+                float v[8];
+                read_frag(st, 32 * (wr * G::TR + i) + r, h, v);
+                split3(v, a0[i], a1[i], a2[i]);
+            }
+#pragma unroll
+            for (int j = 0; j < G::TC; j++) {
+                float v[8];
+                read_frag(st, G::H1 + 32 * (wc * G::TC + j) + r, h, v);
+                split3(v, b0[j], b1[j], b2[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < G::TR; i++)
+#pragma unroll
+                for (int j = 0; j < G::TC; j++) {
+                    floatx16 c = acc[i][j];   // smallest terms first
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[i], b0[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[i], b1[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b2[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[i], b0[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b1[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b0[j], c, 0, 0, 0);
+                    acc[i][j] = c;
+                }
+        }
+    }
+    // this workgroup's slab: dW2 rows from the accumulators (C/D layout: column = lane & 31, row = acc_row), db2
+    float* out = a.part + (size_t)blockIdx.x * (G::H1 + 1) * G::H2;
+    if (rows_mine && cols_mine) {
+#pragma unroll
+        for (int i = 0; i < G::TR; i++)
+#pragma unroll
+            for (int j = 0; j < G::TC; j++)
+#pragma unroll
+                for (int q = 0; q < 16; q++)
+                    out[(size_t)(32 * (wr * G::TR + i) + acc_row(q, h)) * G::H2 + 32 * (wc * G::TC + j) + r] = acc[i][j][q];
+    }
+    if (t < G::H2) out[(size_t)G::H1 * G::H2 + t] = dsum;
+}
+
+template <int NT1>
+void launch_nt2(const Dw2Args& a, int nt2, int grid, hipStream_t s) {
+    switch (nt2) {
+        case 1: hipLaunchKernelGGL((dw2_kernel<NT1, 1>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((dw2_kernel<NT1, 2>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((dw2_kernel<NT1, 4>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        default: hipLaunchKernelGGL((dw2_kernel<NT1, 8>), dim3(grid), dim3(kThreads), 0, s, a); break;
+    }
+}
+
+int tiles_of(int hsize) {   // as g2048_policy.hip: 32-unit tiles rounded up to 1, 2, 4 or 8
+    const int t = (hsize + 31) / 32;
+    return t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : 8;
+}
+
+}  // namespace
+
+namespace g2048_internal {
+int set_error(int code, const char* msg);
+}
+
+extern "C" int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int64_t ld, int64_t col0, int64_t ncols,
+                         int64_t cols_per_part, float* partials, int64_t nparts, void* stream) {
+    using g2048_internal::set_error;
+    if (h1 < 1 || h1 > 256 || h2 < 1 || h2 > 256) return set_error(G2048_EINVAL, "dw2: hidden sizes must be in 1..256");
+    if (!a1t || !d2t || !partials) return set_error(G2048_EINVAL, "dw2: NULL buffer");
+    if (ld <= 0 || (ld & 15) || ld > ((int64_t)1 << 28)) return set_error(G2048_EINVAL, "dw2: ld must be a positive multiple of 16");
+    if (col0 < 0 || (col0 & 15) || ncols < 0 || (ncols & 15) || col0 + ncols > ld)
+        return set_error(G2048_EINVAL, "dw2: column range must be multiples of 16 inside ld");
+    if (cols_per_part <= 0 || (cols_per_part & 15)) return set_error(G2048_EINVAL, "dw2: cols_per_part must be a positive multiple of 16");
+    if (nparts != (ncols + cols_per_part - 1) / cols_per_part || nparts > 65535)
+        return set_error(G2048_EINVAL, "dw2: nparts must be ceil(ncols / cols_per_part) (<= 65535)");
+    if (nparts == 0) return G2048_OK;
+    Dw2Args a{a1t, d2t, partials, (uint32_t)ld, (uint32_t)col0, (uint32_t)ncols, (uint32_t)cols_per_part};
+    const int nt1 = tiles_of(h1), nt2 = tiles_of(h2);
+    hipStream_t s = (hipStream_t)stream;
+    const int grid = (int)nparts;
+    switch (nt1) {
+        case 1: launch_nt2<1>(a, nt2, grid, s); break;
+        case 2: launch_nt2<2>(a, nt2, grid, s); break;
+        case 4: launch_nt2<4>(a, nt2, grid, s); break;
+        default: launch_nt2<8>(a, nt2, grid, s); break;
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(G2048_EHIP, hipGetErrorString(e));
+    return G2048_OK;
+}

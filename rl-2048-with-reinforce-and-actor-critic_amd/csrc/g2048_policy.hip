@@ -26,15 +26,11 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-// grad_kernel column stores.  0 = each phase stores its own columns (a1^T after layer 1, d2^T after d2): with one
-// wave per SIMD the wave then stalls on the VMEM queue (vmcnt caps outstanding ops at 63) while 128 stores per
-// lane drain.  The other modes issue them inside the MFMA loops that follow, so they drain under the MFMAs:
-// 2 = the d2^T values through the d1 loop (2 per k-tile; they are its B operand, already in registers);
-// 3 (default) = that, and the a1^T values as the first output tile of the layer-2 loop reads them from LDS;
-// 1 = as 3 with the a1^T stores spread over every output tile -- measured: the compiler spills 122 VGPRs.
-#ifndef G2048_GRAD_SPREAD
-#define G2048_GRAD_SPREAD 3
-#endif
+// grad_kernel column stores are issued inside the MFMA loops that follow the values' computation, so they drain
+// under the MFMAs (with one wave per SIMD a phase that stores its own 128 columns per lane stalls on the VMEM
+// queue: vmcnt caps outstanding ops at 63): the d2^T values through the d1 loop (2 per k-tile; they are its B
+// operand, already in registers), the a1^T values as the first output tile of the layer-2 loop reads them from LDS
+// (DESIGN.md section 3 has the measured alternatives).
 #ifndef G2048_DIAG
 #define G2048_DIAG 0
 #endif
@@ -816,12 +812,6 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                     const float4 hv = make_float4(activate<ACT>(acc[4 * q + 0] + bv.x), activate<ACT>(acc[4 * q + 1] + bv.y),
                                                   activate<ACT>(acc[4 * q + 2] + bv.z), activate<ACT>(acc[4 * q + 3] + bv.w));
                     h1f[(t * 4 + q) * 64 + lane] = hv;
-                    if (G2048_GRAD_SPREAD != 1 && G2048_GRAD_SPREAD != 3) {
-                        col_store(ra1, 32 * t + acc_row(4 * q + 0, 0), ld4, off, hv.x);
-                        col_store(ra1, 32 * t + acc_row(4 * q + 1, 0), ld4, off, hv.y);
-                        col_store(ra1, 32 * t + acc_row(4 * q + 2, 0), ld4, off, hv.z);
-                        col_store(ra1, 32 * t + acc_row(4 * q + 3, 0), ld4, off, hv.w);
-                    }
                 }
             }
         }
@@ -845,16 +835,13 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, hb.y, acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, hb.z, acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, hb.w, acc, 0, 0, 0);
-                    if (G2048_GRAD_SPREAD == 1 || G2048_GRAD_SPREAD == 3) {
-                        // a1 value v = 4q + c of tile t goes out at output tile (v * NT2) / 16 (mode 1) or with the
-                        // first output tile (mode 3)
+                    if (o == 0) {   // the a1 values of tile t go out with the first output tile
                         const float hv[4] = {hb.x, hb.y, hb.z, hb.w};
 #pragma unroll
-                        for (int c = 0; c < 4; c++)
-                            if ((G2048_GRAD_SPREAD == 3 ? 0 : ((4 * q + c) * NT2) / 16) == o) {
-                                opaque_sgpr(ld4);
-                                col_store(ra1, 32 * t + acc_row(4 * q + c, 0), ld4, off, hv[c]);
-                            }
+                        for (int c = 0; c < 4; c++) {
+                            opaque_sgpr(ld4);
+                            col_store(ra1, 32 * t + acc_row(4 * q + c, 0), ld4, off, hv[c]);
+                        }
                     }
                 }
 #pragma unroll
@@ -956,7 +943,6 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                 dh = fmaf(g[2], wv.z, dh);
                 dh = fmaf(g[3], wv.w, dh);
                 h2[o][r] = dh * activation_derivative<ACT>(h2[o][r]);
-                if (!G2048_GRAD_SPREAD) col_store(rd2, 32 * o + acc_row(r, 0), ld4, off, h2[o][r]);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -995,14 +981,13 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].z, h2[t2][4 * q + 2], acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].w, h2[t2][4 * q + 3], acc, 0, 0, 0);
                 }
-                if (G2048_GRAD_SPREAD) {   // d2 value r of tile t2 goes out at input tile (r * NT1) / 16
+                // d2 value r of tile t2 goes out at input tile (r * NT1) / 16
 #pragma unroll
-                    for (int r = 0; r < 16; r++)
-                        if ((r * NT1) / 16 == o1) {
-                            opaque_sgpr(ld4);
-                            col_store(rd2, 32 * t2 + acc_row(r, 0), ld4, off, h2[t2][r]);
-                        }
-                }
+                for (int r = 0; r < 16; r++)
+                    if ((r * NT1) / 16 == o1) {
+                        opaque_sgpr(ld4);
+                        col_store(rd2, 32 * t2 + acc_row(r, 0), ld4, off, h2[t2][r]);
+                    }
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     fw[q] = fn[q];
