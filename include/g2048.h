@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 9
+#define G2048_ABI_VERSION 10
 
 /* status codes */
 #define G2048_OK 0
@@ -219,10 +219,11 @@ int g2048_policy(const float* packed, int h1, int h2, int activation, const uint
  * (valid steps): forward from the boards, masked softmax (use_mask: the boards' action masks, as
  * logits_to_probs src/MLP.py:139-156), g = (onehot(action) - p) * coef[i] (coef = advantage * step weight),
  * the output and input deltas and the small weight gradients, all in one kernel.  Outputs:
- *   a1t [(H1p + 1) x ld]  columns i < n: the first hidden layer's activations a1^T, then a row of ones;
- *   d2t [H2p x ld]        the second hidden layer's deltas d2^T (columns n..ld-1 of both are written as padding
- *                         with coefficient 0, so a1t d2t^T over all ld columns is the layer-2 weight gradient
- *                         [h1 x h2] in rows < h1 and the layer-2 bias gradient in row H1p);
+ *   a1t, d2t [R x ld] fp32, R = max(H1p, H2p), stored in 16-column blocks: element (row, col) at
+ *                         ((col >> 4) R + row) 16 + (col & 15).  Column i < n of a1t holds sample i's first hidden
+ *                         layer activations a1 (rows < H1p), of d2t its second hidden layer deltas d2 (rows < H2p);
+ *                         columns n..ld-1 are written as padding with coefficient 0 (d2 = 0), so g2048_dw2 over
+ *                         all ld columns gives the layer-2 weight gradient a1^T d2 and bias gradient sum d2;
  *   partials [waves x g2048_grad_partial_size]  per-wave sums: dW1 [16][H1p], db1 [H1p], dW3 [H2p][4], db3 [4].
  * H1p / H2p = hidden sizes rounded up to 32, 64, 128 or 256; ld a multiple of 32, n <= ld < 2^26;
  * waves = g2048_actor_grad_waves() (every wave writes its row); ld < 2^21 (< 2 GB column buffers). */
@@ -252,11 +253,11 @@ int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int
 
 /* The layer-2 weight / bias gradient of the fused update (the a1 d2^T outer products of _backpropagation,
  * src/reinforce_agent.py:639-678, summed over samples): over the columns [col0, col0 + ncols) of the column
- * buffers g2048_actor_grad / g2048_critic_grad write -- a1t [H1p + 1][ld] (its last row is not read) and d2t
- * [H2p][ld] -- partials[p] [H1p + 1][H2p] fp32 = sum over the columns [col0 + p cols_per_part, ...) of a1 d2^T
- * (rows 0..H1p-1, dW2) and of d2 (row H1p, db2); the caller sums the nparts = ceil(ncols / cols_per_part) slabs.
- * Columns must hold zeros in d2t where no sample is (padding).  ld, col0, ncols, cols_per_part multiples of 16.
- * fp32-accurate: each operand split exactly into three bf16 planes, six plane products on the bf16 MFMA. */
+ * buffers g2048_actor_grad / g2048_critic_grad write (a1t, d2t: see there), partials[p] [H1p + 1][H2p] fp32 = sum
+ * over the columns [col0 + p cols_per_part, ...) of a1 d2^T (rows 0..H1p-1, dW2) and of d2 (row H1p, db2); the
+ * caller sums the nparts = ceil(ncols / cols_per_part) slabs.  Columns where no sample is must hold zeros in d2t
+ * (padding).  ld, col0, ncols, cols_per_part multiples of 16.  fp32-accurate: each operand split exactly into three
+ * bf16 planes, six plane products on the bf16 MFMA. */
 int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int64_t ld, int64_t col0, int64_t ncols,
               int64_t cols_per_part, float* partials, int64_t nparts, void* stream);
 

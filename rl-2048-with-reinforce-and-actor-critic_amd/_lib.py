@@ -20,7 +20,7 @@ LIB_PATH = SHIPPED_LIB
 SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
 SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip"), os.path.join(PKG_DIR, "csrc", "g2048_dw2.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # include/g2048.h constants
 OBS_NONE, OBS_RAW, OBS_LOG2, OBS_ONEHOT = -1, 0, 1, 2

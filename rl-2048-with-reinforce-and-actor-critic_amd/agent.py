@@ -106,6 +106,13 @@ def _board_values(b: int) -> np.ndarray:
     return np.where(e > 0, np.left_shift(np.int64(1), e), 0).astype(np.int64)
 
 
+def _unblock(buf: torch.Tensor, rows: int, c0: int, m: int) -> torch.Tensor:
+    """Rows [0, rows) x columns [c0, c0 + m) of a column buffer stored in 16-column blocks (include/g2048.h) as a
+    row-major copy (diagnostics: ReinforceAgent.grad_probe)."""
+    R, ld = buf.shape
+    return buf.reshape(ld // 16, R, 16).permute(1, 0, 2).reshape(R, ld)[:rows, c0:c0 + m]
+
+
 def _padded_units(h: int) -> int:
     """Hidden units as the fused kernels pad them: whole 32-unit MFMA tiles, 1, 2, 4 or 8 of them (tiles_for in
     csrc/g2048_policy.hip)."""
@@ -219,10 +226,11 @@ class ReinforceAgent:
         # ... and the fused critic per time row, V(s') taken from the next row's pass (large batches)
         self.use_critic_rows = True
         self.grad_chunk_steps = 1 << 20
-        # diagnostics (tests): called as grad_probe(slot, k, sample_idx, a1t_cols, d2t_cols) with the column buffers
+        # diagnostics (tests): called as grad_probe(slot, k, sample_idx, a1_cols, d2_cols) with the column buffers
         # of every fused-gradient launch before they are reused -- sample_idx indexes the batch's valid steps
-        # (time-major), a1t_cols [H1p + 1, m] holds the layer-1 activations the kernel computed, d2t_cols [H2p, m]
-        # its layer-2 deltas -- so a checker can evaluate the formula under the kernel's own activation pattern
+        # (time-major), a1_cols [H1p, m] holds the layer-1 activations the kernel computed, d2_cols [H2p, m] its
+        # layer-2 deltas (row-major copies) -- so a checker can evaluate the formula under the kernel's own
+        # activation pattern
         self.grad_probe: Callable | None = None
         self._pack_cache: dict[str, list] = {}
         self._params_version = 0
@@ -420,6 +428,7 @@ class ReinforceAgent:
         H1p, H2p = _padded_units(h1), _padded_units(h2)
         if ncols == 0:
             return torch.zeros(H1p + 1, H2p, dtype=torch.float64, device=self.device)
+        assert a1t.numel() == d2t.numel() and a1t.shape[0] == max(H1p, H2p)
         cus = int(self._lib.g2048_actor_grad_waves()) // 4
         cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * cus)) * 16)
         nparts = -(-ncols // cpp)
@@ -524,8 +533,9 @@ class ReinforceAgent:
         while t_tail > 0 and counts[t_tail - 1] < self.critic_tail_row_max and tail_m + counts[t_tail - 1] <= ld - 32:
             t_tail -= 1
             tail_m += counts[t_tail]
-        a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
-        d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
+        R = max(H1p, H2p)
+        a1t = torch.empty(R, ld, dtype=torch.float32, device=self.device)     # 16-column blocks (include/g2048.h)
+        d2t = torch.empty(R, ld, dtype=torch.float32, device=self.device)
         vout = torch.empty(max(max(counts), tail_m), dtype=torch.float32, device=self.device)
         gamma = float(c.gamma)
 
@@ -545,7 +555,7 @@ class ReinforceAgent:
             if self.grad_probe is not None:
                 for k_, s0_, cnt_, c0 in launched:
                     self.grad_probe("critic", k_, torch.arange(s0_, s0_ + cnt_, device=self.device),
-                                    a1t[:, c0:c0 + cnt_], d2t[:, c0:c0 + cnt_])
+                                    _unblock(a1t, H1p, c0, cnt_), _unblock(d2t, H2p, c0, cnt_))
             launched.clear()
             fold()
             big += self._dw2(a1t, d2t, h1, h2, used)   # every column < used was written by a row launch
@@ -619,6 +629,7 @@ class ReinforceAgent:
         per-wave partials are summed; the padded gradients are cut to the net's shapes at the end."""
         h1, h2, act = spec
         H1p, H2p = _padded_units(h1), _padded_units(h2)
+        R = max(H1p, H2p)
         packed, gpacked = self._pack_net(params, spec, slot), self._pack_net(params, spec, slot, grad=True)
         waves = int(self._lib.g2048_actor_grad_waves())
         pf = int(self._lib.g2048_grad_partial_size(h1, h2))
@@ -637,11 +648,11 @@ class ReinforceAgent:
                     b = self._symmetry_boards(b, k)
                 # column buffers: the kernel writes every column < ld (those past m as zero-coefficient padding)
                 ld = -(-m // 32) * 32
-                a1t = torch.empty(H1p + 1, ld, dtype=torch.float32, device=self.device)
-                d2t = torch.empty(H2p, ld, dtype=torch.float32, device=self.device)
+                a1t = torch.empty(R, ld, dtype=torch.float32, device=self.device)     # 16-column blocks
+                d2t = torch.empty(R, ld, dtype=torch.float32, device=self.device)
                 launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale)
                 if self.grad_probe is not None:
-                    self.grad_probe(slot, k, sel, a1t[:, :m], d2t[:, :m])
+                    self.grad_probe(slot, k, sel, _unblock(a1t, H1p, 0, m), _unblock(d2t, H2p, 0, m))
                 big += self._dw2(a1t, d2t, h1, h2, ld)     # layer-2 weight + bias gradient, chunks summed in fp64
                 small += part.sum(0)
         big, small = big.to(torch.float32), small.to(torch.float32)

@@ -2,19 +2,27 @@
 //
 // update_batch accumulates, per valid step, the outer product a1 d2^T into dW2 and d2 into db2
 // (src/reinforce_agent.py:536-555 -> _backpropagation :639-678).  The fused gradient kernels (g2048_policy.hip)
-// write every sample's a1 and d2 as columns of a1^T [H1p + 1][ld] and d2^T [H2p][ld]; this kernel sums
-// dW2 = a1^T d2 over a column range and db2 = the row sums of d2^T, split over workgroups (one fp32 partial
-// [H1p + 1][H2p] slab per workgroup, rows 0..H1p-1 = dW2, row H1p = db2; the caller sums the slabs in fp64).
+// write every sample's a1 and d2 as columns of a1^T and d2^T, stored in 16-column blocks (element (row, col) at
+// ((col >> 4) R + row) 16 + (col & 15), R = max(H1p, H2p)); this kernel sums dW2 = a1^T d2 over a column range and
+// db2 = the row sums of d2^T, split over workgroups (one fp32 partial [H1p + 1][H2p] slab per workgroup, rows
+// 0..H1p-1 = dW2, row H1p = db2; the caller sums the slabs in fp64).
 //
 // gfx950 design: the product is HBM-bound at 2 KiB of columns per sample only if the arithmetic runs faster than
 // the fp32 MFMA (64 FLOP/clk/SIMD would make it compute-bound at 2x the HBM time).  Every fp32 operand is split
 // exactly into three bf16 planes (x = x0 + x1 + x2, 8 significant bits each) and the six plane products of order
 // <= 2 run on v_mfma_f32_32x32x16_bf16 (16x the fp32 MFMA rate) into fp32 accumulators: fp32-accurate products
 // (the dropped terms are < 2^-24 |x y|), at 6 x 32 cycles per 32x32x16 step against 8 x 64 for fp32 MFMA.
-// Columns are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4), 16 samples per stage, 4 stages with two
-// in flight (counted vmcnt + raw barrier); the 16-B chunks of a staged row are XOR-swizzled by row so that the
-// fragment reads (ds_read_b128) are bank-conflict free.  One 256-thread workgroup per CU: the 4 waves own 2 x 2
-// blocks of the output tiles (4 x 4 tiles of 32 x 32, 256 accumulator registers each for a 256 x 256 layer).
+// Columns are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4), 16 samples per stage -- one block of each
+// buffer, so every stage reads two contiguous runs (the row-major [row][ld] layout read 64 B from each of 512 rows
+// 4 MB apart per stage and ran at 2 TB/s) -- in a 4-slot ring with two stages in flight (counted vmcnt + raw
+// barrier); the 16-B chunks of a staged row are XOR-swizzled by row so that the fragment reads (ds_read_b128) are
+// bank-conflict free.  One 256-thread workgroup per CU: the 4 waves own 2 x 2 blocks of the output tiles (4 x 4
+// tiles of 32 x 32, 256 accumulator registers each for a 256 x 256 layer).  Software-pipelined: each loop step reads
+// and splits stage it + 1 into a second register set while the 96 MFMAs of stage it run, with the interleave pinned
+// by sched_group_barrier (8 LDS reads up front, then per MFMA one LDS read and 4 VALU) -- hipcc otherwise issues the
+// whole split (~360 VALU) ahead of the first MFMA.  Measured at 2^20 columns of a 256 x 256 layer: 905 us with the
+// split in front, 690-750 us pipelined; PMC: MFMA busy 3072 of 4090 cycles per wave-stage, the chip holding ~1.5 GHz
+// under this load (profiles/round3/).
 #include <hip/hip_runtime.h>
 
 #include "g2048.h"
@@ -23,20 +31,29 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-constexpr int kBK = 16;        // samples (columns) per stage = one 32x32x16 MFMA k-step
-constexpr int kStages = 4;     // LDS ring; two stages in flight while one is read
+constexpr int kBK = 16;                     // samples (columns) per stage = one 32x32x16 MFMA k-step
+constexpr int kAhead = 2;                   // stages in flight beyond the one being split
+constexpr int kStages = kAhead + 2;         // LDS ring (a slot is refilled two barriers after its last read)
 constexpr int kThreads = 256;  // 4 waves
 
 __host__ __device__ inline int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // one LDS-DMA of 16 B per lane: lane l's 16 bytes land at lds_wave_base + 16 l (lds_wave_base wave-uniform).
-// Device-only body: the host pass of a template kernel that names the address-space-3 cast drops the kernel's
-// host stub without a diagnostic.
+// Issued through inline asm so that hipcc does not track it: the compiler otherwise treats every pending LDS-DMA as
+// an LDS write and drains the whole ring (s_waitcnt vmcnt(0)) before each ds_read, serialising the pipeline; the
+// kernel counts these loads itself (vmcnt(N) + barrier before a stage is read).  M0 is written and restored in the
+// same statement (the compiler reserves it).  Device-only body: the host pass of a template kernel that names the
+// address-space-3 cast drops the kernel's host stub without a diagnostic.
 __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds_wave_base);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
 #else
     (void)src;
     (void)lds_wave_base;
@@ -46,6 +63,7 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
 template <int NT1, int NT2>
 struct Dw2 {
     static constexpr int H1 = 32 * NT1, H2 = 32 * NT2;
+    static constexpr int RB = H1 > H2 ? H1 : H2;        // rows per 16-column block of both column buffers
     static constexpr int kRows = H1 + H2;               // staged rows: a1 rows, then d2 rows
     static constexpr int kStageFloats = kRows * kBK;    // 64 B per staged row
     static constexpr int kGlds = kRows / 16;            // 1 KiB LDS-DMA instructions per stage (16 rows each)
@@ -55,16 +73,17 @@ struct Dw2 {
 };
 
 struct Dw2Args {
-    const float* a1t;   // [H1p + 1][ld]
-    const float* d2t;   // [H2p][ld]
+    const float* a1t;   // a1^T, 16-column blocks of RB rows
+    const float* d2t;   // d2^T, the same layout
     float* part;        // [nparts][H1p + 1][H2p]
     uint32_t ld, col0, ncols, kb;   // column range [col0, col0 + ncols); workgroup p takes kb columns from col0 + p kb
 };
 
-// exact split of 8 fp32 values into three bf16 planes (round to nearest even at each step)
+
+// exact split of 8 fp32 values into three bf16 planes (x = p0 + p1 + p2 exactly)
 __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
+    for (int j = 0; j < 8; j++) {   // round to nearest even at each step
         const __bf16 h = (__bf16)v[j];
         const float r = v[j] - (float)h;
         const __bf16 m = (__bf16)r;
@@ -104,16 +123,16 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
         g = g < G::kGlds ? g : G::kGlds - 1;
         const int row = 16 * g + (lane >> 2);
         const int chunk = (lane & 3) ^ ((lane >> 4) & 3);
-        const float* base = row < G::H1 ? a.a1t + (size_t)row * a.ld : a.d2t + (size_t)(row - G::H1) * a.ld;
-        src[i] = base + k_begin + 4 * chunk;
+        const float* base = row < G::H1 ? a.a1t + row * kBK : a.d2t + (row - G::H1) * kBK;
+        src[i] = base + (size_t)(k_begin / kBK) * G::RB * kBK + 4 * chunk;   // block k_begin / 16
     }
-    const auto issue = [&](int stage_idx) {
-        float* dst = S + (stage_idx % kStages) * G::kStageFloats;
+    const auto issue_to = [&](int slot, int stage_idx) {
+        float* dst = S + slot * G::kStageFloats;
 #pragma unroll
         for (int i = 0; i < G::kGldsPerWave; i++) {
             int g = w + 4 * i;
             g = g < G::kGlds ? g : G::kGlds - 1;
-            glds16(src[i] + (size_t)stage_idx * kBK, dst + 16 * g * kBK);
+            glds16(src[i] + (size_t)stage_idx * G::RB * kBK, dst + 16 * g * kBK);
         }
     };
 
@@ -123,57 +142,97 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
 #pragma unroll
         for (int j = 0; j < G::TC; j++) acc[i][j] = floatx16{};
     const bool rows_mine = NT1 >= 2 || wr == 0, cols_mine = NT2 >= 2 || wc == 0;
-    float dsum = 0.0f;   // db2: thread t sums d2 row t
+    // db2: thread t sums d2 row t (threads past H2 sum row H2 - 1 and never store: no branch in the loop body)
+    const int drow = G::H1 + (t < G::H2 ? t : G::H2 - 1);
+    float dsum = 0.0f;
 
-    if (iters > 0) issue(0);
-    if (iters > 1) issue(1);
-    for (int it = 0; it < iters; it++) {
-        if (it + 2 < iters) {
-            issue(it + 2);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::kGldsPerWave) : "memory");
-        } else if (it + 1 < iters) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::kGldsPerWave) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        const float* st = S + (it % kStages) * G::kStageFloats;
-        if (t < G::H2) {   // db2
-            const float* rowp = st + (G::H1 + t) * kBK;
+    // the bf16 planes of one stage's operand fragments (this wave's A rows and B rows), double-buffered: the loop
+    // reads and splits stage it + 1 while the MFMAs of stage it run from registers
+    struct Planes {
+        bf16x8 a0[G::TR], a1[G::TR], a2[G::TR], b0[G::TC], b1[G::TC], b2[G::TC];
+    };
+    const auto load = [&](const float* st, Planes& p) {
+        const float* rowp = st + drow * kBK;
 #pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const float4 x = *reinterpret_cast<const float4*>(rowp + 4 * c);
-                dsum += ((x.x + x.y) + x.z) + x.w;
-            }
+        for (int c = 0; c < 4; c++) {
+            const float4 x = *reinterpret_cast<const float4*>(rowp + 4 * c);
+            dsum += x.x;
+            dsum += x.y;
+            dsum += x.z;
+            dsum += x.w;
         }
         if (rows_mine && cols_mine) {
-            bf16x8 a0[G::TR], a1[G::TR], a2[G::TR], b0[G::TC], b1[G::TC], b2[G::TC];
 #pragma unroll
             for (int i = 0; i < G::TR; i++) {
                 float v[8];
                 read_frag(st, 32 * (wr * G::TR + i) + r, h, v);
-                split3(v, a0[i], a1[i], a2[i]);
+                split3(v, p.a0[i], p.a1[i], p.a2[i]);
             }
 #pragma unroll
             for (int j = 0; j < G::TC; j++) {
                 float v[8];
                 read_frag(st, G::H1 + 32 * (wc * G::TC + j) + r, h, v);
-                split3(v, b0[j], b1[j], b2[j]);
+                split3(v, p.b0[j], p.b1[j], p.b2[j]);
             }
+        }
+    };
+    const auto mfma = [&](const Planes& p) {
+        if (rows_mine && cols_mine) {
 #pragma unroll
             for (int i = 0; i < G::TR; i++)
 #pragma unroll
                 for (int j = 0; j < G::TC; j++) {
                     floatx16 c = acc[i][j];   // smallest terms first
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[i], b0[j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[i], b1[j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b2[j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[i], b0[j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b1[j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b0[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a2[i], p.b0[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a1[i], p.b1[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a0[i], p.b2[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a1[i], p.b0[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a0[i], p.b1[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a0[i], p.b0[j], c, 0, 0, 0);
                     acc[i][j] = c;
                 }
+        }
+    };
+    // one loop step: refill the slot of stage it + 1 + kAhead (past the end: stage iters - 1 again into a slot
+    // nobody reads, so the wait count stays uniform), wait for stage it + 1, then split it into `nxt` while the
+    // MFMAs of stage it (`cur`) run; the interleave is pinned (1 MFMA, then up to 4 VALU) since hipcc otherwise
+    // puts the whole split ahead of the first MFMA
+    const auto step = [&](int it, const Planes& cur, Planes& nxt) {
+        const int q = it + 1 + kAhead;
+        issue_to(q % kStages, q < iters ? q : iters - 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kAhead * G::kGldsPerWave) : "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        load(S + ((it + 1) % kStages) * G::kStageFloats, nxt);
+        mfma(cur);
+        constexpr int kMfma = 6 * G::TR * G::TC;
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // DS read: the first fragments' reads up front
+#pragma unroll
+        for (int m = 0; m < kMfma; m++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // VALU
+        }
+    };
+
+    Planes pa, pb;
+    if (iters > 0) {
+#pragma unroll
+        for (int q = 0; q <= kAhead; q++) issue_to(q, q < iters ? q : iters - 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kAhead * G::kGldsPerWave) : "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        load(S, pa);
+        int it = 0;
+        for (; it + 2 < iters; it += 2) {
+            step(it, pa, pb);
+            step(it + 1, pb, pa);
+        }
+        if (it + 1 < iters) {
+            step(it, pa, pb);
+            mfma(pb);
+        } else {
+            mfma(pa);
         }
     }
     // this workgroup's slab: dW2 rows from the accumulators (C/D layout: column = lane & 31, row = acc_row), db2

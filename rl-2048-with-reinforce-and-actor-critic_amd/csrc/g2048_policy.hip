@@ -632,8 +632,9 @@ void launch_pol_nt2(const PolArgs& a, int nt2, int act, int obs, int rng, int gr
 // in A-fragment order; d2 tiles are its B operands register for register, like layer 2 of the forward), and the
 // small weight gradients dW1 (x^T d1), db1, dW3 (a2^T g), db3 on v_mfma_f32_16x16x4f32 through a per-wave LDS
 // transpose, accumulated per wave in LDS across the wave's sample groups.  The one large weight gradient,
-// dW2 = a1^T d2 (and db2 through a ones row), is left to a split-K GEMM over the a1^T / d2^T columns this kernel
-// writes (coalesced: the accumulator layout puts 32 consecutive samples of one unit in a lane half).
+// dW2 = a1^T d2 and db2 = sum d2, is left to g2048_dw2 (g2048_dw2.hip) over the a1^T / d2^T columns this kernel
+// writes (the accumulator layout puts 32 consecutive samples of one unit in a lane half: two 64-B runs, one in
+// each of two 16-column blocks).
 // Packed input-delta weights: w2b [nt1][nt2][4][64][4]: lane l, k-step (t2, r = 4q + u) of output tile o1 at
 // [o1][t2][q][l][u]: W2[32 o1 + (l & 31)][32 t2 + row(r, l >> 5)].
 struct GradPackArgs {
@@ -662,8 +663,8 @@ struct GradArgs {
     const uint64_t* boards;  // [n] sample boards (the obs of each step)
     const uint8_t* actions;  // [n]
     const float* coef;       // [n] advantage * step weight
-    float* a1t;              // [H1p + 1][ld]: a1^T and a row of ones
-    float* d2t;              // [H2p][ld]
+    float* a1t;              // a1^T: [R][ld] in 16-column blocks (col_store), R = 32 max(NT1, NT2)
+    float* d2t;              // d2^T: the same layout
     float* part;             // [waves][grad_part_floats]
     uint32_t n, ld;          // samples; columns (a multiple of 32, >= n): samples n..ld-1 have coef 0
     float obs_scale;
@@ -706,7 +707,10 @@ __device__ __forceinline__ float activation_derivative(float a) {   // from the 
 // The a1^T / d2^T column buffers are addressed as buffer resources: element (row, column) at voffset = this lane's
 // column byte offset (one VGPR for every access) + soffset = row * ld * 4 (scalar), so no per-row 64-bit vector
 // address is ever formed (those kept 2 VGPRs live per row across the whole group and spilled the large nets).
-// Column buffers [rows][ld] fp32: row `row` of this lane's column at scalar offset row * ld4 (ld4 = ld * 4 bytes).
+// Column buffers fp32 in 16-column blocks (include/g2048.h): element (row, col) at ((col >> 4) * R + row) * 16 +
+// (col & 15), R = 32 max(NT1, NT2) rows per block for both buffers, so one stage of 16 samples of every row is
+// one contiguous 64 R bytes (g2048_dw2 streams them; a wave's column stores stay inside two blocks).  Row `row` of
+// this lane's column at scalar offset row * ld4 (ld4 = 64 bytes, the row stride inside a block).
 // The caller re-opaques ld4 per tile (opaque_sgpr): otherwise the compiler hoists every row's offset out of the
 // group loop into its own SGPR (hundreds of them), spills them to VGPR lanes, and pays a v_readlane + hazard nops
 // before every column store.
@@ -744,8 +748,9 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
     float4* h1f = reinterpret_cast<float4*>(S.stage[w]);             // [t][q][lane] during the forward
     float (*T)[33] = reinterpret_cast<float (*)[33]>(S.stage[w]);     // [unit][sample] during the backward
     float gsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // db3 partial (lanes of half 0)
-    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc(a.a1t, 0, (int)((H1p + 1) * a.ld * 4u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rd2 = __builtin_amdgcn_make_buffer_rsrc(a.d2t, 0, (int)(H2p * a.ld * 4u), 0x00020000);
+    constexpr uint32_t RB = 32u * (NT1 > NT2 ? NT1 : NT2);   // rows per 16-column block of both column buffers
+    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc(a.a1t, 0, (int)(RB * a.ld * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd2 = __builtin_amdgcn_make_buffer_rsrc(a.d2t, 0, (int)(RB * a.ld * 4u), 0x00020000);
     floatx4 dw1acc[2 * NT1], dw3acc[2 * NT2];  // dW1^T / dW3^T 16x16 accumulator blocks, across the wave's groups
 #pragma unroll
     for (int k = 0; k < 2 * NT1; k++) dw1acc[k] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -773,8 +778,9 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         // out of the group loop into hundreds of registers
         asm volatile("" ::: "memory");
         const uint32_t cj = a.col_off + j;                        // this sample's column
-        const uint32_t off = (cj + 4u * (uint32_t)h * a.ld) * 4u;  // byte offset: column cj, + acc_row's 4h rows
-        uint32_t ld4 = a.ld * 4u;                                    // row stride in bytes (see col_store)
+        // byte offset of column cj's row 4h (acc_row's lane-half rows) in its 16-column block
+        const uint32_t off = (((cj >> 4) * RB + 4u * (uint32_t)h) * 16u + (cj & 15u)) * 4u;
+        uint32_t ld4 = 64u;                                          // row stride inside a block (see col_store)
         const bool valid = j < a.n;
         const uint64_t b = valid ? a.boards[j] : 0ull;
         const uint32_t act = (valid && !a.critic) ? a.actions[j] : 0u;   // no actions in critic mode
@@ -816,7 +822,6 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
             }
         }
         lds_fence();
-        if (h == 0) col_store(ra1, H1p, ld4, cj * 4u, 1.0f);  // the ones row: db2 comes out of the dW2 GEMM
         GRAD_PH(0);
         float h2[NT2][16];
         float lg[4] = {0.0f, 0.0f, 0.0f, 0.0f};

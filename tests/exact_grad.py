@@ -54,7 +54,7 @@ class PatternProbe:
         self.seen: dict[str, torch.Tensor] = {}
 
     def __call__(self, slot, k, idx, a1t, d2t):
-        h1p, h2p = a1t.shape[0] - 1, d2t.shape[0]
+        h1p, h2p = a1t.shape[0], d2t.shape[0]
         if slot not in self.store:
             self.store[slot] = [torch.zeros(self.K, self.N, h1p // 8, dtype=torch.uint8, device=self.device),
                                 torch.zeros(self.K, self.N, h2p // 8, dtype=torch.uint8, device=self.device)]

@@ -235,44 +235,46 @@ def _steps_of(agent, batch):
 @pytest.mark.parametrize("ncols,cpp", [(4096, 2048), (2048 + 16 * 37, 2048), (1 << 16, 4096), (48, 2048)])
 def test_dw2_kernel_matches_fp64(h1, h2, ncols, cpp):
     """g2048_dw2 (the layer-2 weight / bias gradient: a1 d2^T and the row sums of d2, three bf16 planes per fp32
-    operand on the bf16 MFMA) against fp64 on the same fp32 column buffers, with values spanning several orders of
-    magnitude and zero / negative entries: every slab within 4e-6 of sum |a d| of the exact value (the bf16 MFMA's
-    accumulation into its fp32 accumulator is measured at ~2e-6 of sum |a d| over 2048 columns -- looser than the
-    f32 MFMA's k-ordered fma chain; the gradient-level 1e-5 checks hold the whole update to the exact value), for
-    full and padded (non-multiple-of-32) hidden sizes and partial last slabs."""
+    operand on the bf16 MFMA) against fp64 on the same fp32 column buffers (16-column block layout of
+    include/g2048.h), with values spanning several orders of magnitude and zero / negative entries: every slab
+    within 4e-6 of sum |a d| of the exact value (the bf16 MFMA's accumulation into its fp32 accumulator is measured
+    at ~2e-6 of sum |a d| over 2048 columns -- looser than the f32 MFMA's k-ordered fma chain; the gradient-level
+    1e-5 checks hold the whole update to the exact value), for full and padded (non-multiple-of-32) hidden sizes,
+    a column range starting inside the buffer, and partial last slabs."""
     from rl2048_amd import _lib as L
     from rl2048_amd.agent import _padded_units
 
     H1p, H2p = _padded_units(h1), _padded_units(h2)
-    ld = ncols + 32 + (-(ncols + 32) % 16)
+    R = max(H1p, H2p)
+    col0 = 32
+    ld = col0 + ncols + 32
     g = torch.Generator(device=DEV)
     g.manual_seed(h1 * 1000 + ncols)
-    a1t = torch.randn(H1p + 1, ld, device=DEV, generator=g) * torch.exp(3 * torch.randn(H1p + 1, ld, device=DEV,
-                                                                                           generator=g))
-    a1t = torch.relu(a1t)                              # activations: non-negative, many exact zeros
-    d2t = torch.randn(H2p, ld, device=DEV, generator=g) * torch.exp(2 * torch.randn(H2p, ld, device=DEV, generator=g))
-    a1t[h1:H1p] = 0.0
-    d2t[h2:] = 0.0
-    col0 = 16
+    A = torch.zeros(R, ld, device=DEV)
+    D = torch.zeros(R, ld, device=DEV)
+    A[:h1] = torch.relu(torch.randn(h1, ld, device=DEV, generator=g) *
+                        torch.exp(3 * torch.randn(h1, ld, device=DEV, generator=g)))   # activations: >= 0, many zeros
+    D[:h2] = torch.randn(h2, ld, device=DEV, generator=g) * torch.exp(2 * torch.randn(h2, ld, device=DEV, generator=g))
+    blocked = lambda X: X.reshape(R, ld // 16, 16).permute(1, 0, 2).contiguous()  # noqa: E731 (include/g2048.h)
+    a_in, d_in = blocked(A), blocked(D)
     nparts = -(-ncols // cpp)
     part = torch.full((nparts, H1p + 1, H2p), float("nan"), device=DEV)
     lib = L.lib()
-    a_in, d_in = a1t[:, col0:].contiguous(), d2t[:, col0:].contiguous()   # kept alive until the kernel has run
-    L.check(lib.g2048_dw2(L.ptr(a_in), L.ptr(d_in), h1, h2, ld - col0, 0, ncols, cpp, L.ptr(part), nparts,
+    L.check(lib.g2048_dw2(L.ptr(a_in), L.ptr(d_in), h1, h2, ld, col0, ncols, cpp, L.ptr(part), nparts,
                           L.stream_handle(DEV)))
     torch.cuda.synchronize()
-    A, D = a1t[:, col0:col0 + ncols].double(), d2t[:, col0:col0 + ncols].double()
+    A64, D64 = A[:H1p, col0:col0 + ncols].double(), D[:H2p, col0:col0 + ncols].double()
     for p in range(nparts):
         sl = slice(p * cpp, min((p + 1) * cpp, ncols))
-        ref = A[:H1p, sl] @ D[:, sl].t()
-        bound = A[:H1p, sl].abs() @ D[:, sl].abs().t()
+        ref = A64[:, sl] @ D64[:, sl].t()
+        bound = A64[:, sl].abs() @ D64[:, sl].abs().t()
         got = part[p, :H1p].double()
         rel = float(((got - ref).abs() / bound.clamp_min(1e-30)).max())
         print(f"slab {p}: max |err| / sum |a d| = {rel:.3g}")
         assert bool(((got - ref).abs() <= 4e-6 * bound + 1e-30).all()), (p, rel)
-        db = D[:, sl].sum(1)
-        assert bool(((part[p, H1p].double() - db).abs() <= 4e-6 * D[:, sl].abs().sum(1) + 1e-30).all()), p
+        db = D64[:, sl].sum(1)
+        assert bool(((part[p, H1p].double() - db).abs() <= 4e-6 * D64[:, sl].abs().sum(1) + 1e-30).all()), p
     # bad arguments are rejected, not launched
     with pytest.raises(ValueError):
-        L.check(lib.g2048_dw2(L.ptr(a1t), L.ptr(d2t), h1, h2, ld, 0, ncols + 8, cpp, L.ptr(part), nparts,
+        L.check(lib.g2048_dw2(L.ptr(a_in), L.ptr(d_in), h1, h2, ld, col0, ncols + 8, cpp, L.ptr(part), nparts,
                               L.stream_handle(DEV)))
