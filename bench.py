@@ -276,6 +276,8 @@ def train_iteration_rate(torch, device, episodes: int = 65536, repeats: int = 2,
     critic=True, of configs[2]'s actor-critic: the batched rollout of one episode per lane (g2048_rollout: fused
     policy + env step) and update_from_batch (fused actor / critic gradient kernels + the layer-2 GEMM, fp32),
     timed separately; the last of `repeats` iterations after one warm-up."""
+    import numpy as np
+
     from rl2048_amd import Game2048EnvConfig
     from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
     from rl2048_amd.mlp import MLPConfig
@@ -286,10 +288,12 @@ def train_iteration_rate(torch, device, episodes: int = 65536, repeats: int = 2,
     out = {}
     for rep in range(repeats + 1):
         base = 1000 + rep * episodes
+        # the episode seeds as arrays (the runner's SeedStream.take_array form), made before the timed region
+        es = np.arange(base, base + episodes, dtype=np.int64)
+        ps = es + 7 * episodes
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        batch = agent.rollout_batch(list(range(base, base + episodes)), list(range(base + 7 * episodes,
-                                                                                 base + 8 * episodes)))
+        batch = agent.rollout_batch(es, ps)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         agent.update_from_batch(batch)

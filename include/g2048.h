@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 10
+#define G2048_ABI_VERSION 11
 
 /* status codes */
 #define G2048_OK 0
@@ -260,6 +260,10 @@ int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int
  * bf16 planes, six plane products on the bf16 MFMA. */
 int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int64_t ld, int64_t col0, int64_t ncols,
               int64_t cols_per_part, float* partials, int64_t nparts, void* stream);
+/* acc[i] += sum over p < nparts of partials[p * slab + i] (i < slab), the sum taken in fp64 in a fixed order: folds
+ * g2048_dw2's slabs (slab = (H1p + 1) H2p) or any per-wave fp32 partials into an fp64 accumulator on the device
+ * (the fp64 chunk sums of update_from_batch; no fp32 -> fp64 conversion pass). */
+int g2048_fold_partials(const float* partials, int64_t nparts, int64_t slab, double* acc, void* stream);
 
 /* The whole batched rollout in one launch: ReinforceAgent.run_episode (src/reinforce_agent.py:195-252) for n
  * (env_seed, policy_seed) pairs -- select_action (the fused policy above) + Game2048Env.step until terminated or

@@ -421,21 +421,29 @@ class ReinforceAgent:
     # columns per g2048_dw2 workgroup: one workgroup per CU at 2^20 columns, never fewer than this many columns each
     dw2_min_cols_per_part = 2048
 
-    def _dw2(self, a1t: torch.Tensor, d2t: torch.Tensor, h1: int, h2: int, ncols: int) -> torch.Tensor:
-        """dW2 / db2 of the columns [0, ncols) of the fused kernels' column buffers (g2048_dw2: the a1 d2^T outer
-        products on the bf16 MFMA with three-plane fp32-accurate operands, split over workgroups); returns the fp64
-        sum of the workgroup slabs, [H1p + 1, H2p] (row H1p = db2)."""
+    def _fold(self, part: torch.Tensor, acc: torch.Tensor) -> None:
+        """acc (fp64, contiguous) += the sum of part's rows, taken in fp64 on the device (g2048_fold_partials)."""
+        assert acc.dtype == torch.float64 and acc.is_contiguous() and part.is_contiguous()
+        slab = acc.numel()
+        assert part.numel() % slab == 0
+        L.check(self._lib.g2048_fold_partials(L.ptr(part), part.numel() // slab, slab, L.ptr(acc), self._stream))
+
+    def _dw2(self, a1t: torch.Tensor, d2t: torch.Tensor, h1: int, h2: int, ncols: int, acc: torch.Tensor) -> None:
+        """acc [H1p + 1, H2p] fp64 += dW2 / db2 of the columns [0, ncols) of the fused kernels' column buffers
+        (g2048_dw2: the a1 d2^T outer products on the bf16 MFMA with three-plane fp32-accurate operands, one
+        workgroup per CU; its fp32 slabs folded into acc in fp64; row H1p = db2)."""
         H1p, H2p = _padded_units(h1), _padded_units(h2)
         if ncols == 0:
-            return torch.zeros(H1p + 1, H2p, dtype=torch.float64, device=self.device)
+            return
         assert a1t.numel() == d2t.numel() and a1t.shape[0] == max(H1p, H2p)
+        assert acc.shape == (H1p + 1, H2p)
         cus = int(self._lib.g2048_actor_grad_waves()) // 4
         cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * cus)) * 16)
         nparts = -(-ncols // cpp)
         part = torch.empty(nparts, H1p + 1, H2p, dtype=torch.float32, device=self.device)
         L.check(self._lib.g2048_dw2(L.ptr(a1t), L.ptr(d2t), h1, h2, int(a1t.shape[1]), 0, ncols, cpp, L.ptr(part),
                                     nparts, self._stream))
-        return part.sum(0, dtype=torch.float64)
+        self._fold(part, acc)
 
     def _actor_grad_fused(self, steps: "_Steps", adv: torch.Tensor, step_w: torch.Tensor, K: int,
                           gW: list[torch.Tensor], gb: list[torch.Tensor], spec) -> None:
@@ -544,8 +552,7 @@ class ReinforceAgent:
 
         def fold() -> None:
             # the per-wave partials accumulate in fp32 across row launches; fold them into fp64 every so often
-            nonlocal small
-            small += part.sum(0, dtype=torch.float64)
+            self._fold(part, small)
             part.zero_()
 
         def flush(used: int) -> None:
@@ -558,7 +565,7 @@ class ReinforceAgent:
                                     _unblock(a1t, H1p, c0, cnt_), _unblock(d2t, H2p, c0, cnt_))
             launched.clear()
             fold()
-            big += self._dw2(a1t, d2t, h1, h2, used)   # every column < used was written by a row launch
+            self._dw2(a1t, d2t, h1, h2, used, big)   # every column < used was written by a row launch
 
         def grad_launch(s0: int, cnt: int, tgt: torch.Tensor, k: int) -> None:
             nonlocal col, since_fold
@@ -653,8 +660,8 @@ class ReinforceAgent:
                 launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale)
                 if self.grad_probe is not None:
                     self.grad_probe(slot, k, sel, _unblock(a1t, H1p, 0, m), _unblock(d2t, H2p, 0, m))
-                big += self._dw2(a1t, d2t, h1, h2, ld)     # layer-2 weight + bias gradient, chunks summed in fp64
-                small += part.sum(0)
+                self._dw2(a1t, d2t, h1, h2, ld, big)       # layer-2 weight + bias gradient, chunks summed in fp64
+                self._fold(part, small)
         big, small = big.to(torch.float32), small.to(torch.float32)
         gW[0] += small[:16 * H1p].view(16, H1p)[:, :h1]
         gb[0] += small[16 * H1p:17 * H1p][:h1]

@@ -264,6 +264,35 @@ int tiles_of(int hsize) {   // as g2048_policy.hip: 32-unit tiles rounded up to 
     return t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : 8;
 }
 
+// acc[i] += sum_p part[p slab + i] in fp64.  A workgroup of 64 G threads takes 64 consecutive elements: wave g
+// sums the slabs p = g, g + G, g + 2G, ... (8 loads in flight; each load instruction reads 256 contiguous bytes),
+// then the G wave sums are added in order of g through LDS -- a fixed order, so the result is deterministic.
+// G (1..16) grows as the slab shrinks, so that small slabs with many parts still put enough waves on the chip.
+__global__ void __launch_bounds__(1024) fold_kernel(const float* __restrict__ part, uint32_t nparts, uint32_t slab,
+                                                    double* __restrict__ acc) {
+    __shared__ double ws[16][64];
+    const uint32_t G = blockDim.x >> 6, g = threadIdx.x >> 6, e = threadIdx.x & 63u;
+    const uint32_t i = blockIdx.x * 64u + e;
+    const uint32_t ic = i < slab ? i : slab - 1u;
+    double s = 0.0;
+    uint32_t p = g;
+    for (; p + 7u * G < nparts; p += 8u * G) {
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) v[q] = part[(size_t)(p + q * G) * slab + ic];
+#pragma unroll
+        for (int q = 0; q < 8; q++) s += (double)v[q];
+    }
+    for (; p < nparts; p += G) s += (double)part[(size_t)p * slab + ic];
+    ws[g][e] = s;
+    __syncthreads();
+    if (g == 0 && i < slab) {
+        double t = ws[0][e];
+        for (uint32_t k = 1; k < G; k++) t += ws[k][e];
+        acc[i] += t;
+    }
+}
+
 }  // namespace
 
 namespace g2048_internal {
@@ -292,6 +321,23 @@ extern "C" int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int
         case 4: launch_nt2<4>(a, nt2, grid, s); break;
         default: launch_nt2<8>(a, nt2, grid, s); break;
     }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(G2048_EHIP, hipGetErrorString(e));
+    return G2048_OK;
+}
+
+extern "C" int g2048_fold_partials(const float* partials, int64_t nparts, int64_t slab, double* acc, void* stream) {
+    using g2048_internal::set_error;
+    if (!partials || !acc) return set_error(G2048_EINVAL, "fold_partials: NULL buffer");
+    if (nparts < 0 || slab < 0 || nparts > ((int64_t)1 << 24) || slab > ((int64_t)1 << 28))
+        return set_error(G2048_EINVAL, "fold_partials: nparts / slab out of range");
+    if (nparts == 0 || slab == 0) return G2048_OK;
+    // waves per workgroup: enough that ~4 waves per SIMD (4096 on 256 CUs) each sum at least 8 slabs
+    const int64_t blocks = (slab + 63) / 64;
+    int G = 1;
+    while (G < 16 && blocks * G < 4096 && nparts >= 16 * G) G *= 2;
+    hipLaunchKernelGGL(fold_kernel, dim3((unsigned)blocks), dim3(64 * G), 0, (hipStream_t)stream, partials,
+                       (uint32_t)nparts, (uint32_t)slab, acc);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(G2048_EHIP, hipGetErrorString(e));
     return G2048_OK;

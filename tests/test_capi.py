@@ -30,7 +30,8 @@ def test_header_declares_expected_api():
         "g2048_abi_version", "g2048_last_error", "g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step",
         "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_packed_size",
         "g2048_policy_pack", "g2048_policy", "g2048_rollout", "g2048_grad_packed_size", "g2048_grad_partial_size",
-        "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2"])
+        "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2",
+        "g2048_fold_partials"])
 
 
 def test_library_exports_every_declared_symbol(L):

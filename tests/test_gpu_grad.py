@@ -278,3 +278,31 @@ def test_dw2_kernel_matches_fp64(h1, h2, ncols, cpp):
     with pytest.raises(ValueError):
         L.check(lib.g2048_dw2(L.ptr(a_in), L.ptr(d_in), h1, h2, ld, col0, ncols + 8, cpp, L.ptr(part), nparts,
                               L.stream_handle(DEV)))
+
+
+@pytest.mark.parametrize("nparts,slab", [(256, 257 * 256), (1, 33 * 32), (13, 1000), (1024, 1377), (1024, 5380),
+                                         (37, 63)])
+def test_fold_partials_matches_fp64_sum(nparts, slab):
+    """g2048_fold_partials (the update's fp64 fold of g2048_dw2 slabs and per-wave partials): acc += the sum over
+    slabs, taken in fp64 in a fixed order -- equal to numpy's fp64 sum of the same fp32 values up to fp64 rounding
+    of the (different) summation order, adding to what acc held, and bitwise repeatable."""
+    from rl2048_amd import _lib as L
+
+    g = torch.Generator(device=DEV)
+    g.manual_seed(nparts * 7 + slab)
+    part = torch.randn(nparts, slab, device=DEV, generator=g) * torch.exp(4 * torch.randn(nparts, slab, device=DEV,
+                                                                                         generator=g))
+    acc0 = torch.randn(slab, device=DEV, dtype=torch.float64, generator=g)
+    acc = acc0.clone()
+    L.check(L.lib().g2048_fold_partials(L.ptr(part), nparts, slab, L.ptr(acc), L.stream_handle(DEV)))
+    torch.cuda.synchronize()
+    p64 = part.double().cpu().numpy()
+    ref = acc0.cpu().numpy() + np.add.reduce(p64, axis=0)
+    bound = np.abs(acc0.cpu().numpy()) + np.abs(p64).sum(0)
+    assert np.all(np.abs(acc.cpu().numpy() - ref) <= 1e-14 * bound)
+    again = acc0.clone()
+    L.check(L.lib().g2048_fold_partials(L.ptr(part), nparts, slab, L.ptr(again), L.stream_handle(DEV)))
+    torch.cuda.synchronize()
+    assert torch.equal(again, acc)
+    with pytest.raises(ValueError):
+        L.check(L.lib().g2048_fold_partials(None, nparts, slab, L.ptr(acc), L.stream_handle(DEV)))

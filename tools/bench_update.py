@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--repeats", type=int, default=2)
     ap.add_argument("--lib", default=None, help="another build of libg2048 (A/B scripts)")
     args = ap.parse_args()
+    import numpy as np
     import torch
 
     from rl2048_amd import Game2048EnvConfig
@@ -43,9 +44,11 @@ def main():
                                ReinforceAgentConfig(baseline_mode="batch", use_critic=args.critic), device=dev)
         for rep in range(args.repeats + 1):
             base = 1000 + rep * n
+            es = np.arange(base, base + n, dtype=np.int64)   # seed arrays (SeedStream.take_array form)
+            ps = es + 7 * n
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            batch = agent.rollout_batch(list(range(base, base + n)), list(range(base + 7 * n, base + 8 * n)))
+            batch = agent.rollout_batch(es, ps)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             agent.update_from_batch(batch)
