@@ -411,6 +411,29 @@ def main():
         else:
             dist.init_process_group("gloo")   # rehearsal of the N-rank path with ranks sharing a GPU (timing only)
     B = args.boards
+    # The extra legs (training iterations, policy rollouts) run first, so that the headline env-step leg below is
+    # timed on a chip at its working clock: on a cold chip the first ~20 launches of the step kernel run 10-30 %
+    # slower (profiles/round3/step_cold_trace.log), which a 20-step run would otherwise fold into the headline.
+    train = None
+    if not args.pmc_child and not args.no_train and args.train_episodes > 0:
+        try:
+            train = train_iteration_dp(torch, device, args.train_episodes, rank, world)
+        except Exception as e:  # noqa: BLE001 -- an extra, never the headline
+            train = {"error": repr(e)}
+    policy = None
+    if not args.pmc_child and rank == 0 and world == 1 and not args.no_policy:
+        try:
+            policy = policy_rollout_rate(torch, B, device)
+            policy["gemm_path"] = policy_rollout_rate(torch, B, device, fused=False)
+            policy["train_iteration_configs1"] = train_iteration_rate(torch, device)
+            # configs[2]: 1,048,576 parallel boards, actor-critic (one warm-up, one timed iteration)
+            policy["train_iteration_configs2"] = train_iteration_rate(torch, device, episodes=1 << 20, repeats=1,
+                                                                      critic=True)
+        except Exception as e:  # noqa: BLE001 -- an extra, never the headline
+            policy = {"error": repr(e)}
+    torch.cuda.empty_cache()
+    if world > 1:
+        dist.barrier()
     env = make_env(torch, args, B, rank * B, device)
     K, W = args.steps, args.warmup
     g = torch.Generator(device=device)
@@ -458,24 +481,6 @@ def main():
     if args.pmc_child:
         return
     del actions
-    torch.cuda.empty_cache()
-    train = None
-    if not args.no_train and args.train_episodes > 0:
-        try:
-            train = train_iteration_dp(torch, device, args.train_episodes, rank, world)
-        except Exception as e:  # noqa: BLE001 -- an extra, never the headline
-            train = {"error": repr(e)}
-    policy = None
-    if rank == 0 and world == 1 and not args.no_policy:
-        try:
-            policy = policy_rollout_rate(torch, B, device)
-            policy["gemm_path"] = policy_rollout_rate(torch, B, device, fused=False)
-            policy["train_iteration_configs1"] = train_iteration_rate(torch, device)
-            # configs[2]: 1,048,576 parallel boards, actor-critic (one warm-up, one timed iteration)
-            policy["train_iteration_configs2"] = train_iteration_rate(torch, device, episodes=1 << 20, repeats=1,
-                                                                      critic=True)
-        except Exception as e:  # noqa: BLE001 -- an extra, never the headline
-            policy = {"error": repr(e)}
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
