@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 11
+#define G2048_ABI_VERSION 12
 
 /* status codes */
 #define G2048_OK 0
@@ -244,12 +244,17 @@ int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int 
  * col_off .. col_off + ncols - 1 are written (those past n as zero-coefficient padding; col_off, ncols multiples
  * of 32, n <= ncols, col_off + ncols <= ld) -- so consecutive launches (one per time row of a batch, whose V(s)
  * is the previous row's V(s')) can fill one column buffer before one layer-2 GEMM.  accumulate != 0 adds this
- * launch's per-wave partials into `partials` instead of overwriting them. */
+ * launch's per-wave partials into `partials` instead of overwriting them.
+ * d2_form 1 (factored; ReLU only): the critic's d2 is m * (W3[:, 0] g) with m = [a2 > 0] and g = dL/dV * weight per
+ * sample, so instead of d2 columns d2t receives one 1 KiB record per 16-column block c (ld / 16 records): bytes
+ * [0, 2 H2p) the mask, one uint16 per second-layer unit j (bit k = column 16 c + k has a2_j > 0); bytes [512, 576)
+ * g of the block's 16 columns (fp32); the rest unused.  g2048_dw2_factored reads that form (64 B per sample
+ * instead of 1 KiB).  d2_form 0: d2 columns as for the actor. */
 int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
                       float obs_scale, int loss, float huber_delta, const uint64_t* boards, const float* target,
                       const float* weight, float* delta_out, float* value_out, int64_t n, int64_t ld, int64_t col_off,
                       int64_t ncols, float* a1t, float* d2t, float* partials, int accumulate, int64_t waves,
-                      void* stream);
+                      int d2_form, void* stream);
 
 /* The layer-2 weight / bias gradient of the fused update (the a1 d2^T outer products of _backpropagation,
  * src/reinforce_agent.py:639-678, summed over samples): over the columns [col0, col0 + ncols) of the column
@@ -260,6 +265,12 @@ int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int
  * bf16 planes, six plane products on the bf16 MFMA. */
 int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int64_t ld, int64_t col0, int64_t ncols,
               int64_t cols_per_part, float* partials, int64_t nparts, void* stream);
+/* g2048_dw2 for the ReLU critic's factored form (g2048_critic_grad d2_form 1; records: see there): partials[p] rows
+ * i < H1p = W3[j] * sum over the slab's columns of fl(a1_i g) m_j, row H1p = W3[j] * sum g m_j; w3 = W3[:, 0]
+ * padded with zeros to H2p.  The mask is exact in one bf16 plane, so three plane products per step. */
+int g2048_dw2_factored(const float* a1t, const float* records, const float* w3, int h1, int h2, int64_t ld,
+                       int64_t col0, int64_t ncols, int64_t cols_per_part, float* partials, int64_t nparts,
+                       void* stream);
 /* acc[i] += sum over p < nparts of partials[p * slab + i] (i < slab), the sum taken in fp64 in a fixed order: folds
  * g2048_dw2's slabs (slab = (H1p + 1) H2p) or any per-wave fp32 partials into an fp64 accumulator on the device
  * (the fp64 chunk sums of update_from_batch; no fp32 -> fp64 conversion pass). */

@@ -20,7 +20,7 @@ LIB_PATH = SHIPPED_LIB
 SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
 SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip"), os.path.join(PKG_DIR, "csrc", "g2048_dw2.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 # include/g2048.h constants
 OBS_NONE, OBS_RAW, OBS_LOG2, OBS_ONEHOT = -1, 0, 1, 2
@@ -141,13 +141,14 @@ def _declare(L):
     L.g2048_actor_grad_waves.argtypes = []
     L.g2048_actor_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, vp, vp, vp, i64, i64, vp, vp, vp, i64, vp]
     L.g2048_critic_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, f, vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, vp,
-                                    vp, i32, i64, vp]
+                                    vp, i32, i64, i32, vp]
     L.g2048_dw2.argtypes = [vp, vp, i32, i32, i64, i64, i64, i64, vp, i64, vp]
     L.g2048_fold_partials.argtypes = [vp, i64, i64, vp, vp]
+    L.g2048_dw2_factored.argtypes = [vp, vp, vp, i32, i32, i64, i64, i64, i64, vp, i64, vp]
     for name in ("g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step", "g2048_obs", "g2048_move",
                  "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy",
                  "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad",
-                 "g2048_dw2", "g2048_fold_partials"):
+                 "g2048_dw2", "g2048_fold_partials", "g2048_dw2_factored"):
         getattr(L, name).restype = ctypes.c_int
 
 
@@ -155,7 +156,8 @@ EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g204
                     "g2048_step", "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries",
                     "g2048_policy_packed_size", "g2048_policy_pack", "g2048_policy", "g2048_rollout",
                     "g2048_grad_packed_size", "g2048_grad_partial_size", "g2048_grad_pack", "g2048_actor_grad_waves",
-                    "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2", "g2048_fold_partials")
+                    "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2", "g2048_fold_partials",
+                    "g2048_dw2_factored")
 
 
 def lib():

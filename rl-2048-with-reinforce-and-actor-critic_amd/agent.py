@@ -106,6 +106,19 @@ def _board_values(b: int) -> np.ndarray:
     return np.where(e > 0, np.left_shift(np.int64(1), e), 0).astype(np.int64)
 
 
+def _unrecord(rec: torch.Tensor, w3: torch.Tensor, c0: int, m: int) -> torch.Tensor:
+    """The d2 columns [c0, c0 + m) that the factored block records (g2048_critic_grad d2_form 1) stand for, [H2p, m]:
+    fl(g * W3[j]) where unit j's mask bit is set -- bit for bit the d2 the unfactored kernel computes (its
+    d2 = (g W3[j] + 0 ...) * 1 or * 0)."""
+    H2p = w3.numel()
+    blocks = rec.view(-1, 256)
+    words = blocks.view(torch.int16).view(-1, 512)[:, :H2p].to(torch.int32) & 0xFFFF   # [blocks, H2p]
+    g = blocks[:, 128:144].reshape(-1)                                                   # [blocks * 16]
+    cols = torch.arange(c0, c0 + m, device=rec.device)
+    bits = (words[cols >> 4] >> (cols & 15)[:, None]) & 1                                 # [m, H2p]
+    return ((g[cols][:, None] * w3[None, :]) * bits.to(torch.float32)).t()
+
+
 def _unblock(buf: torch.Tensor, rows: int, c0: int, m: int) -> torch.Tensor:
     """Rows [0, rows) x columns [c0, c0 + m) of a column buffer stored in 16-column blocks (include/g2048.h) as a
     row-major copy (diagnostics: ReinforceAgent.grad_probe)."""
@@ -225,6 +238,7 @@ class ReinforceAgent:
         self.use_fused_grad = True
         # ... and the fused critic per time row, V(s') taken from the next row's pass (large batches)
         self.use_critic_rows = True
+        self.critic_factored_d2 = True   # ReLU critic rows: the factored d2 records + g2048_dw2_factored
         self.grad_chunk_steps = 1 << 20
         # diagnostics (tests): called as grad_probe(slot, k, sample_idx, a1_cols, d2_cols) with the column buffers
         # of every fused-gradient launch before they are reused -- sample_idx indexes the batch's valid steps
@@ -445,6 +459,22 @@ class ReinforceAgent:
                                     nparts, self._stream))
         self._fold(part, acc)
 
+    def _dw2_factored(self, a1t: torch.Tensor, rec: torch.Tensor, w3: torch.Tensor, h1: int, h2: int, ncols: int,
+                      acc: torch.Tensor) -> None:
+        """_dw2 for the ReLU critic's factored d2 form (g2048_critic_grad d2_form 1): the 1 KiB block records (mask
+        words + g) instead of d2 columns; g2048_dw2_factored scales by W3[:, 0] (w3, padded to H2p)."""
+        H1p, H2p = _padded_units(h1), _padded_units(h2)
+        if ncols == 0:
+            return
+        assert rec.numel() * 4 >= (ncols // 16) * 1024 and w3.numel() == H2p and acc.shape == (H1p + 1, H2p)
+        cus = int(self._lib.g2048_actor_grad_waves()) // 4
+        cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * cus)) * 16)
+        nparts = -(-ncols // cpp)
+        part = torch.empty(nparts, H1p + 1, H2p, dtype=torch.float32, device=self.device)
+        L.check(self._lib.g2048_dw2_factored(L.ptr(a1t), L.ptr(rec), L.ptr(w3), h1, h2, int(a1t.shape[1]), 0, ncols,
+                                             cpp, L.ptr(part), nparts, self._stream))
+        self._fold(part, acc)
+
     def _actor_grad_fused(self, steps: "_Steps", adv: torch.Tensor, step_w: torch.Tensor, K: int,
                           gW: list[torch.Tensor], gb: list[torch.Tensor], spec) -> None:
         """The actor branch of update_batch (src/reinforce_agent.py:502-555) for every valid step and symmetry k:
@@ -487,7 +517,7 @@ class ReinforceAgent:
             L.check(self._lib.g2048_critic_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, loss,
                                                 float(c.huber_delta), L.ptr(b), L.ptr(tgt), L.ptr(w),
                                                 L.ptr(deltas[k, s0:s0 + m]), None, m, ld, 0, ld, L.ptr(a1t),
-                                                L.ptr(d2t), L.ptr(part), 0, waves, self._stream))
+                                                L.ptr(d2t), L.ptr(part), 0, waves, 0, self._stream))
 
         if self._critic_by_rows(steps):
             self._critic_grad_rows(steps, step_w, K, gW, gb, deltas, spec)
@@ -543,7 +573,14 @@ class ReinforceAgent:
             tail_m += counts[t_tail]
         R = max(H1p, H2p)
         a1t = torch.empty(R, ld, dtype=torch.float32, device=self.device)     # 16-column blocks (include/g2048.h)
-        d2t = torch.empty(R, ld, dtype=torch.float32, device=self.device)
+        # ReLU: the factored d2 form -- one 1 KiB record (mask words + g) per 16 columns instead of d2 columns
+        fac = act == L.ACT_RELU and self.critic_factored_d2
+        if fac:
+            d2t = torch.empty(ld // 16 * 256, dtype=torch.float32, device=self.device)
+            w3 = torch.zeros(H2p, dtype=torch.float32, device=self.device)
+            w3[:h2] = params["W"][2][:, 0]
+        else:
+            d2t = torch.empty(R, ld, dtype=torch.float32, device=self.device)
         vout = torch.empty(max(max(counts), tail_m), dtype=torch.float32, device=self.device)
         gamma = float(c.gamma)
 
@@ -561,11 +598,15 @@ class ReinforceAgent:
                 return
             if self.grad_probe is not None:
                 for k_, s0_, cnt_, c0 in launched:
+                    d2c = _unrecord(d2t, w3, c0, cnt_) if fac else _unblock(d2t, H2p, c0, cnt_)
                     self.grad_probe("critic", k_, torch.arange(s0_, s0_ + cnt_, device=self.device),
-                                    _unblock(a1t, H1p, c0, cnt_), _unblock(d2t, H2p, c0, cnt_))
+                                    _unblock(a1t, H1p, c0, cnt_), d2c)
             launched.clear()
             fold()
-            self._dw2(a1t, d2t, h1, h2, used, big)   # every column < used was written by a row launch
+            if fac:   # every column < used was written by a row launch
+                self._dw2_factored(a1t, d2t, w3, h1, h2, used, big)
+            else:
+                self._dw2(a1t, d2t, h1, h2, used, big)
 
         def grad_launch(s0: int, cnt: int, tgt: torch.Tensor, k: int) -> None:
             nonlocal col, since_fold
@@ -579,7 +620,7 @@ class ReinforceAgent:
             L.check(self._lib.g2048_critic_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, loss,
                                                 float(c.huber_delta), L.ptr(b), L.ptr(tgt), L.ptr(step_w[s0:s0 + cnt]),
                                                 L.ptr(deltas[k, s0:s0 + cnt]), L.ptr(vout), cnt, ld, col, ncols,
-                                                L.ptr(a1t), L.ptr(d2t), L.ptr(part), 1, waves, self._stream))
+                                                L.ptr(a1t), L.ptr(d2t), L.ptr(part), 1, waves, int(fac), self._stream))
             launched.append((k, s0, cnt, col))
             col += ncols
             since_fold += 1

@@ -60,13 +60,15 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
 #endif
 }
 
-template <int NT1, int NT2>
+template <int NT1, int NT2, bool FAC>
 struct Dw2 {
     static constexpr int H1 = 32 * NT1, H2 = 32 * NT2;
     static constexpr int RB = H1 > H2 ? H1 : H2;        // rows per 16-column block of both column buffers
-    static constexpr int kRows = H1 + H2;               // staged rows: a1 rows, then d2 rows
-    static constexpr int kStageFloats = kRows * kBK;    // 64 B per staged row
-    static constexpr int kGlds = kRows / 16;            // 1 KiB LDS-DMA instructions per stage (16 rows each)
+    static constexpr int kRows = FAC ? H1 : H1 + H2;    // staged rows: a1 rows, then d2 rows (FAC: a1 rows only)
+    static constexpr int kRecFloats = FAC ? 256 : 0;    // FAC: the block's 1 KiB record (mask words, g)
+    static constexpr int kStageFloats = kRows * kBK + kRecFloats;   // 64 B per staged row
+    static constexpr int kRowGlds = kRows / 16;         // 1 KiB LDS-DMA instructions per stage (16 rows each)
+    static constexpr int kGlds = kRowGlds + (FAC ? 1 : 0);          // + the record
     static constexpr int kGldsPerWave = (kGlds + 3) / 4;
     static constexpr int TR = NT1 >= 2 ? NT1 / 2 : 1;   // row tiles per wave (2 x 2 wave grid)
     static constexpr int TC = NT2 >= 2 ? NT2 / 2 : 1;   // column tiles per wave
@@ -74,7 +76,8 @@ struct Dw2 {
 
 struct Dw2Args {
     const float* a1t;   // a1^T, 16-column blocks of RB rows
-    const float* d2t;   // d2^T, the same layout
+    const float* d2t;   // d2^T, the same layout (factored form: the 1 KiB block records)
+    const float* w3;    // factored form: W3[:, 0] padded to H2p
     float* part;        // [nparts][H1p + 1][H2p]
     uint32_t ld, col0, ncols, kb;   // column range [col0, col0 + ncols); workgroup p takes kb columns from col0 + p kb
 };
@@ -103,9 +106,12 @@ __device__ __forceinline__ void read_frag(const float* stage, int row, int h, fl
     v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
 }
 
-template <int NT1, int NT2>
+// FAC: the ReLU critic's factored form (g2048_critic_grad d2_form 1): d2 = m * (W3 g) with a 0/1 mask m and a scalar
+// g per sample, so dW2 = W3[j] * sum (a1 g) m^T and db2 = W3[j] * sum g m: the A operand is a1 * g (one fp32 product,
+// split exactly into three planes), the B operand the mask (exact in bf16), three MFMAs per step instead of six.
+template <int NT1, int NT2, bool FAC>
 __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
-    using G = Dw2<NT1, NT2>;
+    using G = Dw2<NT1, NT2, FAC>;
     __shared__ float S[kStages * G::kStageFloats];   // the only LDS object (see the glds / second-object rule)
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, r = lane & 31;
     const int wr = w >> 1, wc = w & 1;
@@ -116,23 +122,33 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     // this lane's LDS-DMA sources: instruction g (wave w issues g = w, w + 4, ...; past the end: the last one
     // again, an identical rewrite) covers staged rows 16 g .. 16 g + 15; lane -> row 16 g + (lane >> 2), slot
     // lane & 3, which holds the row's chunk (slot ^ ((row >> 2) & 3))
+    // (FAC: instruction kRowGlds copies the block's record, 16 B per lane, unswizzled, after the staged rows; which
+    // instruction that is depends only on the wave, so the per-stage source stride is a scalar)
+    const int ws = __builtin_amdgcn_readfirstlane(w);
+    const auto glds_index = [&](int i) {
+        const int g = ws + 4 * i;
+        return g < G::kGlds ? g : G::kGlds - 1;
+    };
     const float* src[G::kGldsPerWave];
 #pragma unroll
     for (int i = 0; i < G::kGldsPerWave; i++) {
-        int g = w + 4 * i;
-        g = g < G::kGlds ? g : G::kGlds - 1;
-        const int row = 16 * g + (lane >> 2);
-        const int chunk = (lane & 3) ^ ((lane >> 4) & 3);
-        const float* base = row < G::H1 ? a.a1t + row * kBK : a.d2t + (row - G::H1) * kBK;
-        src[i] = base + (size_t)(k_begin / kBK) * G::RB * kBK + 4 * chunk;   // block k_begin / 16
+        const int g = glds_index(i);
+        if (FAC && g == G::kRowGlds) {
+            src[i] = a.d2t + (size_t)(k_begin / kBK) * 256 + 4 * lane;
+        } else {
+            const int row = 16 * g + (lane >> 2);
+            const int chunk = (lane & 3) ^ ((lane >> 4) & 3);
+            const float* base = row < G::H1 ? a.a1t + row * kBK : a.d2t + (row - G::H1) * kBK;
+            src[i] = base + (size_t)(k_begin / kBK) * G::RB * kBK + 4 * chunk;   // block k_begin / 16
+        }
     }
     const auto issue_to = [&](int slot, int stage_idx) {
         float* dst = S + slot * G::kStageFloats;
 #pragma unroll
         for (int i = 0; i < G::kGldsPerWave; i++) {
-            int g = w + 4 * i;
-            g = g < G::kGlds ? g : G::kGlds - 1;
-            glds16(src[i] + (size_t)stage_idx * G::RB * kBK, dst + 16 * g * kBK);
+            const int g = glds_index(i);
+            const uint32_t stride = (FAC && g == G::kRowGlds) ? 256u : (uint32_t)(G::RB * kBK);
+            glds16(src[i] + (size_t)stage_idx * stride, dst + 16 * g * kBK);
         }
     };
 
@@ -144,6 +160,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     const bool rows_mine = NT1 >= 2 || wr == 0, cols_mine = NT2 >= 2 || wc == 0;
     // db2: thread t sums d2 row t (threads past H2 sum row H2 - 1 and never store: no branch in the loop body)
     const int drow = G::H1 + (t < G::H2 ? t : G::H2 - 1);
+    const int dunit = t < G::H2 ? t : G::H2 - 1;
     float dsum = 0.0f;
 
     // the bf16 planes of one stage's operand fragments (this wave's A rows and B rows), double-buffered: the loop
@@ -151,7 +168,47 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     struct Planes {
         bf16x8 a0[G::TR], a1[G::TR], a2[G::TR], b0[G::TC], b1[G::TC], b2[G::TC];
     };
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const auto load = [&](const float* st, Planes& p) {
+        if constexpr (FAC) {
+            const float* rec = st + G::kRows * kBK;
+            const uint16_t* mw = reinterpret_cast<const uint16_t*>(rec);
+            const float* gv = rec + 128;   // byte 512: g of the block's 16 samples
+            {   // db2 (before the W3 scaling): sum over the samples of g where unit `dunit`'s mask bit is set
+                const uint32_t m = mw[dunit];
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const float4 x = *reinterpret_cast<const float4*>(gv + 4 * c);
+                    dsum += ((m >> (4 * c + 0)) & 1u) ? x.x : 0.0f;
+                    dsum += ((m >> (4 * c + 1)) & 1u) ? x.y : 0.0f;
+                    dsum += ((m >> (4 * c + 2)) & 1u) ? x.z : 0.0f;
+                    dsum += ((m >> (4 * c + 3)) & 1u) ? x.w : 0.0f;
+                }
+            }
+            if (rows_mine && cols_mine) {
+                const float4 g0 = *reinterpret_cast<const float4*>(gv + 8 * h);
+                const float4 g1 = *reinterpret_cast<const float4*>(gv + 8 * h + 4);
+                const float gk[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+                for (int i = 0; i < G::TR; i++) {
+                    float v[8];
+                    read_frag(st, 32 * (wr * G::TR + i) + r, h, v);
+#pragma unroll
+                    for (int e = 0; e < 8; e++) v[e] *= gk[e];   // a1 g: the one rounding of the factored form
+                    split3(v, p.a0[i], p.a1[i], p.a2[i]);
+                }
+#pragma unroll
+                for (int j = 0; j < G::TC; j++) {   // mask bits 8h .. 8h+7 of unit n as bf16 1.0 (0x3F80) / 0
+                    const uint32_t m = (uint32_t)mw[32 * (wc * G::TC + j) + r] >> (8 * h);
+                    u32x4 q;
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        q[e] = (((m >> (2 * e)) & 1u) * 0x3F80u) | (((m >> (2 * e + 1)) & 1u) * 0x3F800000u);
+                    p.b0[j] = __builtin_bit_cast(bf16x8, q);
+                }
+            }
+            return;
+        }
         const float* rowp = st + drow * kBK;
 #pragma unroll
         for (int c = 0; c < 4; c++) {
@@ -183,6 +240,13 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
 #pragma unroll
                 for (int j = 0; j < G::TC; j++) {
                     floatx16 c = acc[i][j];   // smallest terms first
+                    if constexpr (FAC) {      // (a1 g) m: the mask is exact in one plane
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a2[i], p.b0[j], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a1[i], p.b0[j], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a0[i], p.b0[j], c, 0, 0, 0);
+                        acc[i][j] = c;
+                        continue;
+                    }
                     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a2[i], p.b0[j], c, 0, 0, 0);
                     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a1[i], p.b1[j], c, 0, 0, 0);
                     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a0[i], p.b2[j], c, 0, 0, 0);
@@ -205,7 +269,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
         asm volatile("" ::: "memory");
         load(S + ((it + 1) % kStages) * G::kStageFloats, nxt);
         mfma(cur);
-        constexpr int kMfma = 6 * G::TR * G::TC;
+        constexpr int kMfma = (FAC ? 3 : 6) * G::TR * G::TC;
         __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // DS read: the first fragments' reads up front
 #pragma unroll
         for (int m = 0; m < kMfma; m++) {
@@ -236,26 +300,30 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
         }
     }
     // this workgroup's slab: dW2 rows from the accumulators (C/D layout: column = lane & 31, row = acc_row), db2
+    // (FAC: each column scaled by W3[j] -- the one multiply of the factored form)
     float* out = a.part + (size_t)blockIdx.x * (G::H1 + 1) * G::H2;
     if (rows_mine && cols_mine) {
 #pragma unroll
-        for (int i = 0; i < G::TR; i++)
+        for (int j = 0; j < G::TC; j++) {
+            const float ws = FAC ? a.w3[32 * (wc * G::TC + j) + r] : 1.0f;
 #pragma unroll
-            for (int j = 0; j < G::TC; j++)
+            for (int i = 0; i < G::TR; i++)
 #pragma unroll
                 for (int q = 0; q < 16; q++)
-                    out[(size_t)(32 * (wr * G::TR + i) + acc_row(q, h)) * G::H2 + 32 * (wc * G::TC + j) + r] = acc[i][j][q];
+                    out[(size_t)(32 * (wr * G::TR + i) + acc_row(q, h)) * G::H2 + 32 * (wc * G::TC + j) + r] =
+                        FAC ? acc[i][j][q] * ws : acc[i][j][q];
+        }
     }
-    if (t < G::H2) out[(size_t)G::H1 * G::H2 + t] = dsum;
+    if (t < G::H2) out[(size_t)G::H1 * G::H2 + t] = FAC ? dsum * a.w3[t] : dsum;
 }
 
-template <int NT1>
+template <int NT1, bool FAC>
 void launch_nt2(const Dw2Args& a, int nt2, int grid, hipStream_t s) {
     switch (nt2) {
-        case 1: hipLaunchKernelGGL((dw2_kernel<NT1, 1>), dim3(grid), dim3(kThreads), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((dw2_kernel<NT1, 2>), dim3(grid), dim3(kThreads), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((dw2_kernel<NT1, 4>), dim3(grid), dim3(kThreads), 0, s, a); break;
-        default: hipLaunchKernelGGL((dw2_kernel<NT1, 8>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((dw2_kernel<NT1, 1, FAC>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((dw2_kernel<NT1, 2, FAC>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((dw2_kernel<NT1, 4, FAC>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        default: hipLaunchKernelGGL((dw2_kernel<NT1, 8, FAC>), dim3(grid), dim3(kThreads), 0, s, a); break;
     }
 }
 
@@ -299,11 +367,11 @@ namespace g2048_internal {
 int set_error(int code, const char* msg);
 }
 
-extern "C" int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int64_t ld, int64_t col0, int64_t ncols,
-                         int64_t cols_per_part, float* partials, int64_t nparts, void* stream) {
+static int dw2_launch(const float* a1t, const float* d2t, const float* w3, bool fac, int h1, int h2, int64_t ld,
+                      int64_t col0, int64_t ncols, int64_t cols_per_part, float* partials, int64_t nparts, void* stream) {
     using g2048_internal::set_error;
     if (h1 < 1 || h1 > 256 || h2 < 1 || h2 > 256) return set_error(G2048_EINVAL, "dw2: hidden sizes must be in 1..256");
-    if (!a1t || !d2t || !partials) return set_error(G2048_EINVAL, "dw2: NULL buffer");
+    if (!a1t || !d2t || !partials || (fac && !w3)) return set_error(G2048_EINVAL, "dw2: NULL buffer");
     if (ld <= 0 || (ld & 15) || ld > ((int64_t)1 << 28)) return set_error(G2048_EINVAL, "dw2: ld must be a positive multiple of 16");
     if (col0 < 0 || (col0 & 15) || ncols < 0 || (ncols & 15) || col0 + ncols > ld)
         return set_error(G2048_EINVAL, "dw2: column range must be multiples of 16 inside ld");
@@ -311,19 +379,30 @@ extern "C" int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int
     if (nparts != (ncols + cols_per_part - 1) / cols_per_part || nparts > 65535)
         return set_error(G2048_EINVAL, "dw2: nparts must be ceil(ncols / cols_per_part) (<= 65535)");
     if (nparts == 0) return G2048_OK;
-    Dw2Args a{a1t, d2t, partials, (uint32_t)ld, (uint32_t)col0, (uint32_t)ncols, (uint32_t)cols_per_part};
+    Dw2Args a{a1t, d2t, w3, partials, (uint32_t)ld, (uint32_t)col0, (uint32_t)ncols, (uint32_t)cols_per_part};
     const int nt1 = tiles_of(h1), nt2 = tiles_of(h2);
     hipStream_t s = (hipStream_t)stream;
     const int grid = (int)nparts;
     switch (nt1) {
-        case 1: launch_nt2<1>(a, nt2, grid, s); break;
-        case 2: launch_nt2<2>(a, nt2, grid, s); break;
-        case 4: launch_nt2<4>(a, nt2, grid, s); break;
-        default: launch_nt2<8>(a, nt2, grid, s); break;
+        case 1: fac ? launch_nt2<1, true>(a, nt2, grid, s) : launch_nt2<1, false>(a, nt2, grid, s); break;
+        case 2: fac ? launch_nt2<2, true>(a, nt2, grid, s) : launch_nt2<2, false>(a, nt2, grid, s); break;
+        case 4: fac ? launch_nt2<4, true>(a, nt2, grid, s) : launch_nt2<4, false>(a, nt2, grid, s); break;
+        default: fac ? launch_nt2<8, true>(a, nt2, grid, s) : launch_nt2<8, false>(a, nt2, grid, s); break;
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(G2048_EHIP, hipGetErrorString(e));
     return G2048_OK;
+}
+
+extern "C" int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int64_t ld, int64_t col0, int64_t ncols,
+                         int64_t cols_per_part, float* partials, int64_t nparts, void* stream) {
+    return dw2_launch(a1t, d2t, nullptr, false, h1, h2, ld, col0, ncols, cols_per_part, partials, nparts, stream);
+}
+
+extern "C" int g2048_dw2_factored(const float* a1t, const float* records, const float* w3, int h1, int h2, int64_t ld,
+                                  int64_t col0, int64_t ncols, int64_t cols_per_part, float* partials, int64_t nparts,
+                                  void* stream) {
+    return dw2_launch(a1t, records, w3, true, h1, h2, ld, col0, ncols, cols_per_part, partials, nparts, stream);
 }
 
 extern "C" int g2048_fold_partials(const float* partials, int64_t nparts, int64_t slab, double* acc, void* stream) {

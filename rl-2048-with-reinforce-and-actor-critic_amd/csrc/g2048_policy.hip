@@ -680,6 +680,8 @@ struct GradArgs {
     // col_off .. col_off + 32 ngroups - 1; those past n are written as zero-coefficient padding)
     uint32_t col_off, ngroups;
     int part_accum;          // add this launch's per-wave partials to `part` instead of overwriting it
+    int d2_form;             // 1 (critic, ReLU): d2t receives the factored record of each 16-column block instead
+                             // of d2 columns (g2048_critic_grad in include/g2048.h; the FAC kernel variant)
 };
 
 template <int NT1, int NT2>
@@ -729,7 +731,11 @@ __device__ __forceinline__ float4 frag_load(__amdgpu_buffer_rsrc_t r, uint32_t v
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
 
-template <int NT1, int NT2, int ACT, int OBS>
+// FAC (critic, ReLU): d2 = m * (W3 g) with m = [a2 > 0] and a scalar g per sample, so instead of the d2 columns the
+// kernel writes, per 16-column block, a 1 KiB record: the ReLU mask as one 16-bit word per second-layer unit (bit k =
+// sample 16 c + k) at bytes [0, 2 H2p), and g of the 16 samples at bytes [512, 576); g2048_dw2_factored rebuilds
+// dW2 = W3 * sum (a1 g) m^T from it (64 B per sample written and read instead of 1 KiB).
+template <int NT1, int NT2, int ACT, int OBS, int FAC = 0>
 __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
     typedef float floatx4 __attribute__((ext_vector_type(4)));
     constexpr int H1p = 32 * NT1, H2p = 32 * NT2;
@@ -750,7 +756,8 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
     float gsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // db3 partial (lanes of half 0)
     constexpr uint32_t RB = 32u * (NT1 > NT2 ? NT1 : NT2);   // rows per 16-column block of both column buffers
     const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc(a.a1t, 0, (int)(RB * a.ld * 4u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rd2 = __builtin_amdgcn_make_buffer_rsrc(a.d2t, 0, (int)(RB * a.ld * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd2 = __builtin_amdgcn_make_buffer_rsrc(
+        a.d2t, 0, FAC ? (int)((a.ld >> 4) * 1024u) : (int)(RB * a.ld * 4u), 0x00020000);
     floatx4 dw1acc[2 * NT1], dw3acc[2 * NT2];  // dW1^T / dW3^T 16x16 accumulator blocks, across the wave's groups
 #pragma unroll
     for (int k = 0; k < 2 * NT1; k++) dw1acc[k] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -935,10 +942,32 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
             __builtin_amdgcn_sched_barrier(0);
         }
         GRAD_PH(2);
-        // ---- d2 = act'(a2) * (W3 g), in place; d2^T columns
+        // ---- d2 = act'(a2) * (W3 g), in place; d2^T columns (FAC: the block records' mask words and g instead)
+        if constexpr (FAC) {
+            if (h == 0) {   // g of this lane's sample at byte 512 + 4 (cj & 15) of its block's record
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g[0]), rd2, (int)((cj >> 4) * 1024u + 512u + (cj & 15u) * 4u),
+                                                      0, 0);
+            }
+        }
 #pragma unroll
         for (int o = 0; o < NT2; o++) {
             opaque_sgpr(ld4);
+            if constexpr (FAC) {
+                // ballot of a2 > 0 per register r: bits 0..31 = samples of unit acc_row(r, 0), 32..63 = of unit
+                // acc_row(r, 1); lane L = 4 r + 2 h' + b stores the 16-bit word of unit 32 o + acc_row(r, h') for
+                // the group's block b (one 16-bit store per lane covers the tile's 32 units x 32 samples)
+                uint32_t mv = 0u;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const uint64_t bal = __ballot(h2[o][r] > 0.0f);
+                    const uint32_t hw = (uint32_t)(bal >> (32 * ((lane >> 1) & 1)));
+                    const uint32_t part = (hw >> (16 * (lane & 1))) & 0xFFFFu;
+                    mv = (lane >> 2) == r ? part : mv;
+                }
+                const uint32_t unit = 32u * (uint32_t)o + (uint32_t)acc_row(lane >> 2, (lane >> 1) & 1);
+                const uint32_t blk = ((a.col_off + gi * 32u) >> 4) + (uint32_t)(lane & 1);
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)mv, rd2, (int)(blk * 1024u + unit * 2u), 0, 0);
+            }
             const float4* w3 = reinterpret_cast<const float4*>(sm.w3p() + (o * 2 + h) * 64);
 #pragma unroll
             for (int r = 0; r < 16; r++) {
@@ -987,12 +1016,14 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fw[q].w, h2[t2][4 * q + 3], acc, 0, 0, 0);
                 }
                 // d2 value r of tile t2 goes out at input tile (r * NT1) / 16
+                if constexpr (!FAC) {
 #pragma unroll
-                for (int r = 0; r < 16; r++)
-                    if ((r * NT1) / 16 == o1) {
-                        opaque_sgpr(ld4);
-                        col_store(rd2, 32 * t2 + acc_row(r, 0), ld4, off, h2[t2][r]);
-                    }
+                    for (int r = 0; r < 16; r++)
+                        if ((r * NT1) / 16 == o1) {
+                            opaque_sgpr(ld4);
+                            col_store(rd2, 32 * t2 + acc_row(r, 0), ld4, off, h2[t2][r]);
+                        }
+                }
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     fw[q] = fn[q];
@@ -1059,7 +1090,10 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
 
 template <int NT1, int NT2>
 void launch_grad(const GradArgs& a, int act, int obs, int grid, hipStream_t s) {
-    if (act == G2048_ACT_RELU) {
+    if (act == G2048_ACT_RELU && a.d2_form) {
+        if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_LOG2, 1>), dim3(grid), dim3(kPolBlock), 0, s, a);
+        else hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_RAW, 1>), dim3(grid), dim3(kPolBlock), 0, s, a);
+    } else if (act == G2048_ACT_RELU) {
         if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_LOG2>), dim3(grid), dim3(kPolBlock), 0, s, a);
         else hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_RAW>), dim3(grid), dim3(kPolBlock), 0, s, a);
     } else {
@@ -1251,7 +1285,7 @@ static int actor_or_critic_grad(const float* packed, const float* grad_packed, i
                          float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions,
                          const float* coef, int64_t n, int64_t ld, int64_t col_off, int64_t ncols, float* a1t, float* d2t,
                          float* partials, int accumulate, int64_t waves, void* stream, int critic, int huber,
-                         float huber_delta, const float* target, float* delta_out, float* v_out) {
+                         float huber_delta, const float* target, float* delta_out, float* v_out, int d2_form = 0) {
     if (n < 0 || ld < n || (ld & 31) || ld > ((int64_t)1 << 21)) return pfail(G2048_EINVAL, "fused gradient: bad n / ld");
     if (col_off < 0 || (col_off & 31) || ncols < n || (ncols & 31) || col_off + ncols > ld)
         return pfail(G2048_EINVAL, "fused gradient: bad column window (col_off / ncols multiples of 32, n <= ncols, "
@@ -1264,6 +1298,8 @@ static int actor_or_critic_grad(const float* packed, const float* grad_packed, i
     if (!packed || !grad_packed || !a1t || !d2t || !partials || (n > 0 && (!boards || !coef)))
         return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
     if (waves != g2048_actor_grad_waves()) return pfail(G2048_EINVAL, "fused gradient: waves != g2048_actor_grad_waves()");
+    if (d2_form != 0 && (d2_form != 1 || !critic || activation != G2048_ACT_RELU))
+        return pfail(G2048_EINVAL, "fused gradient: d2_form 1 (factored) is for the ReLU critic only");
     GradArgs a;
     a.net = packed;
     a.w2b = grad_packed;
@@ -1286,6 +1322,7 @@ static int actor_or_critic_grad(const float* packed, const float* grad_packed, i
     a.col_off = (uint32_t)col_off;
     a.ngroups = (uint32_t)(ncols >> 5);
     a.part_accum = accumulate;
+    a.d2_form = d2_form;
     const int grid = (int)(waves / (kPolBlock / 64));   // one workgroup per CU; every wave writes its partial row
     const int nt1 = tiles_for(h1), nt2 = tiles_for(h2);
     hipStream_t s = (hipStream_t)stream;
@@ -1313,12 +1350,12 @@ int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int
                       float obs_scale, int loss, float huber_delta, const uint64_t* boards, const float* target,
                       const float* weight, float* delta_out, float* value_out, int64_t n, int64_t ld, int64_t col_off,
                       int64_t ncols, float* a1t, float* d2t, float* partials, int accumulate, int64_t waves,
-                      void* stream) {
+                      int d2_form, void* stream) {
     if (loss != 0 && loss != 1) return pfail(G2048_EINVAL, "Unknown critic loss type");
     if (n > 0 && !target) return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
     return actor_or_critic_grad(packed, grad_packed, h1, h2, activation, obs_mode, obs_scale, 0, boards, nullptr, weight,
                                 n, ld, col_off, ncols, a1t, d2t, partials, accumulate, waves, stream, 1, loss,
-                                huber_delta, target, delta_out, value_out);
+                                huber_delta, target, delta_out, value_out, d2_form);
 }
 
 int g2048_rollout(const float* packed, int h1, int h2, int activation, const g2048_env_cfg* cfg, int greedy,

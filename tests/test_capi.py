@@ -31,7 +31,7 @@ def test_header_declares_expected_api():
         "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_packed_size",
         "g2048_policy_pack", "g2048_policy", "g2048_rollout", "g2048_grad_packed_size", "g2048_grad_partial_size",
         "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2",
-        "g2048_fold_partials"])
+        "g2048_fold_partials", "g2048_dw2_factored"])
 
 
 def test_library_exports_every_declared_symbol(L):
@@ -116,12 +116,19 @@ def test_argument_validation_without_gpu(L):
     gargs[12], gargs[5] = 64, L.OBS_ONEHOT
     assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL and b"obs_mode" in lib.g2048_last_error()
     cargs = [p, p, 32, 32, L.ACT_RELU, L.OBS_LOG2, 1.0, 2, 1.0, p, p, p, None, None, 40, 128, 0, 64, p, p, p, 0, 1024,
-             None]
+             0, None]
     assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"critic loss" in lib.g2048_last_error()
     cargs[7] = 0
     for col_off, ncols in ((16, 64), (0, 32), (96, 64), (-32, 64)):   # unaligned, < n, past ld, negative
         cargs[16], cargs[17] = col_off, ncols
         assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"column window" in lib.g2048_last_error()
+    cargs[16], cargs[17] = 0, 64
+    cargs[4], cargs[23] = L.ACT_SIGMOID, 1      # the factored d2 form needs ReLU's 0/1 derivative
+    assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"factored" in lib.g2048_last_error()
+    cargs[4], cargs[23] = L.ACT_RELU, 2
+    assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"factored" in lib.g2048_last_error()
+    dargs = [p, p, None, 32, 32, 64, 0, 64, 64, p, 1, None]   # factored dW2 without W3
+    assert lib.g2048_dw2_factored(*dargs) == L.G2048_EINVAL and b"NULL" in lib.g2048_last_error()
 
 
 def test_config_validation_messages():

@@ -193,14 +193,16 @@ def test_fused_critic_grad_ragged_chunks(chunk, act):
 
 
 @pytest.mark.parametrize("aug,tail", [(False, 0), (True, 0), (False, 64), (True, 100000)])
-@pytest.mark.parametrize("act", ["Sigmoid", "ReLU"])
-def test_fused_critic_rows_mode(act, aug, tail):
+@pytest.mark.parametrize("act,fac", [("Sigmoid", False), ("ReLU", True), ("ReLU", False)])
+def test_fused_critic_rows_mode(act, fac, aug, tail):
     """The per-time-row critic pass (ReinforceAgent._critic_grad_rows: rows last-first, each launch's V(s) serving as
     the previous row's V(s'), one column buffer, accumulated partials) forced on a small batch -- hundreds of
     rows, most of them ragged, a column-buffer flush forced by a small chunk -- against the torch backprop: critic
     and actor gradients and the TD errors (through the actor's advantages).  `tail`: rows below that many samples
     run as the one tail launch with its own V(s') forward (0: none; 64: the later rows, handing over to the chain;
-    100000: all rows, capped by the column buffer).  Gradients: _check_fused_vs_plain (1e-5)."""
+    100000: all rows, capped by the column buffer).  `fac`: the ReLU critic's factored d2 records
+    (g2048_critic_grad d2_form 1 + g2048_dw2_factored, the default) or d2 columns.  Gradients: _check_fused_vs_plain
+    (1e-5 against the exact value under the fused kernels' own ReLU pattern)."""
     acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.97, use_critic=True, critic_loss_type="huber",
                 huber_delta=0.5, augmentation=aug)
     runs = {}
@@ -210,6 +212,7 @@ def test_fused_critic_rows_mode(act, aug, tail):
         ag.use_fused_grad = mode == "fused"
         ag.critic_rows_min_avg = 0
         ag.critic_tail_row_max = tail
+        ag.critic_factored_d2 = fac
         ag.grad_chunk_steps = 4096
         if batch is None:
             batch = ag.rollout_batch(list(range(100, 100 + 160)), list(range(900, 900 + 160)))
@@ -306,3 +309,64 @@ def test_fold_partials_matches_fp64_sum(nparts, slab):
     assert torch.equal(again, acc)
     with pytest.raises(ValueError):
         L.check(L.lib().g2048_fold_partials(None, nparts, slab, L.ptr(acc), L.stream_handle(DEV)))
+
+
+@pytest.mark.parametrize("h1,h2", [(256, 256), (32, 16), (200, 40)])
+@pytest.mark.parametrize("ncols,cpp", [(4096, 2048), (2048 + 16 * 37, 2048), (48, 2048)])
+def test_dw2_factored_kernel_matches_fp64(h1, h2, ncols, cpp):
+    """g2048_dw2_factored (the ReLU critic's dW2 / db2 from the factored records of g2048_critic_grad d2_form 1:
+    a 16-bit mask word per unit and g per column, per 16-column block) against fp64 of W3[j] * sum fl(a1 g) m and
+    W3[j] * sum g m on the same inputs: within 4e-6 of the sum of |terms|, full and padded hidden sizes, a column
+    range starting inside the buffer and partial last slabs."""
+    from rl2048_amd import _lib as L
+    from rl2048_amd.agent import _padded_units, _unrecord
+
+    H1p, H2p = _padded_units(h1), _padded_units(h2)
+    R = max(H1p, H2p)
+    col0 = 32
+    ld = col0 + ncols + 32
+    g = torch.Generator(device=DEV)
+    g.manual_seed(h1 * 7 + ncols)
+    A = torch.zeros(R, ld, device=DEV)
+    A[:h1] = torch.relu(torch.randn(h1, ld, device=DEV, generator=g) *
+                        torch.exp(3 * torch.randn(h1, ld, device=DEV, generator=g)))
+    gc = torch.randn(ld, device=DEV, generator=g) * torch.exp(2 * torch.randn(ld, device=DEV, generator=g))
+    M = (torch.rand(H2p, ld, device=DEV, generator=g) < 0.5)
+    M[h2:] = False
+    w3 = torch.zeros(H2p, device=DEV)
+    w3[:h2] = torch.randn(h2, device=DEV, generator=g)
+    # the records: uint16 mask words at bytes [0, 2 H2p), g at float 128.. of each 1 KiB block
+    rec = torch.zeros(ld // 16, 256, device=DEV)
+    words = torch.zeros(ld // 16, H2p, dtype=torch.int32, device=DEV)
+    for k in range(16):
+        words |= M[:, k::16].t().to(torch.int32) << k
+    w16 = torch.where(words >= 32768, words - 65536, words).to(torch.int16)
+    rec.view(torch.int16)[:, :H2p] = w16
+    rec[:, 128:144] = gc.view(-1, 16)
+    rec = rec.reshape(-1).contiguous()
+    # the record decoder used by the gradient probe gives back fl(g W3[j]) m
+    dec = _unrecord(rec, w3, col0, ncols)
+    assert torch.equal(dec, ((gc[None, col0:col0 + ncols] * w3[:, None]) * M[:, col0:col0 + ncols].float()))
+    blocked = lambda X: X.reshape(R, ld // 16, 16).permute(1, 0, 2).contiguous()  # noqa: E731 (include/g2048.h)
+    a_in = blocked(A)
+    nparts = -(-ncols // cpp)
+    part = torch.full((nparts, H1p + 1, H2p), float("nan"), device=DEV)
+    lib = L.lib()
+    L.check(lib.g2048_dw2_factored(L.ptr(a_in), L.ptr(rec), L.ptr(w3), h1, h2, ld, col0, ncols, cpp, L.ptr(part),
+                                   nparts, L.stream_handle(DEV)))
+    torch.cuda.synchronize()
+    AG = (A[:H1p, col0:col0 + ncols] * gc[None, col0:col0 + ncols]).double()   # fl(a1 g), then exact
+    M64 = M[:, col0:col0 + ncols].double()
+    W = w3.double()[None, :]
+    G64 = gc[col0:col0 + ncols].double()
+    for p in range(nparts):
+        sl = slice(p * cpp, min((p + 1) * cpp, ncols))
+        ref = (AG[:, sl] @ M64[:, sl].t()) * W
+        bound = (AG[:, sl].abs() @ M64[:, sl].t()) * W.abs()
+        got = part[p, :H1p].double()
+        rel = float(((got - ref).abs() / bound.clamp_min(1e-30)).max())
+        print(f"slab {p}: max |err| / sum |terms| = {rel:.3g}")
+        assert bool(((got - ref).abs() <= 4e-6 * bound + 1e-30).all()), (p, rel)
+        db = (M64[:, sl] @ G64[sl]) * w3.double()
+        dbb = (M64[:, sl] @ G64[sl].abs()) * w3.double().abs()
+        assert bool(((part[p, H1p].double() - db).abs() <= 4e-6 * dbb + 1e-30).all()), p
