@@ -35,7 +35,7 @@ namespace {
 thread_local std::string g_err;
 std::mutex g_mu;
 constexpr int kMaxDev = 64;
-uint8_t* g_tab[kMaxDev] = {};   // [65536 x u16 line table][32768 x u8 merge codes, two per byte]
+uint8_t* g_tab[kMaxDev] = {};   // [65536 x u16 line table][32768 x u8 merge codes][32768 x u8 max-merge fields]
 int g_cus[kMaxDev] = {};
 
 int fail(int code, const std::string& msg) {
@@ -55,6 +55,14 @@ int fail(int code, const std::string& msg) {
 // 8 one sweep per wave per launch-equivalent grid (grid = ceil(n / 1024)), 16 no obs writes.
 #ifndef G2048_DIAG
 #define G2048_DIAG 0
+#endif
+#ifndef G2048_LEAN
+#define G2048_LEAN 1
+#endif
+// G2048_WT: the step loop's 16-B per-lane stores (log2 / raw obs, PCG64 state) write through L2 (sc1 buffer stores)
+// instead of leaving dirty lines for the end-of-kernel L2 writeback (tools/kend.hip measures that writeback)
+#ifndef G2048_WT
+#define G2048_WT 0
 #endif
 
 
@@ -78,6 +86,11 @@ constexpr int kBlock = 1024;                  // 16 waves per CU; one workgroup 
 constexpr int kLines = 65536;
 constexpr int kTabBytes = kLines * 2 + kLines / 2;   // 163,840 B = the whole LDS of a gfx950 CU
 constexpr int kTabVec = kTabBytes / 16;
+// the device table in global memory: the line table, the merge codes (board_move_coded: the general reward path,
+// the move / rollout kernels) and the max-merge fields (board_move_lean: the log2-reward step path).  A step
+// kernel stages the line table and ONE of the two 4-bit tables in LDS (160 KiB).
+constexpr int kMxOff = kTabBytes;
+constexpr int kDevTabBytes = kTabBytes + kLines / 2;
 constexpr int kLutSmallN = 16384;             // below this many lanes the tables are read through L1/L2
 constexpr int64_t kMaxLanesPerLaunch = int64_t(1) << 27;   // keeps every byte offset (<= 16 B/lane) in 32 bits
 
@@ -93,6 +106,15 @@ __device__ __forceinline__ void st(T* p, uint32_t idx, T v) {
 
 // observation stores are non-temporal (streaming): measured on MI355X, onehot obs (1,088 B/board) 260 -> 241 us at
 // 1M boards and 1050 -> 908 us at 4M; log2 obs unchanged (tools/ab_nt.sh, profiles/round1/ab_nt.log)
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+constexpr int kRsrcFlags = 0x00020000;   // buffer resource dword3 (raw 32-bit dwords)
+constexpr int kAuxSc1 = 16;              // buffer op aux bit: sc1 (write through L2)
+
+// 16-B write-through store at byte offset off of a buffer resource
+__device__ __forceinline__ void st16_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, f4v_t v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, kAuxSc1);
+}
+
 __device__ __forceinline__ void st_obs(float4* base, int q, float4 v) {
     typedef float f4v __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(base + q));
@@ -102,7 +124,7 @@ struct LineFn {
     const uint16_t* line;
     __device__ uint32_t operator()(uint32_t o) const { return line[o]; }
 };
-struct CodeFn {
+struct CodeFn {   // a 4-bit-per-line table: merge codes or max-merge fields
     const uint8_t* code;
     __device__ uint32_t operator()(uint32_t o) const { return (code[o >> 1] >> ((o & 1u) << 2)) & 15u; }
 };
@@ -145,22 +167,36 @@ __device__ inline void write_obs_wave(float* __restrict__ obs, uint32_t w0, uint
         }
     } else if constexpr (OBS == G2048_OBS_LOG2 || OBS == G2048_OBS_RAW) {
         float4* dst = reinterpret_cast<float4*>(obs) + (size_t)w0 * 4;
+#if G2048_WT
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 4096, kRsrcFlags);
+        const auto st_row = [&](int q, float4 v) { st16_wt(ro, (uint32_t)q * 16u, f4v_t{v.x, v.y, v.z, v.w}); };
+#else
+        const auto st_row = [&](int q, float4 v) { st_obs(dst, q, v); };
+#endif
+        const auto row_obs = [&](uint64_t bb, uint32_t row) {
+            const uint32_t r16 = (uint32_t)(bb >> (16u * row));
+            float v[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int q = k * 64 + lane;
-            const int src = q >> 2;
-            const uint32_t row = (uint32_t)q & 3u;
-            const uint64_t bb = shfl64(b, src);
-            if ((wmask >> src) & 1ull) {
-                const uint32_t r16 = (uint32_t)(bb >> (16u * row));
-                float v[4];
+            for (int t = 0; t < 4; t++) {
+                const uint32_t e = (r16 >> (4 * t)) & 15u;
+                if constexpr (OBS == G2048_OBS_LOG2) v[t] = (float)e * scale;
+                else v[t] = e ? (float)(1u << e) : 0.0f;
+            }
+            return make_float4(v[0], v[1], v[2], v[3]);
+        };
+        if (wmask == ~0ull) {   // wave-uniform: every board of the chunk writes (no per-store lane test)
 #pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const uint32_t e = (r16 >> (4 * t)) & 15u;
-                    if constexpr (OBS == G2048_OBS_LOG2) v[t] = (float)e * scale;
-                    else v[t] = e ? (float)(1u << e) : 0.0f;
-                }
-                st_obs(dst, q, make_float4(v[0], v[1], v[2], v[3]));
+            for (int k = 0; k < 4; k++) {
+                const int q = k * 64 + lane;
+                st_row(q, row_obs(shfl64(b, q >> 2), (uint32_t)q & 3u));
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int q = k * 64 + lane;
+                const int src = q >> 2;
+                const uint64_t bb = shfl64(b, src);
+                if ((wmask >> src) & 1ull) st_row(q, row_obs(bb, (uint32_t)q & 3u));
             }
         }
     }
@@ -302,9 +338,13 @@ __device__ inline void load_lane(const StepArgs& a, uint32_t i, LaneIn& x) {
 // rollout and bench path: no null-pointer tests in the loop, whose uniform conditions the compiler otherwise keeps
 // as spilled 64-bit lane masks), 1 = any of the first three, 2 = the merged list too; 3 = as 0 with the action
 // mask written packed (mask_bits) instead of as int8[4].
-template <int RNG, int XO>
+// RK (reward kind, chosen by the launcher): 0 = any config, `code` is the merge-code table (board_move_coded);
+// 1 = reward_mode "log2" with XO 0 / 3, `code` is the max-merge field table (board_move_lean: no merge decode,
+// no score, count and sum_e from board aggregates, the moved board's nz bits reused by the spawn and the masks).
+template <int RNG, int XO, int RK>
 __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, const LineFn& lut,
                                      const CodeFn& code, bool& wobs, bool& reset, uint32_t& mbits) {
+    static_assert(RK == 0 || XO == 0 || XO == 3, "the lean path writes no score / merged list");
     constexpr bool LIST = XO == 2, EXTRA = XO == 1 || XO == 2;
     const g2048_lanes& L = a.L;
     const uint64_t b = x.b;
@@ -326,22 +366,36 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
 
     // Game2048.step (src/game2048.py:40-70): move, score, spawn only if changed, done of the final board
     MoveSummary s;
-    uint64_t m;
+    uint64_t m, nzm = 0;
     if (G2048_DIAG && (a.diag & 4)) {
         s = MoveSummary{0, 0, 0, 0, 0, 0};
         m = b ^ ((uint64_t)x.act << 60);
+        nzm = nz_bits(m);
+    } else if constexpr (RK == 1) {
+        m = board_move_lean(b, x.act, lut, code, s, nzm);
     } else {
         m = board_move_coded<LIST>(b, x.act, lut, code, s);
     }
     const bool changed = m != b;
-    if (changed && !(G2048_DIAG && (a.diag & 4))) {
-        if constexpr (RNG == G2048_RNG_PCG64) m = spawn_pcg(m, x.g);
-        else m = spawn_philox(m, philox_ctr(a.key, x.seed, sc, 0u));
+    if constexpr (RK == 1) {
+        // nz bits of the final board: the moved board's, plus the spawned tile's
+        if (changed && !(G2048_DIAG && (a.diag & 4))) {
+            uint64_t nzbit;
+            if constexpr (RNG == G2048_RNG_PCG64) m = spawn_pcg_z(m, ~nzm & kNibLsb, x.g, nzbit);
+            else m = spawn_philox_z(m, ~nzm & kNibLsb, philox_ctr(a.key, x.seed, sc, 0u), nzbit);
+            nzm |= nzbit;
+        }
+    } else {
+        if (changed && !(G2048_DIAG && (a.diag & 4))) {
+            if constexpr (RNG == G2048_RNG_PCG64) m = spawn_pcg(m, x.g);
+            else m = spawn_philox(m, philox_ctr(a.key, x.seed, sc, 0u));
+        }
+        nzm = nz_bits(m);
     }
-    const BoardBits bits = board_bits(m);
+    const BoardBits bits = board_bits_nz(m, nzm);
     const bool done = bits_done(bits);
     const bool invalid = !changed && !done;
-    const double r = env_reward(a.rc, s, m, done, invalid, mt);
+    const double r = env_reward_nz<RK == 1>(a.rc, s, nzm, done, invalid, mt);
     const bool trunc = a.max_steps >= 0 && (int64_t)sc >= a.max_steps && !done;
     const uint32_t fl = (changed ? G2048_F_CHANGED : 0u) | (done ? G2048_F_TERMINATED : 0u) |
                         (trunc ? G2048_F_TRUNCATED : 0u) | (invalid ? G2048_F_INVALID : 0u) |
@@ -360,7 +414,17 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     st(a.out.flags, i, (uint8_t)fl);
     st(L.board, i, m);
     st(L.state, i, nst);
-    if constexpr (RNG == G2048_RNG_PCG64) store_pcg(L, i, x.g, false);
+    if constexpr (RNG == G2048_RNG_PCG64) {
+#if G2048_WT
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            L.rng_state, 0, (int)(a.n < (1u << 27) ? a.n * 16u : 0x7FFFFFF0u), kRsrcFlags);
+        st16_wt(rs, i * 16u, f4v_t{__uint_as_float((uint32_t)x.g.s_lo), __uint_as_float((uint32_t)(x.g.s_lo >> 32)),
+                                  __uint_as_float((uint32_t)x.g.s_hi), __uint_as_float((uint32_t)(x.g.s_hi >> 32))});
+        st(L.rng_uint, i, x.g.uinteger);
+#else
+        store_pcg(L, i, x.g, false);
+#endif
+    }
     wobs = true;
     mbits = bits_mask(bits);
     return m;
@@ -368,14 +432,14 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
 
 // One sweep of one wave: the step of board w0 + lane (inputs already in registers), its mask, the wave's obs.
 // A lane's first pending reset has its seed read here (`pseed`), so the read is long complete at the tail.
-template <int OBS, int RNG, int XO>
+template <int OBS, int RNG, int XO, int RK>
 __device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, LaneIn& x, const LineFn& lut,
                                       const CodeFn& code, uint64_t& pending, uint64_t& pseed, uint32_t k) {
     const uint32_t i = w0 + lane;
     bool wobs = false, reset = false;
     uint32_t mbits = 0;
     uint64_t b = 0;
-    if (i < a.n) b = step_lane<RNG, XO>(a, i, x, lut, code, wobs, reset, mbits);
+    if (i < a.n) b = step_lane<RNG, XO, RK>(a, i, x, lut, code, wobs, reset, mbits);
     if (reset) {
         if (!pending) {
             if constexpr (RNG == G2048_RNG_PCG64) pseed = ld(a.L.seed, i);
@@ -418,7 +482,7 @@ static_assert(kTabVec % kBlock == 0, "table fill: whole chunks per thread");
 // of a 1M-board step per CU cost one pass of one wave instead of one divergent pass in most of the 16 waves.
 // (A dynamic schedule -- chunks claimed with device-scope atomics -- measured slower on MI355X: under this
 // kernel's streaming load an atomic's return takes microseconds, and same-address atomics serialize.)
-template <int OBS, int RNG, bool LDS, int XO, int U>
+template <int OBS, int RNG, bool LDS, int XO, int U, int RK>
 __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     static_assert(U == 1, "one board per lane per sweep");
     __shared__ uint4 tab_lds[LDS ? kStepLdsVec : 1];
@@ -443,7 +507,8 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
                 uint32_t c = j + rot;
                 c -= c >= kChunks ? kChunks : 0u;
                 const uint32_t k = c * kBlock + threadIdx.x;
-                tab_lds[k] = src[k];
+                // chunks 8, 9 = the 4-bit table: merge codes (RK 0) or max-merge fields (RK 1, kMxOff)
+                tab_lds[k] = src[k + (RK == 1 && c >= 8u ? (uint32_t)((kMxOff - 2 * kLines) / 16) : 0u)];
             }
         }
         __syncthreads();
@@ -451,21 +516,21 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     }
     G2048_TS(1);
     const LineFn lut{reinterpret_cast<const uint16_t*>(tab)};
-    const CodeFn code{tab + 2 * kLines};
+    const CodeFn code{tab + (LDS || RK == 0 ? 2 * kLines : kMxOff)};
     uint64_t pending = 0, pseed = 0;
     uint32_t k = 0;
     while (w0 < a.n) {                         // wave-uniform
         const uint32_t w2 = w1 + wstride;
         load_lane<RNG>(a, lane_at(w2), C);
-        sweep<OBS, RNG, XO>(a, w0, lane, A, lut, code, pending, pseed, k);
+        sweep<OBS, RNG, XO, RK>(a, w0, lane, A, lut, code, pending, pseed, k);
         if (w1 >= a.n) break;
         const uint32_t w3 = w2 + wstride;
         load_lane<RNG>(a, lane_at(w3), A);
-        sweep<OBS, RNG, XO>(a, w1, lane, B, lut, code, pending, pseed, k + 1);
+        sweep<OBS, RNG, XO, RK>(a, w1, lane, B, lut, code, pending, pseed, k + 1);
         if (w2 >= a.n) break;
         const uint32_t w4 = w3 + wstride;
         load_lane<RNG>(a, lane_at(w4), B);
-        sweep<OBS, RNG, XO>(a, w2, lane, C, lut, code, pending, pseed, k + 2);
+        sweep<OBS, RNG, XO, RK>(a, w2, lane, C, lut, code, pending, pseed, k + 2);
         w0 = w3;
         w1 = w4;
         k += 3;
@@ -768,11 +833,13 @@ g2048_lanes shift_lanes(const g2048_lanes& L, int64_t off) {
 constexpr int kStepU = 1;
 
 template <int OBS, int RNG, bool LDS, int U>
-void launch_step3(const StepArgs& a, int grid, int xo, hipStream_t s) {
-    if (xo == 3) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 3, U>), dim3(grid), dim3(kBlock), 0, s, a);
-    else if (xo == 2) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 2, U>), dim3(grid), dim3(kBlock), 0, s, a);
-    else if (xo == 1) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 1, U>), dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 0, U>), dim3(grid), dim3(kBlock), 0, s, a);
+void launch_step3(const StepArgs& a, int grid, int xo, int rk, hipStream_t s) {
+    if (rk == 1 && xo == 3) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 3, U, 1>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (rk == 1 && xo == 0) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 0, U, 1>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (xo == 3) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 3, U, 0>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (xo == 2) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 2, U, 0>), dim3(grid), dim3(kBlock), 0, s, a);
+    else if (xo == 1) hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 1, U, 0>), dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((step_kernel<OBS, RNG, LDS, 0, U, 0>), dim3(grid), dim3(kBlock), 0, s, a);
 }
 
 template <int OBS, int RNG, int kU>
@@ -787,8 +854,11 @@ void launch_step_u(const StepArgs& a, int cus, hipStream_t s) {
     if (G2048_DIAG && (a.diag & 8)) grid = grid_for(a.n, kBlock, 1 << 30);
     int xo = a.out.merged ? 2 : (a.out.prev_board || a.out.reward64 || a.out.score_add) ? 1 : 0;
     if (xo == 0 && a.out.mask_bits && !a.out.mask) xo = 3;
-    if (lds) launch_step3<OBS, RNG, true, kU>(a, grid, xo, s);
-    else launch_step3<OBS, RNG, false, kU>(a, grid, xo, s);
+    // the lean summary path: log2 rewards, no score / merged-list outputs (G2048_LEAN=0 builds keep the general
+    // path for every config -- tools/ A/B only)
+    const int rk = G2048_LEAN && a.rc.reward_mode == 1 && (xo == 0 || xo == 3) ? 1 : 0;
+    if (lds) launch_step3<OBS, RNG, true, kU>(a, grid, xo, rk, s);
+    else launch_step3<OBS, RNG, false, kU>(a, grid, xo, rk, s);
 }
 
 template <int OBS, int RNG>
@@ -858,14 +928,20 @@ int g2048_init(int device) {
     int prev = 0;
     G2048_HIP(hipGetDevice(&prev));
     G2048_HIP(hipSetDevice(device));
-    static uint8_t host[kTabBytes];
+    static uint8_t host[kDevTabBytes];
     uint16_t* line = reinterpret_cast<uint16_t*>(host);
     uint8_t* code = host + 2 * kLines;
+    uint8_t* mx = host + kMxOff;
     for (uint32_t r = 0; r < (uint32_t)kLines; r++) {
         line[r] = (uint16_t)line_move_left(r);
-        const uint32_t c = line_merge_code(r);
-        if (r & 1u) code[r >> 1] = (uint8_t)(code[r >> 1] | (c << 4));
-        else code[r >> 1] = (uint8_t)c;
+        const uint32_t c = line_merge_code(r), f = line_max_merge_field(r);
+        if (r & 1u) {
+            code[r >> 1] = (uint8_t)(code[r >> 1] | (c << 4));
+            mx[r >> 1] = (uint8_t)(mx[r >> 1] | (f << 4));
+        } else {
+            code[r >> 1] = (uint8_t)c;
+            mx[r >> 1] = (uint8_t)f;
+        }
     }
     uint8_t* d = nullptr;
     hipError_t e = hipMalloc(&d, sizeof(host));

@@ -369,19 +369,95 @@ G2048_HD uint64_t board_move_alu(uint64_t b, uint32_t a, MoveSummary& s) {
     return g;
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Lean merge summary (the step kernel's log2-reward path).  The second row table holds, instead of the merge
+// code, one 4-bit field per line: 0 = no merge, else (largest merged exponent - 1), 1..15 (15 = a saturated
+// 15+15 merge, true exponent 16).  The rest of the summary comes from board aggregates: a merge of two x-tiles
+// leaves one (x+1)-tile and touches no other cell, so
+//   count = tiles(b) - tiles(g)   and   sum_e = sum(e) = nibsum(b) - nibsum(g) + 2 count
+// (each merge removes 2x and adds x+1 = e: nibsum drops by e - 2).  A saturated merge (15+15 -> 15) breaks the
+// second identity by 1, so a line field of 15 sends the lane to the exact per-line sum (line_merges).
+// ---------------------------------------------------------------------------------------------------------
+G2048_HD uint32_t line_max_merge_field(uint32_t row) {
+    uint32_t e0, e1;
+    (void)line_move_alu(row, e0, e1);  // merged exponents in position order, 16 = saturated
+    const uint32_t m = e0 > e1 ? e0 : e1;
+    return m ? m - 1u : 0u;            // merged exponents are >= 2, so 0 is free for "no merge"
+}
+
+// sum of the 16 nibbles of a board (<= 240)
+G2048_HD uint32_t nib_sum64(uint64_t x) {
+    const uint64_t t = (x & 0x0F0F0F0F0F0F0F0Full) + ((x >> 4) & 0x0F0F0F0F0F0F0F0Full);  // 8 bytes, each <= 30
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_sad_u8((uint32_t)t, 0u, __builtin_amdgcn_sad_u8((uint32_t)(t >> 32), 0u, 0u));
+#else
+    uint64_t y = t + (t >> 8);
+    y += y >> 16;
+    y += y >> 32;
+    return (uint32_t)(y & 0xFFu);
+#endif
+}
+
+// Game2048._move (src/game2048.py:158-165) with the line table and the max-merge field table (`mx`): the same
+// board as board_move_coded and the summary fields the log2 reward and max_tile_seen read -- count, sum_e,
+// max_e, overflow -- not score or the merged list.  nzg = nz_bits of the moved board (the spawn's empty cells).
+template <class Lut, class Mx>
+G2048_HD uint64_t board_move_lean(uint64_t b, uint32_t a, const Lut& lut, const Mx& mx, MoveSummary& s,
+                                  uint64_t& nzg) {
+    const uint64_t mvert = 0ull - (uint64_t)((a == 0u) | (a == 2u));
+    const uint64_t mrev = 0ull - (uint64_t)((a == 1u) | (a == 2u));
+    uint64_t f = b ^ ((b ^ transpose(b)) & mvert);
+    f ^= (f ^ reverse_rows(f)) & mrev;
+    uint32_t o[4], nw[4], fm[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) o[j] = (uint32_t)(f >> (16 * j)) & 0xFFFFu;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        nw[j] = (uint32_t)lut(o[j]);
+        fm[j] = (uint32_t)mx(o[j]);
+    }
+    uint64_t g = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) g |= (uint64_t)nw[j] << (16 * j);
+    const uint32_t m01 = fm[0] > fm[1] ? fm[0] : fm[1], m23 = fm[2] > fm[3] ? fm[2] : fm[3];
+    const uint32_t mf = m01 > m23 ? m01 : m23;
+    g ^= (g ^ reverse_rows(g)) & mrev;
+    g ^= (g ^ transpose(g)) & mvert;
+    nzg = nz_bits(g);
+    s.max_e = mf ? mf + 1u : 0u;
+    s.overflow = mf == 15u;
+    s.count = (uint32_t)(popc64(nz_bits(b)) - popc64(nzg));
+    s.sum_e = nib_sum64(b) - nib_sum64(g) + 2u * s.count;
+    if (s.overflow) {  // a saturated 15+15 merge: the aggregate is off by one per such merge; sum the lines
+        uint32_t se = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const LineMerges m = line_merges(o[j], nw[j]);
+            se += m.e0 + m.e1;
+        }
+        s.sum_e = se;
+    }
+    s.score = 0u;
+    s.list = 0u;
+    return g;
+}
+
 // nz / equal-neighbour masks of a board, shared by is_done and action_mask
 struct BoardBits {
     uint64_t nz, z, eqh, eqv;
 };
 
-G2048_HD BoardBits board_bits(uint64_t b) {
+// the masks with the board's nz_bits already known
+G2048_HD BoardBits board_bits_nz(uint64_t b, uint64_t nz) {
     BoardBits r;
-    r.nz = nz_bits(b);
+    r.nz = nz;
     r.z = ~r.nz & kNibLsb;
     r.eqh = ~nz_bits(b ^ (b >> 4)) & r.nz & kHMask;
     r.eqv = ~nz_bits(b ^ (b >> 16)) & r.nz & kVMask;
     return r;
 }
+
+G2048_HD BoardBits board_bits(uint64_t b) { return board_bits_nz(b, nz_bits(b)); }
 
 G2048_HD bool bits_done(const BoardBits& r) { return r.z == 0 && (r.eqh | r.eqv) == 0; }
 
@@ -550,14 +626,22 @@ G2048_HD U4 philox4x32(U4 c, uint32_t k0, uint32_t k1) {
 // ---------------------------------------------------------------------------------------------------------
 // Game2048._spawn (src/game2048.py:108-118): uniform empty cell, then 2 (p=0.9) or 4.
 // ---------------------------------------------------------------------------------------------------------
-G2048_HD uint64_t spawn_pcg(uint64_t b, Pcg64& g) {
-    uint64_t z = ~nz_bits(b) & kNibLsb;
+// the spawn with the board's empty-cell bits z (bit 4i = cell i empty) already known; nzbit = the nz_bits bit of
+// the new tile (0 if the board was full)
+G2048_HD uint64_t spawn_pcg_z(uint64_t b, uint64_t z, Pcg64& g, uint64_t& nzbit) {
+    nzbit = 0;
     uint32_t n = (uint32_t)popc64(z);
     if (n == 0u) return b;
     uint32_t k = pcg_bounded(g, n);
     uint32_t cell = kth_empty_cell(z, k);
     uint64_t e = pcg_random(g) < 0.9 ? 1u : 2u;
+    nzbit = 1ull << (4u * cell);
     return b | (e << (4u * cell));
+}
+
+G2048_HD uint64_t spawn_pcg(uint64_t b, Pcg64& g) {
+    uint64_t nzbit;
+    return spawn_pcg_z(b, ~nz_bits(b) & kNibLsb, g, nzbit);
 }
 
 // logits_to_probs (src/MLP.py:139-156) + the action choice of select_action (src/reinforce_agent.py:178-190) for
@@ -595,14 +679,20 @@ G2048_HD uint32_t softmax_select(const float lg[4], uint32_t mw, bool has_mask, 
 }
 
 // Philox spawn: r.x picks the cell (Lemire, no rejection), r.y < 0.9 * 2**32 picks the 2
-G2048_HD uint64_t spawn_philox(uint64_t b, U4 r) {
-    uint64_t z = ~nz_bits(b) & kNibLsb;
+G2048_HD uint64_t spawn_philox_z(uint64_t b, uint64_t z, U4 r, uint64_t& nzbit) {
+    nzbit = 0;
     uint32_t n = (uint32_t)popc64(z);
     if (n == 0u) return b;
     uint32_t k = (uint32_t)(((uint64_t)r.x * n) >> 32);
     uint32_t cell = kth_empty_cell(z, k);
     uint64_t e = r.y < 3865470566u ? 1u : 2u;
+    nzbit = 1ull << (4u * cell);
     return b | (e << (4u * cell));
+}
+
+G2048_HD uint64_t spawn_philox(uint64_t b, U4 r) {
+    uint64_t nzbit;
+    return spawn_philox_z(b, ~nz_bits(b) & kNibLsb, r, nzbit);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -628,8 +718,11 @@ G2048_HD uint32_t reward_terms(const RewardCfg& c) {
            (c.bonus_mode == 2 ? kRwBonusLog2 : 0u);
 }
 
-G2048_HD double env_reward(const RewardCfg& c, const MoveSummary& s, uint64_t final_board, bool done, bool invalid,
-                           uint32_t& max_tile_e) {
+// final_nz = nz_bits(final board) (the empty-tile term); LOG2_ONLY: the caller guarantees reward_mode "log2" (the
+// summary's score is then not read, and need not have been computed).
+template <bool LOG2_ONLY = false>
+G2048_HD double env_reward_nz(const RewardCfg& c, const MoveSummary& s, uint64_t final_nz, bool done, bool invalid,
+                              uint32_t& max_tile_e) {
     uint32_t t = c.terms;
 #ifdef __HIP_DEVICE_COMPILE__
     // opaque per call: otherwise each bit test is hoisted out of the caller's loop as a 64-bit lane mask (it guards
@@ -637,10 +730,10 @@ G2048_HD double env_reward(const RewardCfg& c, const MoveSummary& s, uint64_t fi
     asm volatile("" : "+s"(t));
 #endif
     if ((t & kRwInvalidPenalty) && invalid) return c.invalid_action_penalty;
-    double r = (t & kRwLog2) ? (double)s.sum_e : (double)s.score;
+    double r = (LOG2_ONLY || (t & kRwLog2)) ? (double)s.sum_e : (double)s.score;
     r *= c.base_reward_scale;
     if (t & kRwEmpty) {
-        const int ne = 16 - popc64(nz_bits(final_board));
+        const int ne = 16 - popc64(final_nz);
         r += c.empty_tile_reward * (double)ne;
     }
     if (t & kRwMerge) r += c.merge_reward * (double)s.count;
@@ -655,6 +748,11 @@ G2048_HD double env_reward(const RewardCfg& c, const MoveSummary& s, uint64_t fi
     r += c.step_reward;
     if (done && (t & kRwEndgame)) r += c.endgame_penalty;
     return r;
+}
+
+G2048_HD double env_reward(const RewardCfg& c, const MoveSummary& s, uint64_t final_board, bool done, bool invalid,
+                           uint32_t& max_tile_e) {
+    return env_reward_nz<false>(c, s, nz_bits(final_board), done, invalid, max_tile_e);
 }
 
 // Flag bits of a step (the G2048_F_* of include/g2048.h; g2048.hip static_asserts they agree).

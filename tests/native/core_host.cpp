@@ -8,6 +8,7 @@ using namespace g2048;
 
 static uint16_t g_lut[65536];
 static uint8_t g_code[32768];
+static uint8_t g_mx[32768];
 static int g_lut_ready = 0;
 
 struct HostLut {
@@ -16,13 +17,17 @@ struct HostLut {
 struct HostCode {
     uint32_t operator()(uint32_t o) const { return (g_code[o >> 1] >> ((o & 1u) << 2)) & 15u; }
 };
+struct HostMx {
+    uint32_t operator()(uint32_t o) const { return (g_mx[o >> 1] >> ((o & 1u) << 2)) & 15u; }
+};
 
 static void ensure_lut() {
     if (g_lut_ready) return;
     for (uint32_t r = 0; r < 65536u; r++) {
         g_lut[r] = (uint16_t)line_move_left(r);
-        const uint32_t c = line_merge_code(r);
+        const uint32_t c = line_merge_code(r), f = line_max_merge_field(r);
         g_code[r >> 1] = (r & 1u) ? (uint8_t)(g_code[r >> 1] | (c << 4)) : (uint8_t)c;
+        g_mx[r >> 1] = (r & 1u) ? (uint8_t)(g_mx[r >> 1] | (f << 4)) : (uint8_t)f;
     }
     g_lut_ready = 1;
 }
@@ -77,6 +82,33 @@ int64_t ch_check_alu(int64_t n, uint64_t seed) {
             const uint64_t m1 = board_move_alu<true>(b, a, s1);
             const uint64_t m2 = board_move_alu<false>(b, a, s2);
             if (m0 != m1 || m0 != m2 || !same(s0, s1, true) || !same(s0, s2, false)) bad++;
+        }
+    };
+    for (uint32_t r = 0; r < 65536u; r++)
+        for (int slot = 0; slot < 4; slot++) {
+            const uint64_t other = rnd() & ~(0xFFFFull << (16 * slot));
+            check(other | ((uint64_t)r << (16 * slot)));
+        }
+    for (int64_t i = 0; i < n; i++) check(rnd());
+    return bad;
+}
+// board_move_lean (the step kernel's log2-reward path) against board_move_coded on every line value in every line
+// slot (other lines random) under all four actions, plus `n` random boards (boards with 15-nibbles included, so
+// the saturated-merge fallback runs): board, count, sum_e, max_e, overflow and the moved board's nz bits
+int64_t ch_check_lean(int64_t n, uint64_t seed) {
+    ensure_lut();
+    int64_t bad = 0;
+    uint64_t x = seed | 1ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    auto check = [&](uint64_t b) {
+        for (uint32_t a = 0; a < 4; a++) {
+            MoveSummary s0, s1;
+            uint64_t nzg = 0;
+            const uint64_t m0 = board_move_coded<false>(b, a, HostLut{}, HostCode{}, s0);
+            const uint64_t m1 = board_move_lean(b, a, HostLut{}, HostMx{}, s1, nzg);
+            if (m0 != m1 || s0.count != s1.count || s0.sum_e != s1.sum_e || s0.max_e != s1.max_e ||
+                (s0.overflow != 0) != (s1.overflow != 0) || nzg != nz_bits(m0))
+                bad++;
         }
     };
     for (uint32_t r = 0; r < 65536u; r++)

@@ -41,6 +41,8 @@ def ch():
     L.ch_board_move_alu.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [u32p] * 6
     L.ch_check_alu.restype = ctypes.c_int64
     L.ch_check_alu.argtypes = [ctypes.c_int64, ctypes.c_uint64]
+    L.ch_check_lean.restype = ctypes.c_int64
+    L.ch_check_lean.argtypes = [ctypes.c_int64, ctypes.c_uint64]
     L.ch_bits_mask.restype = ctypes.c_uint32
     L.ch_bits_mask.argtypes = [ctypes.c_uint64]
     L.ch_bits_done.argtypes = [ctypes.c_uint64]
@@ -108,6 +110,14 @@ def test_board_move_alu_equals_table_move(ch):
     """The table-free move (line_move_alu) against the two-table move: every 16-bit line in every line slot under
     all four actions (boards, merge summaries and merged lists equal), plus 200k random boards."""
     assert ch.ch_check_alu(200_000, 0x2048) == 0
+
+
+def test_board_move_lean_equals_table_move(ch):
+    """The step kernel's log2-reward move (board_move_lean: line table + max-merge field table, count and sum_e from
+    board aggregates, an exact per-line fallback on saturated 15+15 merges) against the two-table move: every
+    16-bit line in every line slot under all four actions, plus 200k random boards -- board, count, sum_e, max_e,
+    overflow and the moved board's nz bits."""
+    assert ch.ch_check_lean(200_000, 0x2049) == 0
 
 
 def test_mask_done_vs_oracle(ch):
