@@ -59,11 +59,7 @@ int fail(int code, const std::string& msg) {
 #ifndef G2048_LEAN
 #define G2048_LEAN 1
 #endif
-// G2048_WT: the step loop's 16-B per-lane stores (log2 / raw obs, PCG64 state) write through L2 (sc1 buffer stores)
-// instead of leaving dirty lines for the end-of-kernel L2 writeback (tools/kend.hip measures that writeback)
-#ifndef G2048_WT
-#define G2048_WT 0
-#endif
+
 
 
 #if G2048_DIAG
@@ -106,15 +102,6 @@ __device__ __forceinline__ void st(T* p, uint32_t idx, T v) {
 
 // observation stores are non-temporal (streaming): measured on MI355X, onehot obs (1,088 B/board) 260 -> 241 us at
 // 1M boards and 1050 -> 908 us at 4M; log2 obs unchanged (tools/ab_nt.sh, profiles/round1/ab_nt.log)
-typedef float f4v_t __attribute__((ext_vector_type(4)));
-constexpr int kRsrcFlags = 0x00020000;   // buffer resource dword3 (raw 32-bit dwords)
-constexpr int kAuxSc1 = 16;              // buffer op aux bit: sc1 (write through L2)
-
-// 16-B write-through store at byte offset off of a buffer resource
-__device__ __forceinline__ void st16_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, f4v_t v) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, kAuxSc1);
-}
-
 __device__ __forceinline__ void st_obs(float4* base, int q, float4 v) {
     typedef float f4v __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(base + q));
@@ -167,12 +154,7 @@ __device__ inline void write_obs_wave(float* __restrict__ obs, uint32_t w0, uint
         }
     } else if constexpr (OBS == G2048_OBS_LOG2 || OBS == G2048_OBS_RAW) {
         float4* dst = reinterpret_cast<float4*>(obs) + (size_t)w0 * 4;
-#if G2048_WT
-        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 4096, kRsrcFlags);
-        const auto st_row = [&](int q, float4 v) { st16_wt(ro, (uint32_t)q * 16u, f4v_t{v.x, v.y, v.z, v.w}); };
-#else
         const auto st_row = [&](int q, float4 v) { st_obs(dst, q, v); };
-#endif
         const auto row_obs = [&](uint64_t bb, uint32_t row) {
             const uint32_t r16 = (uint32_t)(bb >> (16u * row));
             float v[4];
@@ -414,17 +396,7 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     st(a.out.flags, i, (uint8_t)fl);
     st(L.board, i, m);
     st(L.state, i, nst);
-    if constexpr (RNG == G2048_RNG_PCG64) {
-#if G2048_WT
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            L.rng_state, 0, (int)(a.n < (1u << 27) ? a.n * 16u : 0x7FFFFFF0u), kRsrcFlags);
-        st16_wt(rs, i * 16u, f4v_t{__uint_as_float((uint32_t)x.g.s_lo), __uint_as_float((uint32_t)(x.g.s_lo >> 32)),
-                                  __uint_as_float((uint32_t)x.g.s_hi), __uint_as_float((uint32_t)(x.g.s_hi >> 32))});
-        st(L.rng_uint, i, x.g.uinteger);
-#else
-        store_pcg(L, i, x.g, false);
-#endif
-    }
+    if constexpr (RNG == G2048_RNG_PCG64) store_pcg(L, i, x.g, false);
     wobs = true;
     mbits = bits_mask(bits);
     return m;
