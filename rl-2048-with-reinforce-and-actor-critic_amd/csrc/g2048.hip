@@ -361,10 +361,22 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     const bool changed = m != b;
     if constexpr (RK == 1) {
         // nz bits of the final board: the moved board's, plus the spawned tile's
-        if (changed && !(G2048_DIAG && (a.diag & 4))) {
+        if constexpr (RNG == G2048_RNG_PCG64) {
+            if (!(G2048_DIAG && (a.diag & 4))) {
+                // formed for every lane (a wave holds changed and unchanged boards), kept where the board changed
+                Pcg64 g2 = x.g;
+                uint64_t nzbit;
+                const uint64_t m2 = spawn_pcg_lean(m, ~nzm & kNibLsb, g2, nzbit);
+                m = changed ? m2 : m;
+                nzm = changed ? nzm | nzbit : nzm;
+                x.g.s_hi = changed ? g2.s_hi : x.g.s_hi;
+                x.g.s_lo = changed ? g2.s_lo : x.g.s_lo;
+                x.g.uinteger = changed ? g2.uinteger : x.g.uinteger;
+                x.g.has_uint32 = changed ? g2.has_uint32 : x.g.has_uint32;
+            }
+        } else if (changed && !(G2048_DIAG && (a.diag & 4))) {
             uint64_t nzbit;
-            if constexpr (RNG == G2048_RNG_PCG64) m = spawn_pcg_z(m, ~nzm & kNibLsb, x.g, nzbit);
-            else m = spawn_philox_z(m, ~nzm & kNibLsb, philox_ctr(a.key, x.seed, sc, 0u), nzbit);
+            m = spawn_philox_z(m, ~nzm & kNibLsb, philox_ctr(a.key, x.seed, sc, 0u), nzbit);
             nzm |= nzbit;
         }
     } else {

@@ -639,6 +639,45 @@ G2048_HD uint64_t spawn_pcg_z(uint64_t b, uint64_t z, Pcg64& g, uint64_t& nzbit)
     return b | (e << (4u * cell));
 }
 
+G2048_HD uint64_t pcg_output(uint64_t s_hi, uint64_t s_lo) {
+    const uint64_t x = s_hi ^ s_lo;
+    const uint32_t rot = (uint32_t)(s_hi >> 58);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+// random() < 0.9 on numpy's (next_uint64 >> 11) * 2**-53, as an integer compare: 0.9 (the double) * 2**53 is the
+// integer 8106479329266893 (0.9's 52-bit mantissa shifted by 52), and k * 2**-53 < 0.9 <=> k < that integer.
+constexpr uint64_t kRandom09 = 8106479329266893ull;
+
+// _spawn (src/game2048.py:108-118) on the numpy PCG64 stream without branches on the common path (the step kernel's
+// lean path): the one- and two-step successor states are both formed, and next_uint32's buffer decides which one
+// random() draws from -- the same draws as spawn_pcg_z.  A Lemire draw that may be rejected (its low word < n:
+// probability < 2^-28) takes the exact path, spawn_pcg_z on the original state.  Requires z != 0 (the board changed,
+// so the move emptied at least one cell).
+G2048_HD uint64_t spawn_pcg_lean(uint64_t b, uint64_t z, Pcg64& g, uint64_t& nzbit) {
+    const uint32_t n = (uint32_t)popc64(z);
+    Pcg64 A = g;
+    pcg_step(A);
+    Pcg64 B = A;
+    pcg_step(B);
+    const uint64_t oA = pcg_output(A.s_hi, A.s_lo);
+    const bool draw = n > 1u;                        // integers(n) draws nothing for n == 1
+    const bool fresh = draw && !g.has_uint32;        // next_uint32 takes a new 64-bit output (state -> A)
+    const uint32_t u = g.has_uint32 ? g.uinteger : (uint32_t)oA;
+    const uint64_t m = (uint64_t)u * n;
+    if (draw && (uint32_t)m < n) return spawn_pcg_z(b, z, g, nzbit);   // possible Lemire rejection: exact path
+    const uint32_t k = draw ? (uint32_t)(m >> 32) : 0u;
+    const uint64_t r_hi = fresh ? B.s_hi : A.s_hi, r_lo = fresh ? B.s_lo : A.s_lo;
+    const uint64_t e = (pcg_output(r_hi, r_lo) >> 11) < kRandom09 ? 1u : 2u;
+    const uint32_t cell = kth_empty_cell(z, k);
+    g.s_hi = r_hi;
+    g.s_lo = r_lo;
+    g.uinteger = fresh ? (uint32_t)(oA >> 32) : g.uinteger;
+    g.has_uint32 = draw ? (g.has_uint32 ^ 1u) : g.has_uint32;
+    nzbit = 1ull << (4u * cell);
+    return b | (e << (4u * cell));
+}
+
 G2048_HD uint64_t spawn_pcg(uint64_t b, Pcg64& g) {
     uint64_t nzbit;
     return spawn_pcg_z(b, ~nz_bits(b) & kNibLsb, g, nzbit);

@@ -119,6 +119,32 @@ int64_t ch_check_lean(int64_t n, uint64_t seed) {
     for (int64_t i = 0; i < n; i++) check(rnd());
     return bad;
 }
+// spawn_pcg_lean (branch-free spawn of the lean step) against spawn_pcg_z: `n` random (board, PCG64 state, buffer)
+// triples, every empty-cell count, both buffer states, and buffered values 0 / small (the Lemire-rejection fallback)
+int64_t ch_check_spawn_lean(int64_t n, uint64_t seed) {
+    int64_t bad = 0;
+    uint64_t x = seed | 1ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (int64_t i = 0; i < n; i++) {
+        uint64_t b = rnd();
+        const uint64_t keep = rnd() | rnd();   // ~1/4 of the cells emptied
+        b &= 0x1111111111111111ull * 15u & ((keep & 0x1111111111111111ull) * 15u);
+        if (b == 0) b = 1;
+        const uint64_t z = ~nz_bits(b) & kNibLsb;
+        if (z == 0) continue;
+        Pcg64 g;
+        g.s_lo = rnd(); g.s_hi = rnd(); g.i_lo = rnd() | 1u; g.i_hi = rnd();
+        g.has_uint32 = (uint32_t)(i & 1);
+        g.uinteger = (i % 7 == 3) ? 0u : (i % 7 == 5) ? (uint32_t)(i & 3) : (uint32_t)rnd();
+        Pcg64 g0 = g, g1 = g;
+        uint64_t nb0, nb1;
+        const uint64_t m0 = spawn_pcg_z(b, z, g0, nb0), m1 = spawn_pcg_lean(b, z, g1, nb1);
+        if (m0 != m1 || nb0 != nb1 || g0.s_lo != g1.s_lo || g0.s_hi != g1.s_hi || g0.has_uint32 != g1.has_uint32 ||
+            (g0.has_uint32 && g0.uinteger != g1.uinteger))
+            bad++;
+    }
+    return bad;
+}
 uint32_t ch_bits_mask(uint64_t b) { return bits_mask(board_bits(b)); }
 int ch_bits_done(uint64_t b) { return bits_done(board_bits(b)) ? 1 : 0; }
 uint32_t ch_action_mask(uint64_t b) { return action_mask(b); }

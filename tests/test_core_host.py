@@ -43,6 +43,8 @@ def ch():
     L.ch_check_alu.argtypes = [ctypes.c_int64, ctypes.c_uint64]
     L.ch_check_lean.restype = ctypes.c_int64
     L.ch_check_lean.argtypes = [ctypes.c_int64, ctypes.c_uint64]
+    L.ch_check_spawn_lean.restype = ctypes.c_int64
+    L.ch_check_spawn_lean.argtypes = [ctypes.c_int64, ctypes.c_uint64]
     L.ch_bits_mask.restype = ctypes.c_uint32
     L.ch_bits_mask.argtypes = [ctypes.c_uint64]
     L.ch_bits_done.argtypes = [ctypes.c_uint64]
@@ -118,6 +120,13 @@ def test_board_move_lean_equals_table_move(ch):
     16-bit line in every line slot under all four actions, plus 200k random boards -- board, count, sum_e, max_e,
     overflow and the moved board's nz bits."""
     assert ch.ch_check_lean(200_000, 0x2049) == 0
+
+
+def test_spawn_pcg_lean_equals_spawn(ch):
+    """The lean step's branch-free PCG64 spawn (one- and two-step successors formed, next_uint32's buffer picks
+    random()'s state; integer compare for random() < 0.9; exact fallback on a possible Lemire rejection) against
+    spawn_pcg_z on 2M random boards and states, buffered values 0 and tiny included (the fallback path)."""
+    assert ch.ch_check_spawn_lean(2_000_000, 0x2050) == 0
 
 
 def test_mask_done_vs_oracle(ch):
