@@ -159,7 +159,9 @@ def test_configs4_shard_philox_onehot_1m_lanes():
 
     n = 1 << 20
     cfg = dict(obs_mode="onehot", reward_mode="log2", base_reward_scale=0.5, bonus_mode="log2", max_steps=16)
-    env = VecGame2048Env(n, Game2048EnvConfig(**cfg), device=DEV, rng="philox", auto_reset=True, reset_stride=n)
+    # no score output (the throughput configuration): the log2-reward lean step kernel with Philox spawns
+    env = VecGame2048Env(n, Game2048EnvConfig(**cfg), device=DEV, rng="philox", auto_reset=True, reset_stride=n,
+                         track_score=False)
     env.reset(seed=123_456)
     e = env.boards_exponents().reshape(n, 16)
     nz = e[e > 0]

@@ -152,14 +152,17 @@ ENV_CFGS = [
 ]
 
 
+@pytest.mark.parametrize("track_score", [True, False])
 @pytest.mark.parametrize("rng_kind", ["pcg64"])
 @pytest.mark.parametrize("cfg", ENV_CFGS)
-def test_env_step_vs_oracle(cfg, rng_kind):
-    """Game2048Env.step semantics per lane (reward, terminated/truncated, invalid, obs, mask, max_tile_seen)."""
+def test_env_step_vs_oracle(cfg, rng_kind, track_score):
+    """Game2048Env.step semantics per lane (reward, terminated/truncated, invalid, obs, mask, max_tile_seen).
+    track_score=False drops the score output, which sends the log2-reward configs to the lean step kernel (RK 1:
+    max-merge field table, aggregate count / sum_e, branch-free spawn) and the others to the no-output general one."""
     from rl2048_amd import Game2048EnvConfig, VecGame2048Env
 
     n, T = 300, 150
-    env = VecGame2048Env(n, Game2048EnvConfig(**cfg), device=DEV, rng=rng_kind)
+    env = VecGame2048Env(n, Game2048EnvConfig(**cfg), device=DEV, rng=rng_kind, track_score=track_score)
     seeds = [7000 + 13 * i for i in range(n)]
     obs, _ = env.reset(seed=seeds)
     ref = [O.Env(**cfg) for _ in range(n)]
