@@ -144,7 +144,9 @@ int g2048_reset(const g2048_lanes* lanes, const uint64_t* seeds, const uint8_t* 
  * Game2048.step (src/game2048.py:40-70) and the reward of _compute_reward (src/env.py:197-261).
  * actions: [n] uint8.  auto_reset != 0: a lane that terminates or truncates is reset in the same call with
  * seed += reset_stride (flag G2048_F_RESET; obs/mask then describe the new episode).  auto_reset == 0: the
- * lane is marked inactive and later calls leave it untouched (G2048_F_INACTIVE). */
+ * lane is marked inactive and later calls leave it untouched (G2048_F_INACTIVE).  Outputs are the same for every
+ * combination of `out` fields; a log2-reward config that asks for none of merged / prev_board / reward64 /
+ * score_add runs a leaner kernel (no merge decode or score: the reward reads only sum and max of the merges). */
 int g2048_step(const g2048_lanes* lanes, const uint8_t* actions, const g2048_env_cfg* cfg,
                const g2048_step_out* out, int rng_mode, uint64_t philox_key, int auto_reset,
                uint64_t reset_stride, int64_t n, void* stream);
