@@ -145,6 +145,26 @@ int64_t ch_check_spawn_lean(int64_t n, uint64_t seed) {
     }
     return bad;
 }
+// transpose / reverse_rows (byte-permute forms) against their plain shift-and-mask definitions on n random boards
+int64_t ch_check_frames(int64_t n, uint64_t seed) {
+    int64_t bad = 0;
+    uint64_t x = seed | 1ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (int64_t i = 0; i < n; i++) {
+        const uint64_t b = rnd();
+        uint64_t t = b, r = 0;
+        for (int rr = 0; rr < 4; rr++)
+            for (int c = 0; c < 4; c++) {
+                const uint64_t v = (b >> (4 * (4 * rr + c))) & 15u;
+                r |= v << (4 * (4 * rr + (3 - c)));           // reverse_rows: (r,c) -> (r,3-c)
+            }
+        uint64_t tt = 0;
+        for (int rr = 0; rr < 4; rr++)
+            for (int c = 0; c < 4; c++) tt |= ((t >> (4 * (4 * rr + c))) & 15u) << (4 * (4 * c + rr));
+        if (transpose(b) != tt || reverse_rows(b) != r) bad++;
+    }
+    return bad;
+}
 uint32_t ch_bits_mask(uint64_t b) { return bits_mask(board_bits(b)); }
 int ch_bits_done(uint64_t b) { return bits_done(board_bits(b)) ? 1 : 0; }
 uint32_t ch_action_mask(uint64_t b) { return action_mask(b); }

@@ -45,6 +45,8 @@ def ch():
     L.ch_check_lean.argtypes = [ctypes.c_int64, ctypes.c_uint64]
     L.ch_check_spawn_lean.restype = ctypes.c_int64
     L.ch_check_spawn_lean.argtypes = [ctypes.c_int64, ctypes.c_uint64]
+    L.ch_check_frames.restype = ctypes.c_int64
+    L.ch_check_frames.argtypes = [ctypes.c_int64, ctypes.c_uint64]
     L.ch_bits_mask.restype = ctypes.c_uint32
     L.ch_bits_mask.argtypes = [ctypes.c_uint64]
     L.ch_bits_done.argtypes = [ctypes.c_uint64]
@@ -127,6 +129,11 @@ def test_spawn_pcg_lean_equals_spawn(ch):
     random()'s state; integer compare for random() < 0.9; exact fallback on a possible Lemire rejection) against
     spawn_pcg_z on 2M random boards and states, buffered values 0 and tiny included (the fallback path)."""
     assert ch.ch_check_spawn_lean(2_000_000, 0x2050) == 0
+
+
+def test_frame_transforms_match_definitions(ch):
+    """transpose / reverse_rows (delta swap + byte permutes) against the cell-by-cell definitions, 2M boards."""
+    assert ch.ch_check_frames(2_000_000, 0x2051) == 0
 
 
 def test_mask_done_vs_oracle(ch):
