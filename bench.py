@@ -82,7 +82,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"])
     ap.add_argument("--no-policy", action="store_true")
+    ap.add_argument("--no-refconfig", action="store_true",
+                    help="skip the reference runner-config training iterations (runner.py:10-47)")
     ap.add_argument("--no-auto-reset", action="store_true", help="diagnostic: finished lanes go inactive")
+    ap.add_argument("--chip-warmup-seconds", type=float, default=0.5,
+                    help="untimed step launches on a separate env of the same shape before the headline leg")
     ap.add_argument("--trace-steps", type=int, default=0,
                     help="diagnostic: print per-launch kernel us and reset fraction for the first N steps, then exit")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -137,13 +141,18 @@ def pmc_traffic(args) -> dict | None:
     base = os.path.join(ROOT, "gpurun_out", "pmc") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None
     if base:
         os.makedirs(base, exist_ok=True)
+    # the child is a single-process run on this rank's GPU even under torchrun: no rendezvous variables
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT") and not k.startswith("TORCHELASTIC_")}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         out = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir=base)
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "pmc", "--", sys.executable,
                os.path.abspath(__file__), "--pmc-child", "--steps", "10", "--warmup", "3", "--boards",
                str(args.boards), "--rng", args.rng, "--obs", args.obs]
         try:
-            subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           env=env)
         except Exception:  # noqa: BLE001 -- traffic is optional; report null on any profiler failure
             return None
         rows = []
@@ -310,6 +319,50 @@ def train_iteration_rate(torch, device, episodes: int = 65536, repeats: int = 2,
     return out
 
 
+# The configuration runner.py documents in its header (/root/reference/runner.py:10-47): one-hot obs, a
+# 16x17 -> 256 -> 128 -> 64 -> 4 ReLU MLP, actor-critic (MSE), Adam, batch baseline, no max_steps.
+REFCONF_ENV = dict(obs_mode="onehot", obs_log2_scale=1.0, reward_mode="log2", base_reward_scale=1.0, bonus_mode="off",
+                   bonus_scale=1.0, step_reward=0.0, endgame_penalty=0.0, use_action_mask=True,
+                   invalid_action_penalty=-1.0, max_steps=None, empty_tile_reward=0.05, merge_reward=0.0)
+REFCONF_MLP = dict(hidden_sizes=[256, 128, 64], activation="ReLU", init_distribution="HeNormal", last_init_normal=True)
+REFCONF_AGENT = dict(gamma=0.99, learning_rate=0.01, baseline_mode="batch", model_seed=0, reward_rank_weights=None,
+                     optimizer="adam", adam_beta1=0.9, adam_beta2=0.999, augmentation=False, use_critic=True,
+                     critic_learning_rate=0.0005, critic_loss_type="mse", huber_delta=1.0)
+
+
+def train_iteration_refconfig(torch, device, episodes: int, repeats: int = 1) -> dict:
+    """One training iteration (rollout_batch of `episodes` episodes + update_from_batch) of the reference runner's
+    documented config (REFCONF_*), timed per phase; the last of `repeats` timed iterations after one warm-up."""
+    import numpy as np
+
+    from rl2048_amd import Game2048EnvConfig
+    from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
+    from rl2048_amd.mlp import MLPConfig
+
+    agent = ReinforceAgent(Game2048EnvConfig(**REFCONF_ENV), MLPConfig(**REFCONF_MLP),
+                           ReinforceAgentConfig(**REFCONF_AGENT), device=device)
+    out = {}
+    for rep in range(repeats + 1):
+        es = np.arange(3 + rep * episodes, 3 + (rep + 1) * episodes, dtype=np.int64)
+        ps = es + 7 * episodes
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        batch = agent.rollout_batch(es, ps)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        agent.update_from_batch(batch)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        samples = int(batch.lengths.sum())
+        out = {"episodes": episodes, "env_steps": samples, "longest_episode": batch.T, "rollout_s": t1 - t0,
+               "update_s": t2 - t1, "iteration_s": t2 - t0, "env_steps_per_s": samples / (t2 - t0),
+               "paths": agent.last_paths(),
+               "model": "actor-critic (MSE), one-hot obs, MLP 272-256-128-64-4 ReLU fp32, Adam, batch baseline, "
+                        "max_steps None (runner.py:10-47)"}
+        del batch
+    return out
+
+
 def train_iteration_dp(torch, device, episodes_per_rank: int, rank: int, world: int) -> dict:
     """configs[3]'s training iteration, weak-scaled: every rank plays `episodes_per_rank` episodes of the global
     batch (global episode g = rank * E + i; env seed 1000 + g, policy seed 2**40 + g, so N ranks play a partition
@@ -384,12 +437,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         args.gpus = world
-    # profiler passes and the CPU baseline run before this process touches the GPU
+    # The profiler passes and the CPU baseline run on rank 0 before this process touches the GPU, at every N: under
+    # torchrun the other ranks meanwhile wait in init_process_group (well inside its timeout), so the CPU loop is
+    # timed on the same box's host cores in the same run and the roofline carries PMC traffic at N > 1 too.
     traffic = None
-    if rank == 0 and world == 1 and not args.pmc_child and args.traffic == "auto":
+    if rank == 0 and not args.pmc_child and args.traffic == "auto":
         traffic = pmc_traffic(args)
     cpu = None
-    if rank == 0 and world == 1 and not args.pmc_child and not args.no_cpu_baseline:
+    if rank == 0 and not args.pmc_child and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.cpu_baseline_seconds)
 
     import torch
@@ -429,16 +484,36 @@ def main():
             # configs[2]: 1,048,576 parallel boards, actor-critic (one warm-up, one timed iteration)
             policy["train_iteration_configs2"] = train_iteration_rate(torch, device, episodes=1 << 20, repeats=1,
                                                                       critic=True)
+            if not args.no_refconfig:
+                policy["train_iteration_reference_runner_config"] = {
+                    "65536": train_iteration_refconfig(torch, device, 1 << 16),
+                    "1048576": train_iteration_refconfig(torch, device, 1 << 20, repeats=0)}
         except Exception as e:  # noqa: BLE001 -- an extra, never the headline
             policy = {"error": repr(e)}
     torch.cuda.empty_cache()
     if world > 1:
         dist.barrier()
-    env = make_env(torch, args, B, rank * B, device)
     K, W = args.steps, args.warmup
     g = torch.Generator(device=device)
     g.manual_seed(1 + rank)
     actions = torch.randint(0, 4, (K + W, B), dtype=torch.uint8, device=device, generator=g)
+    # Chip warm-up, explicit and independent of the extra legs above: untimed step launches for
+    # --chip-warmup-seconds on a separate env of the same shape (on a cold chip the first ~20 launches of the step
+    # kernel run 10-30 % slower, profiles/round3/step_cold_trace.log); the headline env below starts from the
+    # synthetic random-state boards untouched.
+    warm = {"launches": 0, "seconds": 0.0}
+    if args.chip_warmup_seconds > 0 and not args.trace_steps:
+        wenv = make_env(torch, args, B, rank * B, device)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < args.chip_warmup_seconds:
+            for _ in range(32):
+                wenv.step_into(actions[warm["launches"] % (K + W)])
+                warm["launches"] += 1
+            torch.cuda.synchronize()
+        warm["seconds"] = time.perf_counter() - t0
+        del wenv
+    env = make_env(torch, args, B, rank * B, device)
     if args.trace_steps:
         from rl2048_amd import _lib as L
 
@@ -500,7 +575,9 @@ def main():
                                f"slide/merge + {args.rng} spawn + fp64 reward + done/trunc + auto-reset + action mask (packed) + "
                                f"{args.obs} obs, uniform random actions incl. invalid",
                    "boards_per_gpu": B, "global_boards": B * world, "rng": args.rng, "obs": args.obs,
-                   "parallelism": f"dp{world} (board shards, no data-path collective)"},
+                   "parallelism": f"dp{world} (board shards, no data-path collective)",
+                   "chip_warmup": {"launches": warm["launches"], "seconds": round(warm["seconds"], 3),
+                                   "env": "separate env of the same shape (untimed)"}},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic["bytes"] if traffic else None,

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 12
+#define G2048_ABI_VERSION 13
 
 /* status codes */
 #define G2048_OK 0
@@ -292,6 +292,38 @@ int g2048_rollout(const float* packed, int h1, int h2, int activation, const g20
                   const uint64_t* pol_inc, const uint64_t* pol_buf, uint32_t* queue, int64_t n, int64_t cap,
                   uint64_t* boards, uint8_t* actions, double* rewards, uint8_t* flags, float* probs, int32_t* lengths,
                   double* totals, uint8_t* max_tile, uint64_t* final_board, void* stream);
+
+/* ---- nets of any depth and one-hot first layers (g2048_deep.hip; ABI 13) ----------------------------------------
+ * forward_logits (src/MLP.py:159-196) for 1..G2048_DEEP_MAX_HIDDEN hidden layers of 1..256 units, ReLU / Sigmoid,
+ * on log2 / raw obs (16 features) or one-hot obs (272: the first layer is a gather of W1's rows 17 c + e_c, the
+ * one-hot encoding of src/env.py:143-150 read off the bitboard -- no obs buffer).  Packed layout: g2048_deep.hip. */
+#define G2048_DEEP_MAX_HIDDEN 4
+/* floats of the packed net, or -1 if the shape is not covered (hidden: n_hidden sizes) */
+int64_t g2048_deep_packed_size(int obs_mode, int n_hidden, const int32_t* hidden);
+/* W[l] / b[l] (l = 0..n_hidden): device pointers of the reference-layout fp32 parameters, W_l [in, out] row-major
+ * (params["W"], params["b"] of src/MLP.py:45-94); out_dim 4 (actor) or 1 (critic value head, packed as output 0). */
+int g2048_deep_pack(const float* const* W, const float* const* b, int obs_mode, int n_hidden, const int32_t* hidden,
+                    int out_dim, float* packed, int64_t packed_len, void* stream);
+/* g2048_policy's contract for a packed deep net: forward from boards[lane_index ? lane_index[j] : j] (j < n), then
+ * (actions != NULL) logits_to_probs + select_action's choice (src/reinforce_agent.py:126-192) on the lane's stream;
+ * actions == NULL: forward only (logits_out, e.g. a critic's V(s) in component 0). */
+int g2048_deep_policy(const float* packed, int n_hidden, const int32_t* hidden, int activation, const uint64_t* boards,
+                      const uint32_t* lane_state, const int32_t* lane_index, int obs_mode, float obs_scale, int use_mask,
+                      int greedy, int rng_mode, uint64_t* rng_state, const uint64_t* rng_inc, const uint64_t* rng_buf,
+                      uint64_t philox_key, const uint64_t* lane_seed, float* probs_out, float* logits_out,
+                      uint8_t* actions, int64_t n, void* stream);
+/* The update's one-hot first layer: out[s * ld + j] = act(b1[j] + sum_c W1[17 c + e_c(s), j]) for s < m, j < h1
+ * (W1 the [272, h1] parameter) -- the kept layer-1 activations of _backpropagation (src/reinforce_agent.py:639-678)
+ * without the [m, 272] one-hot obs. */
+int g2048_onehot_layer1(const float* W1, const float* b1, int h1, int activation, const uint64_t* boards, int64_t m,
+                        int64_t ld, float* out, void* stream);
+/* floats of one g2048_onehot_dw1 partial slab: 272 h1 (dW1) + h1 (db1) */
+int64_t g2048_onehot_dw1_slab(int h1);
+/* dW1 = X^T D1 and db1 = sum D1 of a one-hot first layer (X one-hot, D1 = d1[s * ld + j] the layer-1 deltas): slab
+ * p of partials (nparts = ceil(m / per)) holds the sums over samples [p per, (p + 1) per) -- a 16-row scatter-add
+ * per sample in sample order; fold them with g2048_fold_partials. */
+int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m, int64_t ld, int64_t per,
+                     float* partials, int64_t nparts, void* stream);
 
 #ifdef __cplusplus
 }

@@ -18,9 +18,11 @@ REPO_ROOT = os.path.dirname(PKG_DIR)
 SHIPPED_LIB = os.path.join(PKG_DIR, "libg2048.so")
 LIB_PATH = SHIPPED_LIB
 SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
-SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip"), os.path.join(PKG_DIR, "csrc", "g2048_dw2.hip")]
+SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip"), os.path.join(PKG_DIR, "csrc", "g2048_dw2.hip"),
+           os.path.join(PKG_DIR, "csrc", "g2048_deep.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 12
+ABI_VERSION = 13
+DEEP_MAX_HIDDEN = 4
 
 # include/g2048.h constants
 OBS_NONE, OBS_RAW, OBS_LOG2, OBS_ONEHOT = -1, 0, 1, 2
@@ -40,11 +42,29 @@ BUILD_DIR = os.path.join(PKG_DIR, "build")
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC"]
 
 
+_COMPILER_ID: str | None = None
+
+
+def _compiler_id() -> str:
+    """The resolved hipcc and its version text: part of every object's cache key, so a ROCm / hipcc change
+    rebuilds instead of linking objects from another compiler."""
+    global _COMPILER_ID
+    if _COMPILER_ID is None:
+        import shutil
+
+        exe = shutil.which("hipcc") or "hipcc"
+        r = subprocess.run([exe, "--version"], capture_output=True, text=True)
+        _COMPILER_ID = os.path.realpath(exe) + "\n" + r.stdout + r.stderr
+    return _COMPILER_ID
+
+
 def _object_for(src: str, flags: list[str]) -> str:
-    """build/<tu>-<hash>.o: keyed by the TU, every header it may include and the flags (incremental builds)."""
+    """build/<tu>-<hash>.o: keyed by the TU, every header it may include, the flags and the compiler
+    (incremental builds)."""
     import hashlib
 
     h = hashlib.sha256(" ".join(flags).encode())
+    h.update(_compiler_id().encode())
     hdrs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc")))
     for f in [src] + hdrs + [os.path.join(INCLUDE, "g2048.h")]:
         with open(f, "rb") as fh:
@@ -145,10 +165,20 @@ def _declare(L):
     L.g2048_dw2.argtypes = [vp, vp, i32, i32, i64, i64, i64, i64, vp, i64, vp]
     L.g2048_fold_partials.argtypes = [vp, i64, i64, vp, vp]
     L.g2048_dw2_factored.argtypes = [vp, vp, vp, i32, i32, i64, i64, i64, i64, vp, i64, vp]
+    L.g2048_deep_packed_size.argtypes = [i32, i32, vp]
+    L.g2048_deep_packed_size.restype = i64
+    L.g2048_deep_pack.argtypes = [vp, vp, i32, i32, vp, i32, vp, i64, vp]
+    L.g2048_deep_policy.argtypes = [vp, i32, vp, i32, vp, vp, vp, i32, f, i32, i32, i32, vp, vp, vp, u64, vp, vp, vp,
+                                    vp, i64, vp]
+    L.g2048_onehot_layer1.argtypes = [vp, vp, i32, i32, vp, i64, i64, vp, vp]
+    L.g2048_onehot_dw1_slab.argtypes = [i32]
+    L.g2048_onehot_dw1_slab.restype = i64
+    L.g2048_onehot_dw1.argtypes = [vp, vp, i32, i64, i64, i64, vp, i64, vp]
     for name in ("g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step", "g2048_obs", "g2048_move",
                  "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy",
                  "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad",
-                 "g2048_dw2", "g2048_fold_partials", "g2048_dw2_factored"):
+                 "g2048_dw2", "g2048_fold_partials", "g2048_dw2_factored", "g2048_deep_pack", "g2048_deep_policy",
+                 "g2048_onehot_layer1", "g2048_onehot_dw1"):
         getattr(L, name).restype = ctypes.c_int
 
 
@@ -157,7 +187,8 @@ EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g204
                     "g2048_policy_packed_size", "g2048_policy_pack", "g2048_policy", "g2048_rollout",
                     "g2048_grad_packed_size", "g2048_grad_partial_size", "g2048_grad_pack", "g2048_actor_grad_waves",
                     "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2", "g2048_fold_partials",
-                    "g2048_dw2_factored")
+                    "g2048_dw2_factored", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
+                    "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1")
 
 
 def lib():

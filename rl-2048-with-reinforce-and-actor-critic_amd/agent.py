@@ -183,6 +183,14 @@ class _Steps:
             x, m = self.agent._symmetry_features(x, m, k)
         return x, m
 
+    def boards_at(self, sel: torch.Tensor, k: int = 0, nxt: bool = False) -> torch.Tensor:
+        """The bitboards of the valid steps `sel` (or of their successors, as features(nxt=True)), symmetry k."""
+        flat = self.vidx[sel]
+        if nxt:
+            flat = torch.where(self.has_next[sel], flat + self.n, flat)
+        b = self.boards.reshape(-1)[flat].contiguous()
+        return self.agent._symmetry_boards(b, k) if k else b
+
     def actions_k(self, sel: torch.Tensor, k: int) -> torch.Tensor:
         a = self.actions[sel]
         if k == 0:
@@ -251,6 +259,7 @@ class ReinforceAgent:
         self._vec_cache: dict = {}
         self._lib = L.lib()
         self.last_stats: dict = {}
+        self._paths: dict[str, str] = {}   # which implementation ran each phase last (last_paths)
 
     # ============================================================================================ model I/O
     def load_model(self, file_path: str = "params.npz") -> None:
@@ -329,6 +338,11 @@ class ReinforceAgent:
         self._logger.info(f"Checkpoint loaded from {file_path}")
         return {k[len("extra_"):]: v for k, v in st.items() if k.startswith("extra_")}
 
+    def last_paths(self) -> dict[str, str]:
+        """Which implementation ran the last rollout / actor gradient / critic gradient (bench and test
+        reporting)."""
+        return dict(self._paths)
+
     # ============================================================================================ helpers
     @property
     def _stream(self) -> int:
@@ -402,6 +416,105 @@ class ReinforceAgent:
         if any(t.dtype != torch.float32 or t.device != self.device for t in Ws + bs):
             return None
         return h1, h2, act
+
+    def _deep_spec(self, params=None, out_dim: int = 4):
+        """(obs code, hidden sizes, activation code, int32 ctypes array of the sizes) when the net is covered by the
+        any-depth kernels of g2048_deep.hip (1..4 hidden layers of 1..256 units, ReLU / Sigmoid, fp32 on this
+        device, log2 / raw / one-hot obs), else None."""
+        params = self.params if params is None else params
+        Ws, bs = params["W"], params["b"]
+        nh = len(Ws) - 1
+        act = {"ReLU": L.ACT_RELU, "Sigmoid": L.ACT_SIGMOID}.get(self.mlp_config.activation)
+        if act is None or not (1 <= nh <= L.DEEP_MAX_HIDDEN) or len(bs) != len(Ws):
+            return None
+        hidden = tuple(int(W.shape[1]) for W in Ws[:-1])
+        if tuple(Ws[0].shape)[0] != self.input_dim or tuple(Ws[-1].shape)[1] != out_dim or \
+                not all(1 <= h <= 256 for h in hidden):
+            return None
+        if any(tuple(Ws[l].shape)[0] != hidden[l - 1] for l in range(1, nh + 1)):
+            return None
+        if any(t.dtype != torch.float32 or t.device != self.device for t in Ws + bs):
+            return None
+        return (_OBS_CODE[self.env_config.obs_mode], hidden, act, (ctypes.c_int32 * nh)(*hidden))
+
+    def _pack_deep(self, params, dspec, slot: str, out_dim: int) -> torch.Tensor:
+        """g2048_deep_pack of a net, cached per slot until a parameter tensor changes."""
+        Ws, bs = params["W"], params["b"]
+        key = (self._params_version,) + tuple((t.data_ptr(), t._version) for t in Ws + bs)
+        entry = self._pack_cache.setdefault(slot + "/deep", [None, None, None])
+        if key != entry[1]:
+            obs_code, hidden, _, harr = dspec
+            size = int(self._lib.g2048_deep_packed_size(obs_code, len(hidden), harr))
+            if entry[0] is None or entry[0].numel() < size:
+                entry[0] = torch.empty(size, dtype=torch.float32, device=self.device)
+            ws = [t.contiguous() for t in Ws]
+            bb = [t.contiguous() for t in bs]
+            wp = (ctypes.c_void_p * len(ws))(*[t.data_ptr() for t in ws])
+            bp = (ctypes.c_void_p * len(bb))(*[t.data_ptr() for t in bb])
+            L.check(self._lib.g2048_deep_pack(wp, bp, obs_code, len(hidden), harr, out_dim, L.ptr(entry[0]), size,
+                                              self._stream))
+            entry[1] = key
+            entry[2] = (ws, bb)      # keep the contiguous copies alive until the (stream-ordered) pack has run
+        return entry[0]
+
+    def _deep_forward(self, params, dspec, slot: str, boards: torch.Tensor, out_dim: int) -> torch.Tensor:
+        """forward_logits of the boards through g2048_deep_policy (forward only): [m, 4] (a value head in column 0)."""
+        m = boards.numel()
+        out = torch.empty(m, 4, dtype=torch.float32, device=self.device)
+        if m == 0:
+            return out
+        packed = self._pack_deep(params, dspec, slot, out_dim)
+        obs_code, hidden, act, harr = dspec
+        L.check(self._lib.g2048_deep_policy(L.ptr(packed), len(hidden), harr, act, L.ptr(boards.contiguous()), None,
+                                            None, obs_code, float(self.env_config.obs_log2_scale), 0, 1, L.RNG_PCG64,
+                                            None, None, None, 0, None, None, L.ptr(out), None, m, self._stream))
+        return out
+
+    def _onehot_first_layer(self, steps: "_Steps") -> bool:
+        """The batched update gathers the one-hot first layer from the bitboards (g2048_onehot_layer1 /
+        g2048_onehot_dw1) instead of materialising [m, 272] one-hot obs for 272-wide GEMMs."""
+        return steps.boards is not None and self.env_config.obs_mode == "onehot"
+
+    def _mask_from_boards(self, boards: torch.Tensor) -> torch.Tensor:
+        m = boards.numel()
+        mk = torch.empty(m, 4, dtype=torch.int8, device=self.device)
+        L.check(self._lib.g2048_obs(L.ptr(boards), L.OBS_NONE, 1.0, None, L.ptr(mk), m, self._stream))
+        return mk
+
+    def _forward_kept_steps(self, params, steps: "_Steps", sel: torch.Tensor, k: int, want_mask: bool = False):
+        """mlp_forward_kept of the valid steps `sel` (symmetry k): (output, kept activations, boards or None, action
+        mask or None).  On one-hot obs the first layer is g2048_onehot_layer1's gather from the boards (returned for
+        the dW1 scatter)."""
+        act = self.mlp_config.activation
+        if self._onehot_first_layer(steps):
+            b = steps.boards_at(sel, k)
+            W1, b1 = params["W"][0].contiguous(), params["b"][0].contiguous()
+            h1 = int(W1.shape[1])
+            a1 = torch.empty(b.numel(), h1, dtype=torch.float32, device=self.device)
+            L.check(self._lib.g2048_onehot_layer1(L.ptr(W1), L.ptr(b1), h1,
+                                                  {"ReLU": L.ACT_RELU, "Sigmoid": L.ACT_SIGMOID}[act], L.ptr(b),
+                                                  b.numel(), h1, L.ptr(a1), self._stream))
+            out, kept = mlp_forward_kept(params, None, act, a1=a1)
+            return out, kept, b, (self._mask_from_boards(b) if want_mask else None)
+        x, mk = steps.features(sel, k)
+        out, kept = mlp_forward_kept(params, x, act)
+        return out, kept, None, mk
+
+    def _onehot_dw1_into(self, boards: torch.Tensor, d1: torch.Tensor, acc: torch.Tensor) -> None:
+        """acc (fp64 [273 h1]: dW1 rows, then db1) += the one-hot first layer's weight / bias gradient of the deltas
+        d1 [m, h1] (g2048_onehot_dw1 partial slabs folded in fp64)."""
+        m, h1 = d1.shape
+        if m == 0:
+            return
+        d1 = d1.contiguous()
+        slices = -(-h1 // 64)
+        cus = int(self._lib.g2048_actor_grad_waves()) // 4
+        per = max(1024, -(-m * slices // (2 * cus)))
+        nparts = -(-m // per)
+        part = torch.empty(nparts, int(self._lib.g2048_onehot_dw1_slab(h1)), dtype=torch.float32, device=self.device)
+        L.check(self._lib.g2048_onehot_dw1(L.ptr(boards), L.ptr(d1), h1, m, h1, per, L.ptr(part), nparts,
+                                           self._stream))
+        self._fold(part, acc)
 
     def _packed_policy(self, spec) -> torch.Tensor:
         """The actor packed in MFMA fragment order (g2048_policy_pack), re-packed whenever a parameter tensor is
@@ -479,8 +592,8 @@ class ReinforceAgent:
                           gW: list[torch.Tensor], gb: list[torch.Tensor], spec) -> None:
         """The actor branch of update_batch (src/reinforce_agent.py:502-555) for every valid step and symmetry k:
         g2048_actor_grad (forward from the bitboards, masked softmax, deltas, dW1 / db1 / dW3 / db3 per wave)
-        plus one split-K GEMM for the layer-2 weight and bias gradient over the a1^T / d2^T columns the kernel
-        writes.  Accumulates into gW / gb like mlp_backward_."""
+        plus g2048_dw2 for the layer-2 weight and bias gradient over the a1^T / d2^T columns the kernel writes.
+        Accumulates into gW / gb like mlp_backward_."""
         use_mask = int(bool(self.env_config.use_action_mask))
 
         def launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale):
@@ -497,7 +610,7 @@ class ReinforceAgent:
         """The critic branch of update_batch (src/reinforce_agent.py:403-498, _get_grad_logits_critic :884-910):
         V(s') of every step with a successor by the fused forward (g2048_policy, logits only), the TD target
         r + gamma V(s') m on the device, then g2048_critic_grad (value, TD error into `deltas`, loss gradient and
-        backprop) and the same split-K GEMM as the actor."""
+        backprop) and the same g2048_dw2 pass as the actor."""
         c = self.agent_config
         loss = {"mse": 0, "huber": 1}[c.critic_loss_type]
         flat = steps.boards.reshape(-1)
@@ -564,7 +677,9 @@ class ReinforceAgent:
         starts = [0] * len(counts)
         for t in range(1, len(counts)):
             starts[t] = starts[t - 1] + counts[t - 1]
-        blk = 2048                                                         # 64 split-K blocks x 32 columns
+        # column-buffer width: a multiple of 2048 columns, so the buffer splits into whole g2048_dw2 parts
+        # (dw2_min_cols_per_part) and every row launch's 32-column groups stay inside it
+        blk = 2048
         ld = -(-max(self.grad_chunk_steps, max(counts) + 32) // blk) * blk
         # the tail: trailing rows t_tail.. with fewer than critic_tail_row_max samples each, at most ld - 32 in all
         t_tail, tail_m = len(counts), 0
@@ -673,8 +788,9 @@ class ReinforceAgent:
     def _fused_grad(self, params, slot: str, spec, steps: "_Steps", K: int, gW: list[torch.Tensor],
                     gb: list[torch.Tensor], out_dim: int, launch) -> None:
         """Chunked driver of the fused gradient kernels: per chunk of valid steps (symmetry k) `launch` runs the
-        kernel, then the layer-2 weight + bias gradient a1^T d2 is one split-K strided-batched GEMM and the
-        per-wave partials are summed; the padded gradients are cut to the net's shapes at the end."""
+        kernel, then the layer-2 weight + bias gradient a1^T d2 over the kernel's column buffers is g2048_dw2
+        (_dw2: bf16 three-plane MFMA, one fp32 slab per workgroup folded into fp64) and the per-wave partials are
+        folded into fp64 (g2048_fold_partials); the padded gradients are cut to the net's shapes at the end."""
         h1, h2, act = spec
         H1p, H2p = _padded_units(h1), _padded_units(h2)
         R = max(H1p, H2p)
@@ -753,7 +869,12 @@ class ReinforceAgent:
             raise ValueError("env_seeds and policy_seeds must have the same length")
         spec = self._fused_policy_spec()
         if spec is not None and rng == "pcg64" and self.env_config.max_steps is not None and self.use_fused_rollout:
+            self._paths["rollout"] = "g2048_rollout (one persistent launch)"
             return self._rollout_fused(env_seeds, policy_seeds, spec, use_greedy, record_probs)
+        dspec = self._deep_spec() if spec is None and self.use_fused_policy else None
+        self._paths["rollout"] = ("g2048_policy + g2048_step per step (active lanes)" if spec is not None else
+                                  "g2048_deep_policy + g2048_step per step (active lanes)" if dspec is not None else
+                                  "hipBLASLt forward (active lanes) + g2048_sample + g2048_step per step")
         env = self._vec_env(n, rng)
         env.reset(seed=_seed_seq(env_seeds))
         dev = self.device
@@ -780,6 +901,8 @@ class ReinforceAgent:
         # src/MLP.py:22-43 -> select_action src/reinforce_agent.py:138-145)
         use_mask = bool(self.env_config.use_action_mask)
         packed = self._packed_policy(spec) if spec is not None else None
+        dpacked = self._pack_deep(self.params, dspec, "actor", 4) if dspec is not None else None
+        logits_buf = None
         active_idx = None
         t = 0
         while True:
@@ -792,24 +915,33 @@ class ReinforceAgent:
                 if probs is not None:
                     probs = torch.cat([probs, torch.zeros(grow, n, 4, dtype=torch.float32, device=dev)])
                 cap += grow
-            if spec is not None:
-                # fused forward + choice straight from the boards, on the lanes still active at the last check
-                # (compacted every check_every steps); the step then skips the obs buffer
-                if active_idx is None or t % check_every == 0:
-                    active_idx = torch.nonzero(env.active).view(-1).to(torch.int32)
-                m = int(active_idx.numel())
-                L.check(self._lib.g2048_policy(L.ptr(packed), spec[0], spec[1], spec[2], L.ptr(env.board),
-                                               L.ptr(env.state), L.ptr(active_idx) if m < n else None,
-                                               _OBS_CODE[self.env_config.obs_mode],
-                                               float(self.env_config.obs_log2_scale), int(use_mask),
-                                               int(use_greedy), rng_mode, L.ptr(pst), L.ptr(pinc), L.ptr(pbuf),
-                                               env.philox_key ^ 0x5A5A, L.ptr(pseeds),
-                                               L.ptr(probs[t]) if probs is not None else None, None,
-                                               L.ptr(actions[t]), m if m < n else n, self._stream))
+            # the lanes still active at the last check (compacted every check_every steps)
+            if active_idx is None or t % check_every == 0:
+                active_idx = torch.nonzero(env.active).view(-1).to(torch.int32)
+            m = int(active_idx.numel())
+            if spec is not None or dspec is not None:
+                # fused forward + choice straight from the boards; the step then skips the obs buffer
+                common = (L.ptr(env.board), L.ptr(env.state), L.ptr(active_idx) if m < n else None,
+                          _OBS_CODE[self.env_config.obs_mode], float(self.env_config.obs_log2_scale), int(use_mask),
+                          int(use_greedy), rng_mode, L.ptr(pst), L.ptr(pinc), L.ptr(pbuf), env.philox_key ^ 0x5A5A,
+                          L.ptr(pseeds), L.ptr(probs[t]) if probs is not None else None, None, L.ptr(actions[t]),
+                          m if m < n else n, self._stream)
+                if spec is not None:
+                    L.check(self._lib.g2048_policy(L.ptr(packed), spec[0], spec[1], spec[2], *common))
+                else:
+                    L.check(self._lib.g2048_deep_policy(L.ptr(dpacked), len(dspec[1]), dspec[3], dspec[2], *common))
                 env.step_into(actions[t], reward=env.reward, flags=flags[t], prev_board=boards[t], write_obs=False,
                               reward64=rewards[t])
             else:
-                logits = self._policy_logits(env.obs)
+                if m < n:
+                    # forward only the active lanes; finished lanes are skipped by g2048_sample (lane state)
+                    if logits_buf is None:
+                        logits_buf = torch.zeros(n, 4, dtype=torch.float32, device=dev)
+                    ai = active_idx.long()
+                    logits_buf.index_copy_(0, ai, self._policy_logits(env.obs.index_select(0, ai)))
+                    logits = logits_buf
+                else:
+                    logits = self._policy_logits(env.obs)
                 L.check(self._lib.g2048_sample(L.ptr(logits), L.ptr(env.mask) if use_mask else None,
                                                L.ptr(env.state), int(use_greedy), rng_mode, L.ptr(pst),
                                                L.ptr(pinc), L.ptr(pbuf), env.philox_key ^ 0x5A5A, L.ptr(pseeds),
@@ -1086,19 +1218,32 @@ class ReinforceAgent:
             ncW = len(self.critic_params["W"])
             cspec = (self._fused_critic_spec() if steps.boards is not None and c.critic_loss_type in ("mse", "huber")
                      else None)
+            self._paths["critic_grad"] = "g2048_critic_grad + g2048_dw2" if cspec is not None else "hipBLASLt backprop"
             if cspec is not None:
                 with torch.no_grad():
                     self._critic_grad_fused(steps, step_w, K, critic_g[:ncW], critic_g[ncW:], deltas, cspec)
+            cdspec = self._deep_spec(self.critic_params, 1) if cspec is None and steps.boards is not None else None
+            oh1 = self._onehot_first_layer(steps) and cspec is None
+            acc1c = torch.zeros(273 * int(self.critic_params["W"][0].shape[1]), dtype=torch.float64,
+                                device=self.device) if oh1 else None
+            if cspec is None:
+                self._paths["critic_grad"] = (("g2048_onehot_layer1 + hipBLASLt backprop + g2048_onehot_dw1"
+                                               if oh1 else "hipBLASLt backprop") +
+                                              ("; V(s') by g2048_deep_policy" if cdspec is not None else ""))
             for k in range(K if cspec is None else 0):
                 for sel in self._chunks(steps.N):
-                    x, _ = steps.features(sel, k)
                     with torch.no_grad():
-                        v, kept = mlp_forward_kept(self.critic_params, x, self.mlp_config.activation)
+                        v, kept, bsel, _ = self._forward_kept_steps(self.critic_params, steps, sel, k)
                         v = v.view(-1)
                         hn = steps.has_next[sel]
-                        xn, _ = steps.features(sel, k, nxt=True)   # the step itself where there is no successor
-                        vn = forward_logits(self.critic_params, xn, self.mlp_config.activation,
-                                            keep_cache=False)[0].view(-1)
+                        # V(s'): the step itself where there is no successor (masked below)
+                        if cdspec is not None:
+                            vn = self._deep_forward(self.critic_params, cdspec, "critic",
+                                                    steps.boards_at(sel, k, nxt=True), 1)[:, 0]
+                        else:
+                            xn, _ = steps.features(sel, k, nxt=True)
+                            vn = forward_logits(self.critic_params, xn, self.mlp_config.activation,
+                                                keep_cache=False)[0].view(-1)
                         r = steps.rewards[sel]
                         tgt = r + (float(c.gamma) * vn) * hn.to(torch.float32)
                         deltas[k, sel] = tgt - v
@@ -1111,8 +1256,13 @@ class ReinforceAgent:
                         else:
                             raise ValueError(f"Unknown critic loss type: {c.critic_loss_type}")
                         g = g * step_w[sel]
+                        fl = (lambda d, b_=bsel: self._onehot_dw1_into(b_, d, acc1c)) if bsel is not None else None
                         mlp_backward_(self.critic_params, kept, self.mlp_config.activation, g.unsqueeze(1),
-                                      critic_g[:ncW], critic_g[ncW:])
+                                      critic_g[:ncW], critic_g[ncW:], first_layer_grad=fl)
+            if acc1c is not None:
+                h1c = int(self.critic_params["W"][0].shape[1])
+                critic_g[0] += acc1c[:272 * h1c].view(272, h1c).to(torch.float32)
+                critic_g[ncW] += acc1c[272 * h1c:].to(torch.float32)
             # advantages from TD errors, over all K x n "episodes"
             lane_k = (torch.arange(K, device=self.device).unsqueeze(1) * n_local + lane.unsqueeze(0)).reshape(-1)
             adv = self._advantages(deltas.reshape(-1), lane_k, K * n_local,
@@ -1124,19 +1274,30 @@ class ReinforceAgent:
 
         nW = len(self.params["W"])
         gspec = self._fused_grad_spec() if steps.boards is not None else None
+        self._paths["actor_grad"] = "g2048_actor_grad + g2048_dw2" if gspec is not None else "hipBLASLt backprop"
         with torch.no_grad():
             if gspec is not None:
                 self._actor_grad_fused(steps, adv, step_w, K, actor_g[:nW], actor_g[nW:], gspec)
+            oh1 = gspec is None and self._onehot_first_layer(steps)
+            acc1 = torch.zeros(273 * int(self.params["W"][0].shape[1]), dtype=torch.float64,
+                               device=self.device) if oh1 else None
+            if gspec is None and oh1:
+                self._paths["actor_grad"] = "g2048_onehot_layer1 + hipBLASLt backprop + g2048_onehot_dw1"
             for k in range(K if gspec is None else 0):
                 for sel in self._chunks(steps.N):
-                    x, mk = steps.features(sel, k)
+                    logits, kept, bsel, mk = self._forward_kept_steps(self.params, steps, sel, k, want_mask=True)
                     if steps.boards is not None and not self.env_config.use_action_mask:
                         mk = None   # bare-board obs: unmasked probabilities, as select_action used them
-                    logits, kept = mlp_forward_kept(self.params, x, self.mlp_config.activation)
                     p = logits_to_probs(logits, mk)
                     onehot = torch.nn.functional.one_hot(steps.actions_k(sel, k), 4).to(torch.float32)
                     g = (onehot - p) * (adv[k, sel] * step_w[sel]).unsqueeze(1)
-                    mlp_backward_(self.params, kept, self.mlp_config.activation, g, actor_g[:nW], actor_g[nW:])
+                    fl = (lambda d, b_=bsel: self._onehot_dw1_into(b_, d, acc1)) if bsel is not None else None
+                    mlp_backward_(self.params, kept, self.mlp_config.activation, g, actor_g[:nW], actor_g[nW:],
+                                  first_layer_grad=fl)
+            if acc1 is not None:
+                h1 = int(self.params["W"][0].shape[1])
+                actor_g[0] += acc1[:272 * h1].view(272, h1).to(torch.float32)
+                actor_g[nW] += acc1[272 * h1:].to(torch.float32)
 
             # ONE collective: actor + critic gradients and the episode count; then the 1 / n_traj weight
             dp.reduce_gradients_(actor_g + (critic_g or []), n_local * K)

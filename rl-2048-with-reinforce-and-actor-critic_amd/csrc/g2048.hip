@@ -985,6 +985,8 @@ int g2048_step(const g2048_lanes* lanes, const uint8_t* actions, const g2048_env
     if (!actions) return fail(G2048_EINVAL, "actions is NULL");
     if (!out || !out->reward || !out->flags) return fail(G2048_EINVAL, "out.reward / out.flags are required");
     if (n < 0) return fail(G2048_EINVAL, "n < 0");
+    if (rng_mode == G2048_RNG_PHILOX && cfg->max_steps < 0)
+        return fail(G2048_EINVAL, "Philox mode needs a finite max_steps: its draw counter is the 20-bit lane step count");
     const uint8_t* tab = nullptr;
     int cus = 256;
     if ((rc = tab_for_current(tab, cus))) return rc;

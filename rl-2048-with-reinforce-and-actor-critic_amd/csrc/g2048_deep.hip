@@ -1,0 +1,578 @@
+// g2048_deep.hip -- the policy / value MLP of ANY depth for the rollout and the update (part of libg2048.so).
+//
+// The reference's forward (forward_logits, src/MLP.py:159-196) is generic in depth: hidden_sizes is a list, and
+// runner.py documents [256, 128, 64] on one-hot obs (runner.py:10-47).  g2048_policy.hip's kernels are register-
+// specialised for two hidden layers of log2 / raw obs; this file covers the rest:
+//   * g2048_deep_policy: forward of 1..4 hidden layers of 1..256 units (ReLU / Sigmoid) + masked softmax +
+//     select_action's choice (src/reinforce_agent.py:178-190), straight from the bitboards -- no obs buffer.  One
+//     256-thread workgroup (4 waves) per group of 32 boards, two workgroups per CU: every layer's activations live
+//     in LDS ([unit][board], row stride 33 floats), its 32-unit output tiles are split over the 4 waves and run on
+//     v_mfma_f32_32x32x2_f32 (exact fp32, a k-ordered fmaf chain) with the weight fragments streamed from L2 in
+//     A-fragment order (one 16-B load per lane = four k-steps) and the activations as the B operand read from LDS;
+//     bias + activation in registers on the way back to LDS; the output layer (4 logits, or the value) on VALU.
+//   * the one-hot first layer (obs_mode "onehot": 16 cells x 17 one-hot features, src/env.py:131-150) is NOT a
+//     272-wide GEMM: x has exactly one 1 per cell, so x W1 = sum over the 16 cells of W1's row 17 c + e_c -- a gather
+//     of 16 rows of the (padded, row-major) W1 table, read straight from the bitboard's nibbles.  Each lane adds the
+//     float4 slices of its board's rows (the 8 lanes of one board read 128-B contiguous pieces of each 1 KiB row).
+//   * g2048_onehot_layer1 / g2048_onehot_dw1: the same gather for the update's kept layer-1 activations, and its
+//     transpose -- dW1 = X^T D1 of a one-hot X is a 16-row scatter-add of each sample's layer-1 delta: one wave owns
+//     a 64-unit slice of a [272][64] LDS accumulator (rows 17 c + e_c, conflict-free: one row per wave-wide add),
+//     a contiguous range of samples, and writes one fp32 partial slab; g2048_fold_partials sums the slabs in fp64.
+// Roofline: the dense layers are fp32-MFMA bound (157.3 TFLOP/s dense fp32 on MI355X); the one-hot gather moves
+// 16 rows x 4 H1 B per board through L1/L2 instead of 2 x 272 x H1 flops; dW1 is LDS-bound (16 adds of 256 B per
+// sample and slice).
+#include <hip/hip_runtime.h>
+
+#include "g2048.h"
+#include "g2048_core.h"
+
+using namespace g2048;
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxHidden = G2048_DEEP_MAX_HIDDEN;   // hidden layers
+constexpr int kDeepBlock = 256;                      // 4 waves; two workgroups per CU
+constexpr int kActStride = 33;                       // LDS activation row stride in floats: [unit][32 boards + 1]
+constexpr int kOneHotRows = 272;                     // 16 cells x 17 one-hot features (src/env.py:143-150)
+
+// the hidden unit held by accumulator register r of lane half h of a v_mfma_f32_32x32x2_f32 result tile
+__host__ __device__ inline int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// Packed net layout (floats; nt[l] = 32-unit tiles of hidden layer l, zero padded -- exact, a padded unit's
+// outgoing weights are zero):
+//   layer 0 weights   one-hot: table [272][32 nt0] row-major (row 17 c + e = W1[17 c + e, :]);
+//                     else:    A fragments [nt0][8][64] (k-step s, lane l: W1[2 s + (l >> 5)][32 t + (l & 31)])
+//   layer l >= 1      A fragments [nt_l][nt_{l-1}][4][64][4]: output tile o, k-tile t, lane l, k-step s = 4 q + u at
+//                     [o][t][q][l][u] = W_l[32 t + 2 s + (l >> 5)][32 o + (l & 31)]
+//   bias l            [32 nt_l]
+//   output layer      [32 nt_{L-1}][4] row-major (a value head is output 0), bias [4]
+struct DeepNet {
+    int L;                            // hidden layers
+    int onehot;                       // first layer is the one-hot gather table
+    int nt[kMaxHidden];
+    int64_t w[kMaxHidden + 1], b[kMaxHidden + 1];
+    int64_t total;
+};
+
+int tiles_of(int h) { return (h + 31) / 32; }
+
+bool deep_layout(int L, const int* hidden, int onehot, DeepNet& n) {
+    if (L < 1 || L > kMaxHidden || !hidden) return false;
+    n = DeepNet{};
+    n.L = L;
+    n.onehot = onehot;
+    int64_t off = 0;
+    for (int l = 0; l < L; l++) {
+        if (hidden[l] < 1 || hidden[l] > 256) return false;
+        n.nt[l] = tiles_of(hidden[l]);
+        n.w[l] = off;
+        if (l == 0) off += onehot ? (int64_t)kOneHotRows * 32 * n.nt[0] : (int64_t)n.nt[0] * 8 * 64;
+        else off += (int64_t)n.nt[l] * n.nt[l - 1] * 1024;
+        n.b[l] = off;
+        off += 32 * n.nt[l];
+    }
+    n.w[L] = off;
+    off += (int64_t)32 * n.nt[L - 1] * 4;
+    n.b[L] = off;
+    off += 4;
+    n.total = off;
+    return true;
+}
+
+struct DeepPackArgs {
+    DeepNet net;
+    const float* W[kMaxHidden + 1];
+    const float* B[kMaxHidden + 1];
+    int h[kMaxHidden];
+    int out;
+    float* dst;
+};
+
+// one thread per packed float
+__global__ void __launch_bounds__(256) deep_pack_kernel(DeepPackArgs a) {
+    const DeepNet& n = a.net;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n.total; q += (int64_t)gridDim.x * blockDim.x) {
+        float v = 0.0f;
+        int l = n.L;
+        while (l > 0 && q < n.w[l]) l--;          // the segment: [w[l], b[l]) weights, [b[l], w[l+1]) bias
+        if (l == n.L) {
+            if (q < n.b[l]) {
+                const int64_t x = q - n.w[l];
+                const int j = (int)(x >> 2), o = (int)(x & 3);
+                v = (j < a.h[n.L - 1] && o < a.out) ? a.W[n.L][(int64_t)j * a.out + o] : 0.0f;
+            } else {
+                const int o = (int)(q - n.b[l]);
+                v = o < a.out ? a.B[n.L][o] : 0.0f;
+            }
+        } else if (q >= n.b[l]) {
+            const int j = (int)(q - n.b[l]);
+            v = j < a.h[l] ? a.B[l][j] : 0.0f;
+        } else if (l == 0) {
+            const int64_t x = q - n.w[0];
+            if (n.onehot) {
+                const int H = 32 * n.nt[0];
+                const int row = (int)(x / H), j = (int)(x % H);
+                v = j < a.h[0] ? a.W[0][(int64_t)row * a.h[0] + j] : 0.0f;
+            } else {
+                const int lane = (int)(x & 63), s = (int)((x >> 6) & 7), t = (int)(x >> 9);
+                const int k = 2 * s + (lane >> 5), j = 32 * t + (lane & 31);
+                v = j < a.h[0] ? a.W[0][k * a.h[0] + j] : 0.0f;
+            }
+        } else {
+            const int64_t x = q - n.w[l];
+            const int u = (int)(x & 3), lane = (int)((x >> 2) & 63), qq = (int)((x >> 8) & 3);
+            const int64_t tt = x >> 10;
+            const int t = (int)(tt % n.nt[l - 1]), o = (int)(tt / n.nt[l - 1]);
+            const int k = 32 * t + 2 * (4 * qq + u) + (lane >> 5), j = 32 * o + (lane & 31);
+            v = (k < a.h[l - 1] && j < a.h[l]) ? a.W[l][(int64_t)k * a.h[l] + j] : 0.0f;
+        }
+        a.dst[q] = v;
+    }
+}
+
+template <int ACT>
+__device__ __forceinline__ float activate(float z) {
+    if constexpr (ACT == 0) return fmaxf(z, 0.0f);
+    else return 1.0f / (1.0f + expf(-z));
+}
+
+template <int OBS>
+__device__ __forceinline__ float obs_value(uint64_t b, int cell, float scale) {
+    const uint32_t e = (uint32_t)(b >> (4 * cell)) & 15u;
+    if constexpr (OBS == G2048_OBS_LOG2) return (float)e * scale;
+    else return e ? (float)(1u << e) : 0.0f;
+}
+
+struct DeepSmem {
+    float act[2][256 * kActStride];   // ping-pong activations [unit][board]
+    float part[8][32][4];             // output-layer partial sums [unit slice][board][output]
+    uint64_t board[32];               // the group's boards
+};
+
+// The forward of the group's 32 boards (S.board) through every hidden layer, leaving the output layer's 8 partial
+// sums per board in S.part (the caller adds them in order p = 0..7 plus the output bias).  Every thread of the
+// workgroup calls it; it ends with a barrier.
+template <int OBS, int ACT>
+__device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, DeepSmem& S, float obs_scale) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
+    // ---- first hidden layer -> S.act[0]
+    {
+        float* out = S.act[0];
+        const int nt0 = net.nt[0];
+        if constexpr (OBS == G2048_OBS_ONEHOT) {
+            // wave w: boards 8 w .. 8 w + 7, 8 lanes per board; lane k of a board: units 4 k + 32 m (m < nt0)
+            const int bb = 8 * w + (lane >> 3), k = lane & 7;
+            const uint64_t b = S.board[bb];
+            const int H = 32 * nt0;
+            const float* tab = P + net.w[0] + 4 * k;
+            float4 acc[8];
+#pragma unroll
+            for (int m = 0; m < 8; m++) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+            for (int c = 0; c < 16; c++) {
+                const float* row = tab + (int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * H;
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    if (m < nt0) {
+                        const float4 v = *reinterpret_cast<const float4*>(row + 32 * m);
+                        acc[m].x += v.x;
+                        acc[m].y += v.y;
+                        acc[m].z += v.z;
+                        acc[m].w += v.w;
+                    }
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < 8; m++) {
+                if (m < nt0) {
+                    const int u = 32 * m + 4 * k;
+                    const float4 bv = *reinterpret_cast<const float4*>(P + net.b[0] + u);
+                    out[(u + 0) * kActStride + bb] = activate<ACT>(acc[m].x + bv.x);
+                    out[(u + 1) * kActStride + bb] = activate<ACT>(acc[m].y + bv.y);
+                    out[(u + 2) * kActStride + bb] = activate<ACT>(acc[m].z + bv.z);
+                    out[(u + 3) * kActStride + bb] = activate<ACT>(acc[m].w + bv.w);
+                }
+            }
+        } else {
+            const uint64_t b = S.board[col];
+            float x[8];
+#pragma unroll
+            for (int s = 0; s < 8; s++) x[s] = obs_value<OBS>(b, 2 * s + h, obs_scale);
+            const float* w1f = P + net.w[0];
+            for (int t = w; t < nt0; t += 4) {
+                floatx16 acc = {};
+#pragma unroll
+                for (int s = 0; s < 8; s++)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1f[(t * 8 + s) * 64 + lane], x[s], acc, 0, 0, 0);
+                const float* bb = P + net.b[0] + 32 * t;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int u = tile_row(r, h);
+                    out[(32 * t + u) * kActStride + col] = activate<ACT>(acc[r] + bb[u]);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // ---- dense hidden layers 1 .. L-1 (ping-pong)
+    for (int l = 1; l < net.L; l++) {
+        const float* in = S.act[(l - 1) & 1];
+        float* out = S.act[l & 1];
+        const int ntin = net.nt[l - 1], ntout = net.nt[l];
+        const float4* __restrict__ frag = reinterpret_cast<const float4*>(P + net.w[l]) + lane;
+        const float* bias = P + net.b[l];
+        for (int o = w; o < ntout; o += 4) {
+            floatx16 acc = {};
+            const float4* fo = frag + (int64_t)o * ntin * 256;
+            float4 fa[4], fb[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) fa[q] = fo[q * 64];
+            for (int t = 0; t < ntin; t++) {
+                const float4* nx = fo + (t + 1 < ntin ? t + 1 : t) * 256;
+#pragma unroll
+                for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
+                const float* ib = in + (32 * t + h) * kActStride + col;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, ib[(8 * q + 0) * kActStride], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, ib[(8 * q + 2) * kActStride], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, ib[(8 * q + 4) * kActStride], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, ib[(8 * q + 6) * kActStride], acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) fa[q] = fb[q];
+            }
+            const float* bb = bias + 32 * o;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int u = tile_row(r, h);
+                out[(32 * o + u) * kActStride + col] = activate<ACT>(acc[r] + bb[u]);
+            }
+        }
+        __syncthreads();
+    }
+    // ---- output layer partials: thread (p = tid >> 5, board = tid & 31) sums units [p Hp / 8, (p + 1) Hp / 8)
+    {
+        const float* in = S.act[(net.L - 1) & 1];
+        const int Hp = 32 * net.nt[net.L - 1];
+        const int p = threadIdx.x >> 5, bb = threadIdx.x & 31, per = Hp >> 3;
+        const float4* wo = reinterpret_cast<const float4*>(P + net.w[net.L]);
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        for (int j = p * per; j < (p + 1) * per; j++) {
+            const float x = in[j * kActStride + bb];
+            const float4 wv = wo[j];
+            s0 = fmaf(x, wv.x, s0);
+            s1 = fmaf(x, wv.y, s1);
+            s2 = fmaf(x, wv.z, s2);
+            s3 = fmaf(x, wv.w, s3);
+        }
+        S.part[p][bb][0] = s0;
+        S.part[p][bb][1] = s1;
+        S.part[p][bb][2] = s2;
+        S.part[p][bb][3] = s3;
+    }
+    __syncthreads();
+}
+
+// the 4 outputs of board `bb` from the partials (threads 0..31 after deep_forward)
+__device__ __forceinline__ void deep_logits(const DeepNet& net, const float* __restrict__ P, const DeepSmem& S, int bb,
+                                            float lg[4]) {
+    const float* bo = P + net.b[net.L];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        float v = S.part[0][bb][k];
+#pragma unroll
+        for (int p = 1; p < 8; p++) v += S.part[p][bb][k];
+        lg[k] = v + bo[k];
+    }
+}
+
+struct DeepPolArgs {
+    DeepNet net;
+    const float* packed;
+    const uint64_t* boards;
+    const uint32_t* lane_state;   // env lane state words (G2048_LS_ACTIVE, step count) or NULL
+    const int32_t* lane_index;    // entry j -> lane lane_index[j] (NULL: lane j)
+    uint64_t *rs, *inc, *buf;
+    uint64_t key;
+    const uint64_t* lane_seed;
+    float* probs_out;
+    float* logits_out;
+    uint8_t* actions;             // NULL: forward only (logits_out / the value of a critic net)
+    float obs_scale;
+    uint32_t n;
+    int use_mask, greedy;
+};
+
+__device__ __forceinline__ uint32_t mask_word_of(uint64_t b) {
+    const uint32_t m = action_mask(b);   // int8[4] as one word: byte a = bit a
+    return (m & 1u) | ((m & 2u) << 7) | ((m & 4u) << 14) | ((m & 8u) << 21);
+}
+
+template <int OBS, int ACT, int RNG>
+__global__ void __launch_bounds__(kDeepBlock, 2) deep_policy_kernel(DeepPolArgs a) {
+    __shared__ DeepSmem S;
+    const uint32_t groups = (a.n + 31u) >> 5;
+    const int tid = threadIdx.x;
+    for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
+        const uint32_t j = gi * 32u + (uint32_t)(tid & 31);
+        const uint32_t jc = j < a.n ? j : a.n - 1u;
+        const uint32_t i = a.lane_index ? (uint32_t)a.lane_index[jc] : jc;
+        if (tid < 32) S.board[tid] = a.boards[i];
+        __syncthreads();
+        deep_forward<OBS, ACT>(a.net, a.packed, S, a.obs_scale);
+        if (tid < 32 && j < a.n) {
+            const uint32_t ls = a.lane_state ? a.lane_state[i] : G2048_LS_ACTIVE;
+            if (ls & G2048_LS_ACTIVE) {
+                float lg[4];
+                deep_logits(a.net, a.packed, S, tid, lg);
+                if (a.logits_out) reinterpret_cast<float4*>(a.logits_out)[i] = make_float4(lg[0], lg[1], lg[2], lg[3]);
+                if (a.actions) {
+                    const uint32_t mw = a.use_mask ? mask_word_of(S.board[tid]) : 0x01010101u;
+                    double u = 0.0;
+                    if (!a.greedy) {
+                        if constexpr (RNG == G2048_RNG_PCG64) {
+                            Pcg64 g;
+                            const ulonglong2 sv = reinterpret_cast<const ulonglong2*>(a.rs)[i];
+                            const ulonglong2 iv = reinterpret_cast<const ulonglong2*>(a.inc)[i];
+                            const uint64_t bf = a.buf[i];
+                            g.s_lo = sv.x; g.s_hi = sv.y; g.i_lo = iv.x; g.i_hi = iv.y;
+                            g.has_uint32 = (uint32_t)(bf >> 32); g.uinteger = (uint32_t)bf;
+                            u = pcg_random(g);
+                            reinterpret_cast<ulonglong2*>(a.rs)[i] = make_ulonglong2(g.s_lo, g.s_hi);
+                        } else {
+                            const uint64_t sd = a.lane_seed ? a.lane_seed[i] : (uint64_t)i;
+                            U4 c{(uint32_t)sd, (uint32_t)(sd >> 32), ls & G2048_LS_STEP_MASK, 3u};
+                            const U4 r = philox4x32(c, (uint32_t)a.key, (uint32_t)(a.key >> 32));
+                            const uint64_t xx = ((uint64_t)r.x << 32) | r.y;
+                            u = (double)(xx >> 11) * (1.0 / 9007199254740992.0);
+                        }
+                    }
+                    float p[4];
+                    const uint32_t act = softmax_select(lg, mw, a.use_mask != 0, a.greedy != 0, u, p);
+                    if (a.probs_out) reinterpret_cast<float4*>(a.probs_out)[i] = make_float4(p[0], p[1], p[2], p[3]);
+                    a.actions[i] = (uint8_t)act;
+                }
+            }
+        }
+        // S.board is rewritten by threads 0..31 only, after they finished with it; every other LDS buffer is
+        // rewritten only after the next group's first barrier
+    }
+}
+
+// ------------------------------------------------------------------------------------ one-hot layer 1 (update)
+// a1[s][j] = act(b1[j] + sum_c W1[17 c + e_c(s)][j]) for samples s < m, units j < h1: one wave per sample (lanes =
+// units, 64 at a time), rows read coalesced from the unpadded [272][h1] weight (the torch parameter itself).
+template <int ACT>
+__global__ void __launch_bounds__(256) onehot_l1_kernel(const float* __restrict__ W1, const float* __restrict__ b1,
+                                                         const uint64_t* __restrict__ boards, int h1, int64_t m,
+                                                         int64_t ld, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t s = wave; s < m; s += waves) {
+        const uint64_t b = boards[s];
+        for (int j0 = 0; j0 < h1; j0 += 64) {
+            const int j = j0 + lane;
+            if (j < h1) {
+                float acc = 0.0f;
+#pragma unroll
+                for (int c = 0; c < 16; c++) acc += W1[(int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * h1 + j];
+                out[s * ld + j] = activate<ACT>(acc + b1[j]);
+            }
+        }
+    }
+}
+
+// dW1 / db1 partials of a one-hot first layer: block (slice, part) owns units [64 slice, 64 slice + 64) and
+// samples [part * per, ...): acc[17 c + e_c(s)][lane] += d1[s][64 slice + lane] in sample order (one wave, LDS adds
+// in program order: deterministic), then slab rows 0..271 = dW1 and row 272 = db1 of its columns.
+constexpr int kDw1Rows = kOneHotRows + 1;
+
+__global__ void __launch_bounds__(64) onehot_dw1_kernel(const uint64_t* __restrict__ boards, const float* __restrict__ d1,
+                                                        int h1, int64_t m, int64_t ld, int64_t per,
+                                                        float* __restrict__ part) {
+    __shared__ float acc[kOneHotRows * 64];
+    const int lane = threadIdx.x;
+    const int slice = blockIdx.x, p = blockIdx.y;
+    const int j = 64 * slice + lane;
+    for (int r = 0; r < kOneHotRows; r++) acc[r * 64 + lane] = 0.0f;
+    float db = 0.0f;
+    const int64_t s0 = (int64_t)p * per, s1 = s0 + per < m ? s0 + per : m;
+    const bool live = j < h1;
+    const auto add = [&](uint64_t b, float v) {
+        db += v;
+#pragma unroll
+        for (int c = 0; c < 16; c++) acc[(17 * c + (int)((b >> (4 * c)) & 15u)) * 64 + lane] += v;
+    };
+    int64_t s = s0;
+    for (; s + 4 <= s1; s += 4) {                   // the next 4 samples' loads in flight together
+        uint64_t bq[4];
+        float vq[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            bq[k] = boards[s + k];                      // wave-uniform
+            vq[k] = live ? d1[(s + k) * ld + j] : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) add(bq[k], vq[k]);
+    }
+    for (; s < s1; s++) add(boards[s], live ? d1[s * ld + j] : 0.0f);
+    float* slab = part + (int64_t)p * kDw1Rows * h1;
+    if (live) {
+        for (int r = 0; r < kOneHotRows; r++) slab[(int64_t)r * h1 + j] = acc[r * 64 + lane];
+        slab[(int64_t)kOneHotRows * h1 + j] = db;
+    }
+}
+
+int device_cus() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0) cus = c;
+    }
+    return cus;
+}
+
+template <int OBS, int ACT>
+void launch_deep_rng(const DeepPolArgs& a, int rng, int grid, hipStream_t s) {
+    if (rng == G2048_RNG_PCG64)
+        hipLaunchKernelGGL((deep_policy_kernel<OBS, ACT, G2048_RNG_PCG64>), dim3(grid), dim3(kDeepBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL((deep_policy_kernel<OBS, ACT, G2048_RNG_PHILOX>), dim3(grid), dim3(kDeepBlock), 0, s, a);
+}
+
+template <int OBS>
+void launch_deep_act(const DeepPolArgs& a, int act, int rng, int grid, hipStream_t s) {
+    if (act == G2048_ACT_RELU) launch_deep_rng<OBS, 0>(a, rng, grid, s);
+    else launch_deep_rng<OBS, 1>(a, rng, grid, s);
+}
+
+}  // namespace
+
+namespace g2048_internal {   // g2048.hip
+int set_error(int code, const char* msg);
+}  // namespace g2048_internal
+
+namespace {
+int dfail(int code, const char* msg) { return g2048_internal::set_error(code, msg); }
+int check_hip() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK : dfail(G2048_EHIP, hipGetErrorString(e));
+}
+}  // namespace
+
+extern "C" {
+
+int64_t g2048_deep_packed_size(int obs_mode, int n_hidden, const int32_t* hidden) {
+    DeepNet n;
+    if (obs_mode != G2048_OBS_LOG2 && obs_mode != G2048_OBS_RAW && obs_mode != G2048_OBS_ONEHOT) return -1;
+    if (!deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, n)) return -1;
+    return n.total;
+}
+
+int g2048_deep_pack(const float* const* W, const float* const* b, int obs_mode, int n_hidden, const int32_t* hidden,
+                    int out_dim, float* packed, int64_t packed_len, void* stream) {
+    DeepNet n;
+    if (obs_mode != G2048_OBS_LOG2 && obs_mode != G2048_OBS_RAW && obs_mode != G2048_OBS_ONEHOT)
+        return dfail(G2048_EINVAL, "deep policy: obs_mode must be log2, raw or onehot");
+    if (!deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, n))
+        return dfail(G2048_EINVAL, "deep policy: 1..4 hidden layers of 1..256 units");
+    if (out_dim != 1 && out_dim != 4) return dfail(G2048_EINVAL, "deep policy: output width must be 4 or 1");
+    if (!W || !b || !packed) return dfail(G2048_EINVAL, "deep policy: NULL buffer");
+    if (packed_len < n.total) return dfail(G2048_EINVAL, "deep policy: packed buffer too small");
+    DeepPackArgs a{};
+    a.net = n;
+    for (int l = 0; l <= n_hidden; l++) {
+        if (!W[l] || !b[l]) return dfail(G2048_EINVAL, "deep policy: NULL weight");
+        a.W[l] = W[l];
+        a.B[l] = b[l];
+    }
+    for (int l = 0; l < n_hidden; l++) a.h[l] = hidden[l];
+    a.out = out_dim;
+    a.dst = packed;
+    const int grid = (int)((n.total + 255) / 256 < 4096 ? (n.total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(deep_pack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    return check_hip();
+}
+
+int g2048_deep_policy(const float* packed, int n_hidden, const int32_t* hidden, int activation, const uint64_t* boards,
+                      const uint32_t* lane_state, const int32_t* lane_index, int obs_mode, float obs_scale, int use_mask,
+                      int greedy, int rng_mode, uint64_t* rng_state, const uint64_t* rng_inc, const uint64_t* rng_buf,
+                      uint64_t philox_key, const uint64_t* lane_seed, float* probs_out, float* logits_out,
+                      uint8_t* actions, int64_t n, void* stream) {
+    if (n < 0 || n > (int64_t)0xFFFFFFE0) return dfail(G2048_EINVAL, "n out of range");
+    if (obs_mode != G2048_OBS_LOG2 && obs_mode != G2048_OBS_RAW && obs_mode != G2048_OBS_ONEHOT)
+        return dfail(G2048_EINVAL, "deep policy: obs_mode must be log2, raw or onehot");
+    DeepNet net;
+    if (!deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, net))
+        return dfail(G2048_EINVAL, "deep policy: 1..4 hidden layers of 1..256 units");
+    if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
+        return dfail(G2048_EINVAL, "Unsupported activation");
+    if (rng_mode != G2048_RNG_PCG64 && rng_mode != G2048_RNG_PHILOX) return dfail(G2048_EINVAL, "Unsupported rng_mode");
+    if (!packed || !boards || (!actions && !logits_out))
+        return dfail(G2048_EINVAL, "deep policy: packed / boards and actions or logits_out are required");
+    if (actions && !greedy && rng_mode == G2048_RNG_PCG64 && (!rng_state || !rng_inc || !rng_buf))
+        return dfail(G2048_EINVAL, "PCG64 sampling needs rng_state / rng_inc / rng_buf");
+    if (n == 0) return G2048_OK;
+    DeepPolArgs a;
+    a.net = net;
+    a.packed = packed;
+    a.boards = boards;
+    a.lane_state = lane_state;
+    a.lane_index = lane_index;
+    a.rs = rng_state;
+    a.inc = const_cast<uint64_t*>(rng_inc);
+    a.buf = const_cast<uint64_t*>(rng_buf);
+    a.key = philox_key;
+    a.lane_seed = lane_seed;
+    a.probs_out = probs_out;
+    a.logits_out = logits_out;
+    a.actions = actions;
+    a.obs_scale = obs_scale;
+    a.n = (uint32_t)n;
+    a.use_mask = use_mask;
+    a.greedy = greedy;
+    const int64_t groups = (n + 31) / 32;
+    const int64_t cap = 2 * (int64_t)device_cus();   // persistent: two workgroups per CU
+    const int grid = (int)(groups < cap ? groups : cap);
+    hipStream_t s = (hipStream_t)stream;
+    if (obs_mode == G2048_OBS_ONEHOT) launch_deep_act<G2048_OBS_ONEHOT>(a, activation, rng_mode, grid, s);
+    else if (obs_mode == G2048_OBS_LOG2) launch_deep_act<G2048_OBS_LOG2>(a, activation, rng_mode, grid, s);
+    else launch_deep_act<G2048_OBS_RAW>(a, activation, rng_mode, grid, s);
+    return check_hip();
+}
+
+int g2048_onehot_layer1(const float* W1, const float* b1, int h1, int activation, const uint64_t* boards, int64_t m,
+                        int64_t ld, float* out, void* stream) {
+    if (m < 0 || h1 < 1 || ld < h1) return dfail(G2048_EINVAL, "one-hot layer 1: bad m / h1 / ld");
+    if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
+        return dfail(G2048_EINVAL, "Unsupported activation");
+    if (!W1 || !b1 || (m > 0 && (!boards || !out))) return dfail(G2048_EINVAL, "one-hot layer 1: NULL buffer");
+    if (m == 0) return G2048_OK;
+    const int64_t blocks = (m + 3) / 4;
+    const int grid = (int)(blocks < 8 * device_cus() ? blocks : 8 * device_cus());
+    hipStream_t s = (hipStream_t)stream;
+    if (activation == G2048_ACT_RELU)
+        hipLaunchKernelGGL(onehot_l1_kernel<0>, dim3(grid), dim3(256), 0, s, W1, b1, boards, h1, m, ld, out);
+    else
+        hipLaunchKernelGGL(onehot_l1_kernel<1>, dim3(grid), dim3(256), 0, s, W1, b1, boards, h1, m, ld, out);
+    return check_hip();
+}
+
+int64_t g2048_onehot_dw1_slab(int h1) { return h1 < 1 || h1 > 256 ? -1 : (int64_t)kDw1Rows * h1; }
+
+int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m, int64_t ld, int64_t per,
+                     float* partials, int64_t nparts, void* stream) {
+    if (h1 < 1 || h1 > 256 || m < 0 || ld < h1 || per < 1) return dfail(G2048_EINVAL, "one-hot dW1: bad sizes");
+    if (nparts != (m + per - 1) / per || nparts > 65535) return dfail(G2048_EINVAL, "one-hot dW1: nparts != ceil(m / per)");
+    if (m > 0 && (!boards || !d1 || !partials)) return dfail(G2048_EINVAL, "one-hot dW1: NULL buffer");
+    if (m == 0) return G2048_OK;
+    hipLaunchKernelGGL(onehot_dw1_kernel, dim3((h1 + 63) / 64, (unsigned)nparts), dim3(64), 0, (hipStream_t)stream,
+                       boards, d1, h1, m, ld, per, partials);
+    return check_hip();
+}
+
+}  // extern "C"

@@ -298,6 +298,9 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
         } else {
             mfma(pa);
         }
+        // the LDS-DMA refills issued past the last stage (kept so the wait count stays uniform) are not tracked
+        // by the compiler: drain them before the workgroup ends, so its LDS is never handed on with writes in flight
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     // this workgroup's slab: dW2 rows from the accumulators (C/D layout: column = lane & 31, row = acc_row), db2
     // (FAC: each column scaled by W3[j] -- the one multiply of the factored form)

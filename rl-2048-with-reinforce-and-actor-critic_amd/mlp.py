@@ -136,12 +136,18 @@ def _wgrad_(out: torch.Tensor, a: torch.Tensor, d: torch.Tensor) -> None:
         out.addmm_(a.t(), d)
 
 
-def mlp_forward_kept(params: dict[str, list[torch.Tensor]], x: torch.Tensor, activation_mode: str):
-    """forward_logits (src/MLP.py:159-196) keeping the layer inputs a_0..a_{L-1} for mlp_backward_."""
+def mlp_forward_kept(params: dict[str, list[torch.Tensor]], x: torch.Tensor | None, activation_mode: str,
+                     a1: torch.Tensor | None = None):
+    """forward_logits (src/MLP.py:159-196) keeping the layer inputs a_0..a_{L-1} for mlp_backward_.  a1: the first
+    hidden layer's activations computed elsewhere (the one-hot gather, g2048_onehot_layer1); then x is not needed
+    and a_0 is kept as None."""
     Ws, bs = params["W"], params["b"]
-    acts = [x.to(torch.float32)]
-    a = acts[0]
-    for i in range(len(Ws)):
+    if a1 is not None:
+        acts, a, first = [None, a1], a1, 1
+    else:
+        acts = [x.to(torch.float32)]
+        a, first = acts[0], 0
+    for i in range(first, len(Ws)):
         if i < len(Ws) - 1 and activation_mode == "ReLU" and a.dim() == 2:
             a = torch._addmm_activation(bs[i], a, Ws[i], use_gelu=False)   # bias + ReLU in the GEMM epilogue
             acts.append(a)
@@ -156,15 +162,20 @@ def mlp_forward_kept(params: dict[str, list[torch.Tensor]], x: torch.Tensor, act
 
 
 def mlp_backward_(params: dict[str, list[torch.Tensor]], acts: list[torch.Tensor], activation_mode: str,
-                  grad_out: torch.Tensor, grad_W: list[torch.Tensor], grad_b: list[torch.Tensor]) -> None:
+                  grad_out: torch.Tensor, grad_W: list[torch.Tensor], grad_b: list[torch.Tensor],
+                  first_layer_grad=None) -> None:
     """The manual backprop of src/reinforce_agent.py:_backpropagation (:639-678) and _activation_derivative
     (:624-636) for a whole batch at once: given the kept layer inputs (mlp_forward_kept) and dL/d(output) =
     grad_out [m, out], ACCUMULATE dL/dW_i = a_i^T d_i and dL/db_i = sum_rows d_i into grad_W / grad_b (tensors
     shaped like the params), with d_{i-1} = (d_i W_i^T) * act'(a_i); act' = 1[a > 0] (ReLU) or a (1 - a)
-    (Sigmoid), computed from the kept activation."""
+    (Sigmoid), computed from the kept activation.  first_layer_grad(d1): accumulates layer 0's weight and bias
+    gradient from its delta instead (the one-hot scatter, g2048_onehot_dw1; acts[0] is then None)."""
     Ws = params["W"]
     d = grad_out
     for i in range(len(Ws) - 1, -1, -1):
+        if i == 0 and first_layer_grad is not None:
+            first_layer_grad(d)
+            break
         _wgrad_(grad_W[i], acts[i], d)
         grad_b[i].add_(d.sum(0))
         if i > 0:

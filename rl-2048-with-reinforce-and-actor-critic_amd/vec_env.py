@@ -90,10 +90,15 @@ class VecGame2048Env:
         self.config = config or Game2048EnvConfig()
         self._cfg = env_cfg_struct(self.config)          # validates modes (ValueError like src/env.py:110,223,249)
         self.n = int(num_envs)
-        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        L.ensure_device(self.device)
         if rng not in ("pcg64", "philox"):
             raise ValueError(f"Unsupported rng: {rng}")
+        if rng == "philox" and self.config.max_steps is None:
+            # the Philox counter of the spawn / policy draws is the lane's 20-bit step count: past 2**20 - 1 steps
+            # of one episode the draws would repeat (and a lane repeating an unmasked invalid action never ends)
+            raise ValueError("rng='philox' needs a finite max_steps (<= "
+                             f"{L.MAX_STEPS_LIMIT}): its draw counter is the 20-bit lane step count")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        L.ensure_device(self.device)
         self.rng_mode = L.RNG_PCG64 if rng == "pcg64" else L.RNG_PHILOX
         self.auto_reset = bool(auto_reset)
         self.reset_stride = int(reset_stride if reset_stride is not None else num_envs)

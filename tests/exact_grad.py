@@ -97,6 +97,44 @@ def bwd64(W, x, z1, a1, z2, a2, g, acc):
     acc[3] += d1.sum(0)
 
 
+_U32 = 2.0 ** -24   # fp32 unit roundoff
+
+
+def _gamma(n: int) -> float:
+    """gamma_n = n u / (1 - n u): the classical bound on the relative error of an n-term fp32 dot product
+    accumulated by recursive (fmaf-chain) summation, relative to the sum of the terms' magnitudes."""
+    return n * _U32 / (1.0 - n * _U32)
+
+
+def pattern_flip_check(W, b, x, z1, z2, m1, m2, stats: dict, key: str) -> None:
+    """Bound the fp32 path's ReLU pattern (m1, m2: bool [m, h], as the kernels used it) against fp64's own
+    (z1 > 0, z2 > 0 of the exact forward):
+      layer 1:  |fl32(z1) - z1| <= e1 = gamma_{17} (|x| |W1| + |b1|)   (16 obs features + bias; the obs are exact);
+      layer 2:  |fl32(z2) - z2| <= e2 = gamma_{h1+1} ((a1 + e1) |W2| + |b2|) + e1 |W2|   (the fp32 a1 differs from
+                the exact one by at most e1 per unit -- ReLU is 1-Lipschitz -- and enters an h1-term sum).
+    A unit-sample on which the two patterns disagree must therefore have |z| <= e; stats[key] accumulates the
+    disagreement counts, the unit-samples compared and the violations of the bound.  A layer-2 row whose kernel
+    pattern is all-zero is skipped (the kernel reads its pattern from d2 != 0, and d2 = 0 there because the
+    sample's loss gradient g is 0 -- no ReLU is consulted)."""
+    st = stats.setdefault(key, dict(n1=0, n2=0, tot1=0, tot2=0, viol1=0, viol2=0, max_ratio=0.0))
+    e1 = _gamma(x.shape[1] + 1) * (x.abs() @ W[0].abs() + b[0].abs())
+    d1 = (z1 > 0) != m1
+    st["n1"] += int(d1.sum())
+    st["tot1"] += d1.numel()
+    st["viol1"] += int((d1 & (z1.abs() > e1)).sum())
+    a1 = torch.relu(z1)
+    W2a = W[1].abs()
+    e2 = _gamma(W[1].shape[0] + 1) * ((a1 + e1) @ W2a + b[1].abs()) + e1 @ W2a
+    live = m2.any(dim=1, keepdim=True)
+    d2 = ((z2 > 0) != m2) & live
+    st["n2"] += int(d2.sum())
+    st["tot2"] += int(live.sum()) * m2.shape[1]
+    st["viol2"] += int((d2 & (z2.abs() > e2)).sum())
+    for d, z, e in ((d1, z1, e1), (d2, z2, e2)):
+        if bool(d.any()):
+            st["max_ratio"] = max(st["max_ratio"], float((z.abs()[d] / e[d]).max()))
+
+
 def _net64(params):
     return [w.double() for w in params["W"]], [b.double() for b in params["b"]]
 
@@ -121,11 +159,14 @@ def snapshot(agent) -> tuple[dict, dict | None]:
     return cp(agent.params), cp(agent.critic_params)
 
 
-def exact_update_grads(agent, batch, patterns=None, chunk: int | None = None, params=None) -> dict:
+def exact_update_grads(agent, batch, patterns=None, chunk: int | None = None, params=None, flip_probe=None,
+                       flip_stats: dict | None = None) -> dict:
     """Pre-clip gradients {"actor": [...], "critic": [...]} of update_batch on `batch`, fp64, under `patterns`
     (None, "plain" or a PatternProbe).  params: (actor, critic) parameter dicts (snapshot()) -- default the
     agent's current ones.  Covers the configurations the GPU tests use: ReLU nets, MSE / Huber critic, baselines
-    off / batch / batch_norm / each, augmentation; no reward rank weights."""
+    off / batch / batch_norm / each, augmentation; no reward rank weights.  flip_probe (a PatternProbe, with
+    patterns=None): also compare the fused kernels' ReLU pattern with fp64's own on every sample
+    (pattern_flip_check), counts into flip_stats["actor" / "critic"]."""
     actor_p, critic_p = params if params is not None else (agent.params, agent.critic_params)
     c = agent.agent_config
     assert agent.mlp_config.activation == "ReLU" and not c.reward_rank_weights
@@ -177,6 +218,10 @@ def exact_update_grads(agent, batch, patterns=None, chunk: int | None = None, pa
                 hn = has_next[sl]
                 xn32 = agent._obs_from_boards(boards(torch.where(hn, vidx[sl] + n, vidx[sl]), k))[0]
                 z1, a1, z2, a2, v = fwd64(Wc, bc, x32.double(), masks_for("critic", critic_p, x32, k, sl))
+                if flip_probe is not None:
+                    pattern_flip_check(Wc, bc, x32.double(), z1, z2,
+                                       *flip_probe.masks("critic", k, sl, Wc[0].shape[1], Wc[1].shape[1]),
+                                       flip_stats, "critic")
                 vn = fwd64(Wc, bc, xn32.double())[4][:, 0]
                 r32 = R64.reshape(-1)[vidx[sl]].float().double()      # np.array(rewards, float32) (:420)
                 tgt = r32 + c.gamma * vn * hn.double()
@@ -216,6 +261,9 @@ def exact_update_grads(agent, batch, patterns=None, chunk: int | None = None, pa
             sl = slice(s, min(s + chunk, N))
             x32, mk = agent._obs_from_boards(boards(vidx[sl], k))
             z1, a1, z2, a2, lg = fwd64(W, b, x32.double(), masks_for("actor", actor_p, x32, k, sl))
+            if flip_probe is not None:
+                pattern_flip_check(W, b, x32.double(), z1, z2,
+                                   *flip_probe.masks("actor", k, sl, W[0].shape[1], W[1].shape[1]), flip_stats, "actor")
             if use_mask:
                 lg = torch.where(mk.bool(), lg, torch.full_like(lg, -1e9))
             p = torch.softmax(lg, dim=1)

@@ -263,6 +263,30 @@ def _update_cases():
             hidden_sizes=[256, 256], activation="ReLU", init_distribution="HeNormal", last_init_normal=True),
             agent=dict(gamma=0.99, learning_rate=1e-4, baseline_mode="batch_norm", optimizer="adam", use_critic=True,
                        critic_learning_rate=1e-4, model_seed=1), n=4, updates=1),
+        # round 4: one-hot first layers and depth != 2 (the fused-kernel families of g2048_deep.hip); the first is
+        # the configuration runner.py documents in its header (runner.py:10-47), max_steps None included
+        dict(name="refconf-onehot-256-128-64", env=dict(
+            obs_mode="onehot", obs_log2_scale=1.0, reward_mode="log2", base_reward_scale=1.0, bonus_mode="off",
+            bonus_scale=1.0, step_reward=0.0, endgame_penalty=0.0, use_action_mask=True, invalid_action_penalty=-1.0,
+            max_steps=None, empty_tile_reward=0.05, merge_reward=0.0), mlp=dict(
+            hidden_sizes=[256, 128, 64], activation="ReLU", init_distribution="HeNormal", last_init_normal=True),
+            agent=dict(gamma=0.99, learning_rate=0.01, baseline_mode="batch", model_seed=0, optimizer="adam",
+                       adam_beta1=0.9, adam_beta2=0.999, augmentation=False, use_critic=True,
+                       critic_learning_rate=0.0005, critic_loss_type="mse", huber_delta=1.0), n=4, updates=2),
+        dict(name="deep3-log2-batch-sgd", env=ENV_A, mlp=dict(
+            hidden_sizes=[64, 48, 32], activation="ReLU", init_distribution="HeNormal", last_init_normal=True),
+            agent=dict(gamma=0.99, learning_rate=1e-2, baseline_mode="batch", model_seed=109)),
+        dict(name="onehot-relu-128x64-huber", env=dict(ENV_B, obs_mode="onehot"), mlp=dict(
+            hidden_sizes=[128, 64], activation="ReLU", init_distribution="HeNormal", last_init_normal=True),
+            agent=dict(gamma=0.99, learning_rate=1e-2, baseline_mode="batch_norm", optimizer="adam", use_critic=True,
+                       critic_loss_type="huber", huber_delta=0.5, critic_learning_rate=5e-3, model_seed=110)),
+        dict(name="deep4-onehot-sigmoid-each", env=dict(ENV_A, obs_mode="onehot"), mlp=dict(
+            hidden_sizes=[40, 33, 20, 10], activation="Sigmoid", init_distribution="XavierNormal",
+            last_init_normal=True), agent=dict(gamma=0.95, learning_rate=1e-2, baseline_mode="each", model_seed=111)),
+        dict(name="onehot-relu-aug-critic", env=dict(ENV_A, obs_mode="onehot"), mlp=dict(
+            hidden_sizes=[64, 32], activation="ReLU", init_distribution="HeNormal", last_init_normal=True),
+            agent=dict(gamma=0.99, learning_rate=1e-2, baseline_mode="batch", augmentation=True, use_critic=True,
+                       model_seed=112), n=4),
     ]
     for e in extra:
         e.setdefault("n", 6)

@@ -29,6 +29,14 @@ def update_cases() -> list[dict]:
     return json.loads(str(load("update")["cases"]))
 
 
+def _n_update_cases() -> int:
+    with np.load(os.path.join(GOLDEN, "update.npz"), allow_pickle=False) as z:
+        return len(json.loads(str(z["cases"])))
+
+
+N_UPDATE_CASES = _n_update_cases()
+
+
 def n_layers(case: dict) -> int:
     return len(case["mlp"]["hidden_sizes"]) + 1
 

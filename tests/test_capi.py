@@ -31,7 +31,8 @@ def test_header_declares_expected_api():
         "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_packed_size",
         "g2048_policy_pack", "g2048_policy", "g2048_rollout", "g2048_grad_packed_size", "g2048_grad_partial_size",
         "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2",
-        "g2048_fold_partials", "g2048_dw2_factored"])
+        "g2048_fold_partials", "g2048_dw2_factored", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
+        "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1"])
 
 
 def test_library_exports_every_declared_symbol(L):
@@ -83,6 +84,12 @@ def test_argument_validation_without_gpu(L):
     cfg.reward_mode, cfg.max_steps = 0, L.MAX_STEPS_LIMIT + 1      # the 20-bit lane step count
     rc = lib.g2048_step(ctypes.byref(lanes), None, ctypes.byref(cfg), ctypes.byref(out), 0, 0, 0, 0, 1, None)
     assert rc == L.G2048_EINVAL and b"max_steps" in lib.g2048_last_error()
+    cfg.max_steps = -1                                                  # Philox draws need a finite max_steps
+    q = ctypes.c_void_p(8)
+    plan = L.Lanes(q, q, q, None, None, None)
+    pout = L.StepOut(q, q, None, None, None, None, None, None, None)
+    rc = lib.g2048_step(ctypes.byref(plan), q, ctypes.byref(cfg), ctypes.byref(pout), L.RNG_PHILOX, 0, 0, 0, 1, None)
+    assert rc == L.G2048_EINVAL and b"Philox" in lib.g2048_last_error()
     from rl2048_amd.config import Game2048EnvConfig, env_cfg_struct
 
     with pytest.raises(ValueError, match="max_steps"):
@@ -140,6 +147,15 @@ def test_config_validation_messages():
             env_cfg_struct(Game2048EnvConfig(**kw))
     assert env_cfg_struct(Game2048EnvConfig(max_steps=None)).max_steps == -1
     assert env_cfg_struct(Game2048EnvConfig(max_steps=0)).max_steps == 0
+
+
+def test_philox_needs_finite_max_steps():
+    """Philox's draw counter is the 20-bit lane step count, so a Philox env without max_steps is refused at
+    construction (before any device is touched); PCG64 without max_steps is fine."""
+    from rl2048_amd import Game2048EnvConfig, VecGame2048Env
+
+    with pytest.raises(ValueError, match="finite max_steps"):
+        VecGame2048Env(4, Game2048EnvConfig(max_steps=None), device="cpu", rng="philox")
 
 
 def test_no_cpu_fallback():

@@ -17,7 +17,9 @@ of the formula under the ReLU activation pattern each fp32 path computed (tests/
 pattern is read from their own column buffers (ReinforceAgent.grad_probe), the plain hipBLASLt path's recomputed
 on its own chunks.  At millions of samples fp32 rounding of pre-activations next to 0 flips ReLU derivatives, in
 every fp32 evaluation (the reference's included) on different samples; the errors against fp64 with fp64's own
-pattern are printed beside.
+pattern are printed beside.  That basis is itself checked: every unit-sample where the fused pattern differs from
+fp64's own must lie within the fp32 accumulation bound of the kink, and such unit-samples must be rare
+(tests/exact_grad.py pattern_flip_check).
 """
 import numpy as np
 import pytest
@@ -120,11 +122,14 @@ def _run_config(episodes, critic, k_sample):
     plain.update_from_batch(batch)
     exact_f = EG.exact_update_grads(agent, batch, patterns=probe, params=params0)
     errs = EG.grad_errors(agent.last_grads, exact_f)
-    del exact_f, probe
+    del exact_f
     exact_p = EG.exact_update_grads(plain, batch, patterns="plain", params=params0)
     errs_plain = EG.grad_errors(plain.last_grads, exact_p)
     del exact_p
-    exact = EG.exact_update_grads(agent, batch, params=params0)       # plain fp64, no imposed pattern
+    # plain fp64 (no imposed pattern), and the fused kernels' pattern compared with fp64's own on every unit-sample
+    flips: dict = {}
+    exact = EG.exact_update_grads(agent, batch, params=params0, flip_probe=probe, flip_stats=flips)
+    del probe
     errs_free = EG.grad_errors(agent.last_grads, exact)
     errs_free_plain = EG.grad_errors(plain.last_grads, exact)
     for which in nets:
@@ -134,6 +139,16 @@ def _run_config(episodes, critic, k_sample):
     print(f"\n{episodes} episodes, {N} steps: fused vs fp64 under the fused kernels' ReLU pattern {fmt(errs)} | "
           f"plain fp32 GEMM path vs fp64 under its pattern {fmt(errs_plain)} | vs fp64 with fp64's own pattern: "
           f"fused {fmt(errs_free)}, plain {fmt(errs_free_plain)}")
+    # the basis is bounded: every unit-sample where the fused kernels' ReLU pattern differs from fp64's own lies
+    # within the fp32 accumulation bound of the kink (|z| <= gamma_n sum |a w|, tests/exact_grad.py
+    # pattern_flip_check), and such unit-samples are rare (<= 1e-5 of those compared, per layer and net)
+    for which in nets:
+        f = flips[which]
+        print(f"{which}: ReLU pattern vs fp64's own: layer 1 {f['n1']} of {f['tot1']} unit-samples differ, layer 2 "
+              f"{f['n2']} of {f['tot2']}; bound violations {f['viol1']} / {f['viol2']}; max |z| / bound "
+              f"{f['max_ratio']:.3f}", flush=True)
+        assert f["viol1"] == 0 and f["viol2"] == 0, (which, f)
+        assert f["n1"] <= 1e-5 * f["tot1"] and f["n2"] <= 1e-5 * f["tot2"], (which, f)
     # the north star's 1e-5, for both fp32 paths, each against the exact value of the formula under the activation
     # pattern that path computed (module docstring)
     assert all(v < 1e-5 for v in errs.values()), errs

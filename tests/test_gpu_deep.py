@@ -1,0 +1,197 @@
+"""GPU: the any-depth / one-hot kernels of g2048_deep.hip against fp32 / fp64 references of the same ops.
+
+* g2048_deep_policy (forward only): logits / value of random nets of 1..4 hidden layers (sizes not multiples of
+  32 included), ReLU / Sigmoid, on log2 / raw / one-hot obs, against an fp64 forward of the materialised obs
+  (src/MLP.py:159-196) -- within fp32 accumulation error;
+* g2048_deep_policy (choice): the probabilities against torch's masked softmax of the kernel's own logits, and the
+  action against g2048_sample run on those logits with a copy of the same PCG64 streams (the same device
+  softmax_select and numpy Generator.choice replay: bit-identical), greedy included, compacted lane lists;
+* g2048_onehot_layer1 against act(onehot(obs) @ W1 + b1) in fp64;
+* g2048_onehot_dw1 (+ g2048_fold_partials) against X^T D1 / sum D1 in fp64, ragged part sizes.
+The end-to-end parity of these paths (rollouts and updates of one-hot / 3- and 4-layer nets, the reference
+runner's documented config included) is in tests/test_gpu_ref_fixtures.py against the real reference's outputs.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _lib():
+    from rl2048_amd import _lib as L
+
+    L.ensure_device(DEV)
+    return L
+
+
+def _boards(rng, n, hi=11):
+    e = rng.integers(0, hi + 1, size=(n, 16))
+    e[rng.random((n, 16)) < 0.35] = 0
+    b = (e.astype(np.uint64) << (4 * np.arange(16, dtype=np.uint64))).sum(1)
+    return torch.from_numpy(b.view(np.int64)).to(DEV), e
+
+
+def _obs64(e, mode, scale):
+    if mode == "onehot":
+        x = np.zeros((len(e), 16, 17))
+        np.put_along_axis(x, e[:, :, None], 1.0, axis=2)
+        return torch.from_numpy(x.reshape(len(e), 272)).to(DEV)
+    if mode == "log2":
+        return torch.from_numpy((e * np.float32(scale)).astype(np.float32).astype(np.float64)).to(DEV)
+    return torch.from_numpy(np.where(e > 0, 2.0 ** e, 0.0)).to(DEV)
+
+
+def _net(rng, din, hidden, dout):
+    sizes = [din] + list(hidden) + [dout]
+    W = [torch.from_numpy((rng.standard_normal((a, b)) * np.sqrt(2.0 / a)).astype(np.float32)).to(DEV)
+         for a, b in zip(sizes[:-1], sizes[1:])]
+    B = [torch.from_numpy((rng.standard_normal(b) * 0.1).astype(np.float32)).to(DEV) for b in sizes[1:]]
+    return W, B
+
+
+def _fwd64(W, B, x, act):
+    a = x
+    for i, (w, b) in enumerate(zip(W, B)):
+        z = a @ w.double() + b.double()
+        a = z if i == len(W) - 1 else (torch.relu(z) if act == "ReLU" else torch.sigmoid(z))
+    return a
+
+
+def _pack(L, W, B, obs_code, hidden, dout):
+    lib = L.lib()
+    harr = (ctypes.c_int32 * len(hidden))(*hidden)
+    size = int(lib.g2048_deep_packed_size(obs_code, len(hidden), harr))
+    assert size > 0
+    packed = torch.empty(size, dtype=torch.float32, device=DEV)
+    wp = (ctypes.c_void_p * len(W))(*[w.data_ptr() for w in W])
+    bp = (ctypes.c_void_p * len(B))(*[b.data_ptr() for b in B])
+    L.check(lib.g2048_deep_pack(wp, bp, obs_code, len(hidden), harr, dout, L.ptr(packed), size, L.stream_handle(DEV)))
+    return packed, harr
+
+
+NETS = [("onehot", [256, 128, 64], "ReLU"), ("onehot", [40, 33, 20, 10], "Sigmoid"), ("onehot", [128, 64], "ReLU"),
+        ("log2", [64, 48, 32], "ReLU"), ("raw", [7], "Sigmoid"), ("log2", [256, 256, 256, 256], "ReLU"),
+        ("onehot", [1], "ReLU")]
+
+
+@pytest.mark.parametrize("dout", [4, 1])
+@pytest.mark.parametrize("mode,hidden,act", NETS)
+def test_deep_forward_matches_fp64(mode, hidden, act, dout):
+    L = _lib()
+    code = {"raw": L.OBS_RAW, "log2": L.OBS_LOG2, "onehot": L.OBS_ONEHOT}[mode]
+    rng = np.random.default_rng(len(hidden) * 7 + hidden[0] + dout)
+    din = 272 if mode == "onehot" else 16
+    W, B = _net(rng, din, hidden, dout)
+    packed, harr = _pack(L, W, B, code, hidden, dout)
+    n = 3000 + 17                       # ragged last group; > 2 workgroups per CU of groups on small nets
+    b, e = _boards(rng, n)
+    out = torch.empty(n, 4, dtype=torch.float32, device=DEV)
+    L.check(L.lib().g2048_deep_policy(L.ptr(packed), len(hidden), harr, L.ACT_RELU if act == "ReLU" else L.ACT_SIGMOID,
+                                      L.ptr(b), None, None, code, 0.0625, 0, 1, L.RNG_PCG64, None, None, None, 0, None,
+                                      None, L.ptr(out), None, n, L.stream_handle(DEV)))
+    ref = _fwd64(W, B, _obs64(e, mode, 0.0625), act)
+    got = out[:, :dout].double()
+    # fp32 accumulation: within a few ulps of the sum of magnitudes of the last layer's inputs
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 2e-6, err
+    if dout == 1:
+        assert bool((out[:, 1:] == 0).all())
+
+
+@pytest.mark.parametrize("greedy", [0, 1])
+@pytest.mark.parametrize("compact", [False, True])
+def test_deep_choice_equals_g2048_sample(greedy, compact):
+    """The fused choice == g2048_sample on the kernel's own logits with a copy of the same PCG64 streams."""
+    L = _lib()
+    lib, st = L.lib(), L.stream_handle(DEV)
+    rng = np.random.default_rng(5 + greedy)
+    hidden = [256, 128, 64]
+    W, B = _net(rng, 272, hidden, 4)
+    packed, harr = _pack(L, W, B, L.OBS_ONEHOT, hidden, 4)
+    n = 5000 + 3
+    b, e = _boards(rng, n)
+    seeds = torch.arange(n, dtype=torch.int64, device=DEV) + 777
+    rs = torch.empty(2 * n, dtype=torch.int64, device=DEV)
+    inc = torch.empty(2 * n, dtype=torch.int64, device=DEV)
+    buf = torch.empty(n, dtype=torch.int64, device=DEV)
+    L.check(lib.g2048_seed_pcg64(L.ptr(seeds), L.ptr(rs), L.ptr(inc), L.ptr(buf), n, st))
+    rs2 = rs.clone()
+    idx = torch.from_numpy(np.sort(rng.choice(n, size=n // 3, replace=False)).astype(np.int32)).to(DEV) if compact \
+        else None
+    m = n // 3 if compact else n
+    acts = torch.full((n,), 9, dtype=torch.uint8, device=DEV)
+    probs = torch.zeros(n, 4, dtype=torch.float32, device=DEV)
+    logits = torch.zeros(n, 4, dtype=torch.float32, device=DEV)
+    L.check(lib.g2048_deep_policy(L.ptr(packed), 3, harr, L.ACT_RELU, L.ptr(b), None, L.ptr(idx), L.OBS_ONEHOT, 1.0, 1,
+                                  greedy, L.RNG_PCG64, L.ptr(rs), L.ptr(inc), L.ptr(buf), 0, None, L.ptr(probs),
+                                  L.ptr(logits), L.ptr(acts), m, st))
+    # the same choice from the same logits through g2048_sample (lane state: only the listed lanes active)
+    mask = torch.empty(n, 4, dtype=torch.int8, device=DEV)
+    L.check(lib.g2048_obs(L.ptr(b), L.OBS_NONE, 1.0, None, L.ptr(mask), n, st))
+    ls = torch.zeros(n, dtype=torch.int32, device=DEV)
+    sel = idx.long() if compact else torch.arange(n, device=DEV)
+    ls[sel] = L.LS_ACTIVE
+    acts2 = torch.full((n,), 9, dtype=torch.uint8, device=DEV)
+    probs2 = torch.zeros(n, 4, dtype=torch.float32, device=DEV)
+    L.check(lib.g2048_sample(L.ptr(logits), L.ptr(mask), L.ptr(ls), greedy, L.RNG_PCG64, L.ptr(rs2), L.ptr(inc),
+                             L.ptr(buf), 0, None, L.ptr(probs2), L.ptr(acts2), n, st))
+    assert torch.equal(acts, acts2) and torch.equal(probs, probs2)
+    if not greedy:
+        assert torch.equal(rs, rs2)
+    # untouched lanes stay untouched; probabilities are the masked softmax of the logits
+    if compact:
+        off = torch.ones(n, dtype=torch.bool, device=DEV)
+        off[sel] = False
+        assert bool((acts[off] == 9).all())
+    p_ref = torch.softmax(torch.where(mask[sel].bool(), logits[sel], torch.full_like(logits[sel], -1e9)).double(), 1)
+    assert float((probs[sel].double() - p_ref).abs().max()) < 1e-6
+    ref = _fwd64(W, B, _obs64(e, "onehot", 1.0), "ReLU")[sel]
+    assert float((logits[sel].double() - ref).abs().max() / ref.abs().max()) < 2e-6
+
+
+@pytest.mark.parametrize("h1,act", [(256, "ReLU"), (100, "Sigmoid"), (64, "ReLU"), (1, "ReLU")])
+def test_onehot_layer1_matches_fp64(h1, act):
+    L = _lib()
+    rng = np.random.default_rng(h1)
+    W, B = _net(rng, 272, [h1], 4)
+    n = 7001
+    b, e = _boards(rng, n, hi=15)
+    ld = h1 + 3
+    out = torch.full((n, ld), 7.0, dtype=torch.float32, device=DEV)
+    L.check(L.lib().g2048_onehot_layer1(L.ptr(W[0]), L.ptr(B[0]), h1, L.ACT_RELU if act == "ReLU" else L.ACT_SIGMOID,
+                                        L.ptr(b), n, ld, L.ptr(out), L.stream_handle(DEV)))
+    z = _obs64(e, "onehot", 1.0) @ W[0].double() + B[0].double()
+    ref = torch.relu(z) if act == "ReLU" else torch.sigmoid(z)
+    assert float((out[:, :h1].double() - ref).abs().max() / ref.abs().max()) < 1e-6
+    assert bool((out[:, h1:] == 7.0).all())
+
+
+@pytest.mark.parametrize("h1,m,per", [(256, 20000, 1024), (100, 5000, 777), (64, 3, 1024), (1, 999, 100)])
+def test_onehot_dw1_matches_fp64(h1, m, per):
+    L = _lib()
+    lib, st = L.lib(), L.stream_handle(DEV)
+    rng = np.random.default_rng(h1 + m)
+    b, e = _boards(rng, m, hi=15)
+    d1 = torch.from_numpy(rng.standard_normal((m, h1)).astype(np.float32)).to(DEV)
+    nparts = -(-m // per)
+    slab = int(lib.g2048_onehot_dw1_slab(h1))
+    assert slab == 273 * h1
+    part = torch.empty(nparts, slab, dtype=torch.float32, device=DEV)
+    L.check(lib.g2048_onehot_dw1(L.ptr(b), L.ptr(d1), h1, m, h1, per, L.ptr(part), nparts, st))
+    acc = torch.zeros(slab, dtype=torch.float64, device=DEV)
+    L.check(lib.g2048_fold_partials(L.ptr(part), nparts, slab, L.ptr(acc), st))
+    X = _obs64(e, "onehot", 1.0)
+    ref_w = X.t() @ d1.double()
+    ref_b = d1.double().sum(0)
+    # each slab is an fp32 sequential sum of <= per terms: |error| <= gamma_per * sum |terms| (elementwise)
+    g = per * 2.0 ** -24 / (1 - per * 2.0 ** -24)
+    assert bool(((acc[:272 * h1].view(272, h1) - ref_w).abs() <= g * (X.t() @ d1.double().abs()) + 1e-30).all())
+    assert bool(((acc[272 * h1:] - ref_b).abs() <= g * d1.double().abs().sum(0) + 1e-30).all())
+    # rows of a one-hot feature no sample has are exactly zero
+    seen = torch.zeros(272, dtype=torch.bool, device=DEV)
+    seen[(torch.arange(16, device=DEV) * 17 + torch.from_numpy(e).to(DEV)).reshape(-1)] = True
+    assert bool((acc[:272 * h1].view(272, h1)[~seen] == 0).all())

@@ -386,7 +386,7 @@ def test_philox_mode_distribution():
     from rl2048_amd import Game2048EnvConfig, VecGame2048Env
 
     n = 1 << 16
-    env = VecGame2048Env(n, Game2048EnvConfig(max_steps=None), device=DEV, rng="philox", auto_reset=True)
+    env = VecGame2048Env(n, Game2048EnvConfig(max_steps=1024), device=DEV, rng="philox", auto_reset=True)
     env.reset(seed=11)
     e = env.boards_exponents().reshape(n, 16).cpu().numpy()
     nz = e[e > 0]

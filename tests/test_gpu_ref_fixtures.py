@@ -198,7 +198,7 @@ def _params_before(ci: int, u: int, L: int, which: str):
 ROLLOUT_PATHS = ["rollout", "policy", "gemm"]
 
 
-@pytest.mark.parametrize("ci", range(34))
+@pytest.mark.parametrize("ci", range(RF.N_UPDATE_CASES))
 def test_rollout_matches_reference_run_episode(ci):
     """rollout_batch == the reference's run_episode for each (env_seed, policy_seed) of the fixture, from the
     same parameters: every action (numpy Generator.choice replayed on the device), board, fp64 reward, episode
@@ -284,7 +284,7 @@ def assert_step_matches(got_after, got_before, ref_after, ref_before, grads_ref,
 
 
 @pytest.mark.parametrize("path", ["device", "dropin"])
-@pytest.mark.parametrize("ci", range(34))
+@pytest.mark.parametrize("ci", range(RF.N_UPDATE_CASES))
 def test_update_matches_reference_update_batch(ci, path):
     """update_from_batch (device trajectory buffer: fused gradient kernels where the net fits) and update_batch
     (drop-in, reference trajectory dicts) == src/reinforce_agent.py update_batch, update after update: pre-clip
@@ -426,6 +426,8 @@ def test_runner_matches_reference_training_and_evaluation(tmp_path):
             diff = np.abs(p.cpu().numpy().astype(np.float64) - r)
             assert diff.max() <= 3 * 2 * lr, (j, diff.max())
             rels.append(RF.rel(p.cpu().numpy(), r))
+            # ... and end to end the actor stays pinned near the measured error (<= 5e-7 normwise on MI355X)
+            assert rels[-1] < 1e-4, (j, rels[-1])
         print("\nrunner final actor vs the reference's (normwise per tensor):", rels, "per-update gradient errors:",
               checked)
         for gi, greedy in enumerate((True, False)):
