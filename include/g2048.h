@@ -312,6 +312,41 @@ int g2048_deep_policy(const float* packed, int n_hidden, const int32_t* hidden, 
                       int greedy, int rng_mode, uint64_t* rng_state, const uint64_t* rng_inc, const uint64_t* rng_buf,
                       uint64_t philox_key, const uint64_t* lane_seed, float* probs_out, float* logits_out,
                       uint8_t* actions, int64_t n, void* stream);
+/* Trajectory buffers of a batched rollout: rows are time-major [cap, n] (row t of episode e at t n + e); boards
+ * (pre-step), actions, rewards (fp64, the Python floats run_episode records), flags (G2048_F_*), probs [cap, n, 4]
+ * (NULL ok); per episode: lengths, totals (fp64 running sum in step order), max_tile (log2 of max_tile_seen),
+ * final_board.  Rows at or past an episode's length are not written. */
+typedef struct g2048_traj {
+    uint64_t* boards;
+    uint8_t* actions;
+    double* rewards;
+    uint8_t* flags;
+    float* probs;
+    int32_t* lengths;
+    double* totals;
+    uint8_t* max_tile;
+    uint64_t* final_board;
+} g2048_traj;
+/* Episodes suspended at row cap (g2048_deep_rollout): per episode board, meta {rows so far, step count, max tile
+ * exponent} (3 x uint32), running total; list[0 .. *count) = the suspended episodes (count zero before the call). */
+typedef struct g2048_suspend {
+    uint64_t* board;
+    uint32_t* meta;
+    double* total;
+    int32_t* list;
+    uint32_t* count;
+} g2048_suspend;
+/* g2048_rollout for a packed deep net (any depth, one-hot obs included) and for unbounded episodes: episodes
+ * order[0 .. n_order) (NULL: 0 .. n-1, n_order = n) run to their end inside one persistent launch; one that reaches
+ * row cap without ending (max_steps None, or cap < max_steps) is suspended -- streams written back into env_* /
+ * pol_*, its state into *sus -- and is resumed by a later call with resume = 1, order = the suspended list and the
+ * trajectory buffers grown (same n, larger cap; rows below the old cap kept).  queue: one uint32, zero before each
+ * call. */
+int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden, int activation, const g2048_env_cfg* cfg,
+                       int greedy, uint64_t* env_state, const uint64_t* env_inc, uint64_t* env_buf, uint64_t* pol_state,
+                       const uint64_t* pol_inc, uint64_t* pol_buf, uint32_t* queue, const int32_t* order,
+                       int64_t n_order, int resume, const g2048_suspend* sus, int64_t n, int64_t cap,
+                       const g2048_traj* traj, void* stream);
 /* The update's one-hot first layer: out[s * ld + j] = act(b1[j] + sum_c W1[17 c + e_c(s), j]) for s < m, j < h1
  * (W1 the [272, h1] parameter) -- the kept layer-1 activations of _backpropagation (src/reinforce_agent.py:639-678)
  * without the [m, 272] one-hot obs. */

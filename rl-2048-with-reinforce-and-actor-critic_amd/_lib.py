@@ -127,6 +127,15 @@ class StepOut(ctypes.Structure):
                                                          "reward64", "score_add", "mask_bits")]
 
 
+class Traj(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in ("boards", "actions", "rewards", "flags", "probs", "lengths",
+                                                     "totals", "max_tile", "final_board")]
+
+
+class Suspend(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in ("board", "meta", "total", "list", "count")]
+
+
 _lib = None
 _lock = threading.RLock()
 _inited_devices: set[int] = set()
@@ -170,6 +179,8 @@ def _declare(L):
     L.g2048_deep_pack.argtypes = [vp, vp, i32, i32, vp, i32, vp, i64, vp]
     L.g2048_deep_policy.argtypes = [vp, i32, vp, i32, vp, vp, vp, i32, f, i32, i32, i32, vp, vp, vp, u64, vp, vp, vp,
                                     vp, i64, vp]
+    L.g2048_deep_rollout.argtypes = [vp, i32, vp, i32, P(EnvCfg), i32, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32,
+                                     P(Suspend), i64, i64, P(Traj), vp]
     L.g2048_onehot_layer1.argtypes = [vp, vp, i32, i32, vp, i64, i64, vp, vp]
     L.g2048_onehot_dw1_slab.argtypes = [i32]
     L.g2048_onehot_dw1_slab.restype = i64
@@ -178,7 +189,7 @@ def _declare(L):
                  "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy",
                  "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad",
                  "g2048_dw2", "g2048_fold_partials", "g2048_dw2_factored", "g2048_deep_pack", "g2048_deep_policy",
-                 "g2048_onehot_layer1", "g2048_onehot_dw1"):
+                 "g2048_deep_rollout", "g2048_onehot_layer1", "g2048_onehot_dw1"):
         getattr(L, name).restype = ctypes.c_int
 
 
@@ -188,7 +199,7 @@ EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g204
                     "g2048_grad_packed_size", "g2048_grad_partial_size", "g2048_grad_pack", "g2048_actor_grad_waves",
                     "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2", "g2048_fold_partials",
                     "g2048_dw2_factored", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
-                    "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1")
+                    "g2048_deep_rollout", "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1")
 
 
 def lib():

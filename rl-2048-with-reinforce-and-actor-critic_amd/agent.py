@@ -871,7 +871,12 @@ class ReinforceAgent:
         if spec is not None and rng == "pcg64" and self.env_config.max_steps is not None and self.use_fused_rollout:
             self._paths["rollout"] = "g2048_rollout (one persistent launch)"
             return self._rollout_fused(env_seeds, policy_seeds, spec, use_greedy, record_probs)
-        dspec = self._deep_spec() if spec is None and self.use_fused_policy else None
+        dspec = self._deep_spec() if self.use_fused_policy else None
+        if dspec is not None and rng == "pcg64" and self.use_fused_rollout:
+            self._paths["rollout"] = "g2048_deep_rollout (persistent launches, suspended episodes resumed)"
+            return self._rollout_deep(env_seeds, policy_seeds, dspec, use_greedy, record_probs)
+        if spec is not None:
+            dspec = None
         self._paths["rollout"] = ("g2048_policy + g2048_step per step (active lanes)" if spec is not None else
                                   "g2048_deep_policy + g2048_step per step (active lanes)" if dspec is not None else
                                   "hipBLASLt forward (active lanes) + g2048_sample + g2048_step per step")
@@ -996,6 +1001,75 @@ class ReinforceAgent:
                                         L.ptr(actions), L.ptr(rewards), L.ptr(flags),
                                         L.ptr(probs) if probs is not None else None, L.ptr(lengths), L.ptr(totals),
                                         L.ptr(max_e), L.ptr(final), self._stream))
+        T = int(lengths.max().item()) if n else 0
+        return TrajectoryBatch(boards=boards[:T], actions=actions[:T], rewards=rewards[:T], flags=flags[:T],
+                               lengths=lengths, total_reward=totals,
+                               max_tile=torch.ones(n, dtype=torch.int64, device=dev) << max_e.to(torch.int64),
+                               final_boards=final, probs=probs[:T] if probs is not None else None)
+
+    # first trajectory capacity of g2048_deep_rollout when max_steps is None (doubled while episodes run past it)
+    deep_rollout_cap0 = 512
+
+    def _rollout_deep(self, env_seeds, policy_seeds, dspec, use_greedy: bool, record_probs: bool) -> TrajectoryBatch:
+        """rollout_batch through g2048_deep_rollout (any depth, one-hot obs, max_steps None): every episode runs
+        inside a persistent launch until it ends or fills the trajectory buffer's `cap` rows; the episodes that
+        filled it are suspended by the kernel, the buffer grows (x2) and one more launch resumes just those."""
+        from .config import env_cfg_struct
+        from .vec_env import _as_u64_seeds
+
+        n = len(env_seeds)
+        dev = self.device
+        es = _as_u64_seeds(_seed_seq(env_seeds), n, 0, dev)
+        ps = _as_u64_seeds(_seed_seq(policy_seeds), n, 0, dev)
+        streams = []
+        for seeds in (es, ps):
+            st = torch.empty(2 * n, dtype=torch.int64, device=dev)
+            inc = torch.empty(2 * n, dtype=torch.int64, device=dev)
+            buf = torch.empty(n, dtype=torch.int64, device=dev)
+            L.check(self._lib.g2048_seed_pcg64(L.ptr(seeds), L.ptr(st), L.ptr(inc), L.ptr(buf), n, self._stream))
+            streams += [st, inc, buf]
+        ms = self.env_config.max_steps
+        cap = max(int(ms) if ms is not None else self.deep_rollout_cap0, 1)
+        boards = torch.empty(cap, n, dtype=torch.int64, device=dev)
+        actions = torch.zeros(cap, n, dtype=torch.uint8, device=dev)
+        rewards = torch.zeros(cap, n, dtype=torch.float64, device=dev)
+        flags = torch.full((cap, n), L.F_INACTIVE, dtype=torch.uint8, device=dev)
+        probs = torch.zeros(cap, n, 4, dtype=torch.float32, device=dev) if record_probs else None
+        lengths = torch.empty(n, dtype=torch.int32, device=dev)
+        totals = torch.empty(n, dtype=torch.float64, device=dev)
+        max_e = torch.empty(n, dtype=torch.uint8, device=dev)
+        final = torch.empty(n, dtype=torch.int64, device=dev)
+        sus_board = torch.empty(n, dtype=torch.int64, device=dev)
+        sus_meta = torch.empty(3 * n, dtype=torch.int32, device=dev)
+        sus_total = torch.empty(n, dtype=torch.float64, device=dev)
+        sus_list = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        sus_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        sus = L.Suspend(*[L.ptr(t) for t in (sus_board, sus_meta, sus_total, sus_list, sus_count)])
+        queue = torch.zeros(1, dtype=torch.int32, device=dev)
+        cfg = env_cfg_struct(self.env_config)
+        packed = self._pack_deep(self.params, dspec, "actor", 4)
+        obs_code, hidden, act, harr = dspec
+        order, n_order, resume = None, n, 0
+        while True:
+            traj = L.Traj(*[L.ptr(t) for t in (boards, actions, rewards, flags, probs, lengths, totals, max_e, final)])
+            L.check(self._lib.g2048_deep_rollout(L.ptr(packed), len(hidden), harr, act, ctypes.byref(cfg),
+                                                 int(use_greedy), *[L.ptr(t) for t in streams], L.ptr(queue),
+                                                 L.ptr(order), n_order, resume, ctypes.byref(sus), n, cap,
+                                                 ctypes.byref(traj), self._stream))
+            k = int(sus_count.item())          # one host sync per launch
+            if k == 0:
+                break
+            order, n_order, resume = sus_list[:k].clone(), k, 1
+            queue.zero_()
+            sus_count.zero_()
+            grow = cap
+            boards = torch.cat([boards, torch.empty(grow, n, dtype=torch.int64, device=dev)])
+            actions = torch.cat([actions, torch.zeros(grow, n, dtype=torch.uint8, device=dev)])
+            rewards = torch.cat([rewards, torch.zeros(grow, n, dtype=torch.float64, device=dev)])
+            flags = torch.cat([flags, torch.full((grow, n), L.F_INACTIVE, dtype=torch.uint8, device=dev)])
+            if probs is not None:
+                probs = torch.cat([probs, torch.zeros(grow, n, 4, dtype=torch.float32, device=dev)])
+            cap += grow
         T = int(lengths.max().item()) if n else 0
         return TrajectoryBatch(boards=boards[:T], actions=actions[:T], rewards=rewards[:T], flags=flags[:T],
                                lengths=lengths, total_reward=totals,

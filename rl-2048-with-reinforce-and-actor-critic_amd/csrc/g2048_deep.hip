@@ -362,6 +362,162 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_policy_kernel(DeepPolArgs 
     }
 }
 
+// ------------------------------------------------------------------------------------ rollout
+// The whole batched rollout (ReinforceAgent.run_episode, src/reinforce_agent.py:195-252, for n (env_seed,
+// policy_seed) pairs) for a net of any depth / one-hot obs, in one persistent launch: a workgroup runs 32 episode
+// slots, every step is deep_forward over the 32 slots' boards, then the slot owners (lanes 0..31 of wave 0) choose
+// (softmax_select on the slot's policy stream), step the env in registers (env_step_pcg, row tables through L1/L2)
+// and write the trajectory row; a finished slot takes the next episode from the queue.  Unbounded episodes
+// (max_steps None, src/env.py:289-296): an episode that reaches row `cap` without ending is SUSPENDED -- its board,
+// counters, running total and both streams are written back per episode and the episode is listed -- and the host
+// grows the trajectory buffer and resumes the listed episodes (resume = 1) from row cap on.
+struct GLine {
+    const uint16_t* p;
+    __device__ uint32_t operator()(uint32_t o) const { return p[o]; }
+};
+struct GCode {
+    const uint8_t* p;
+    __device__ uint32_t operator()(uint32_t o) const { return (p[o >> 1] >> ((o & 1u) << 2)) & 15u; }
+};
+
+struct DeepRollArgs {
+    DeepNet net;
+    const float* packed;
+    const uint8_t* tab;
+    RewardCfg rc;
+    int64_t max_steps;
+    float obs_scale;
+    int use_mask, greedy;
+    uint64_t* env_rs;
+    const uint64_t* env_inc;
+    uint64_t* env_buf;
+    uint64_t* pol_rs;
+    const uint64_t* pol_inc;
+    uint64_t* pol_buf;
+    uint32_t* next;
+    const int32_t* order;
+    uint32_t n_order;
+    int resume;
+    g2048_suspend sus;
+    g2048_traj tr;
+    uint32_t n, cap;
+};
+
+__device__ __forceinline__ Pcg64 load_stream(const uint64_t* rs, const uint64_t* inc, const uint64_t* buf, uint32_t e) {
+    Pcg64 g;
+    const ulonglong2 s = reinterpret_cast<const ulonglong2*>(rs)[e];
+    const ulonglong2 c = reinterpret_cast<const ulonglong2*>(inc)[e];
+    const uint64_t bf = buf[e];
+    g.s_lo = s.x;
+    g.s_hi = s.y;
+    g.i_lo = c.x;
+    g.i_hi = c.y;
+    g.has_uint32 = (uint32_t)(bf >> 32);
+    g.uinteger = (uint32_t)bf;
+    return g;
+}
+
+__device__ __forceinline__ void store_stream(uint64_t* rs, uint64_t* buf, uint32_t e, const Pcg64& g) {
+    reinterpret_cast<ulonglong2*>(rs)[e] = make_ulonglong2(g.s_lo, g.s_hi);
+    buf[e] = ((uint64_t)g.has_uint32 << 32) | g.uinteger;
+}
+
+constexpr uint32_t kNoEpisode = 0xFFFFFFFFu;
+
+template <int OBS, int ACT>
+__global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArgs a) {
+    __shared__ DeepSmem S;
+    __shared__ int go;
+    const int tid = threadIdx.x;
+    const bool owner = tid < 32;
+    const GLine lut{reinterpret_cast<const uint16_t*>(a.tab)};
+    const GCode code{a.tab + 2 * 65536};
+    uint32_t ep = kNoEpisode, t = 0, sc = 0, mt = 2;
+    uint64_t b = 0;
+    double total = 0.0;
+    Pcg64 ge{}, gp{};
+    bool drained = false;                              // wave-0-uniform: the queue is empty (claims only grow)
+    const auto start = [&](uint32_t e) {
+        ep = e;
+        ge = load_stream(a.env_rs, a.env_inc, a.env_buf, e);
+        gp = load_stream(a.pol_rs, a.pol_inc, a.pol_buf, e);
+        if (a.resume) {
+            b = a.sus.board[e];
+            t = a.sus.meta[3 * (size_t)e];
+            sc = a.sus.meta[3 * (size_t)e + 1];
+            mt = a.sus.meta[3 * (size_t)e + 2];
+            total = a.sus.total[e];
+        } else {
+            b = spawn_pcg(spawn_pcg(0ull, ge), ge);    // Game2048.reset (src/game2048.py:26-34)
+            t = 0;
+            sc = 0;
+            mt = 2;                                   // max_tile_seen = 4 (src/env.py:188)
+            total = 0.0;
+        }
+    };
+    const auto claim = [&]() {                         // wave 0 only
+        if (drained) return;
+        const bool need = owner && ep == kNoEpisode;
+        const uint64_t bal = __ballot(need);
+        if (!bal) return;
+        const int leader = __builtin_ctzll(bal);
+        uint32_t base = 0;
+        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(a.next, (uint32_t)__popcll(bal));
+        base = (uint32_t)__shfl((int)base, leader, 64);
+        const uint32_t idx =
+            base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (need && idx < a.n_order) start(a.order ? (uint32_t)a.order[idx] : idx);
+        drained = __ballot(need && idx >= a.n_order) != 0ull;
+    };
+    if (tid < 64) claim();
+    while (true) {
+        if (tid < 64) {
+            const uint64_t live = __ballot(owner && ep != kNoEpisode);
+            if (tid == 0) go = live != 0ull;
+            if (owner) S.board[tid] = ep != kNoEpisode ? b : 0ull;
+        }
+        __syncthreads();
+        if (!go) break;                                // block-uniform
+        deep_forward<OBS, ACT>(a.net, a.packed, S, a.obs_scale);
+        if (owner && ep != kNoEpisode) {
+            float lg[4];
+            deep_logits(a.net, a.packed, S, tid, lg);
+            const uint32_t mw = a.use_mask ? mask_word_of(b) : 0x01010101u;
+            const double u = a.greedy ? 0.0 : pcg_random(gp);
+            float p[4];
+            const uint32_t act = softmax_select(lg, mw, a.use_mask != 0, a.greedy != 0, u, p);
+            const StepValues ov = env_step_pcg(b, act, sc, mt, ge, a.rc, a.max_steps, lut, code);
+            const size_t row = (size_t)t * a.n + ep;
+            a.tr.boards[row] = b;
+            a.tr.actions[row] = (uint8_t)act;
+            a.tr.rewards[row] = ov.reward;
+            a.tr.flags[row] = (uint8_t)ov.flags;
+            if (a.tr.probs) reinterpret_cast<float4*>(a.tr.probs)[row] = make_float4(p[0], p[1], p[2], p[3]);
+            total += ov.reward;                        // total_reward += float(reward) (src/reinforce_agent.py:233)
+            b = ov.board;
+            t += 1;
+            if ((ov.flags & (kFTerminated | kFTruncated)) != 0u) {
+                a.tr.lengths[ep] = (int32_t)t;
+                a.tr.totals[ep] = total;
+                a.tr.max_tile[ep] = (uint8_t)mt;
+                a.tr.final_board[ep] = b;
+                ep = kNoEpisode;
+            } else if (t >= a.cap) {                   // out of trajectory rows: suspend for the host to resume
+                store_stream(a.env_rs, a.env_buf, ep, ge);
+                store_stream(a.pol_rs, a.pol_buf, ep, gp);
+                a.sus.board[ep] = b;
+                a.sus.meta[3 * (size_t)ep] = t;
+                a.sus.meta[3 * (size_t)ep + 1] = sc;
+                a.sus.meta[3 * (size_t)ep + 2] = mt;
+                a.sus.total[ep] = total;
+                a.sus.list[atomicAdd(a.sus.count, 1u)] = (int32_t)ep;
+                ep = kNoEpisode;
+            }
+        }
+        if (tid < 64) claim();
+    }
+}
+
 // ------------------------------------------------------------------------------------ one-hot layer 1 (update)
 // a1[s][j] = act(b1[j] + sum_c W1[17 c + e_c(s)][j]) for samples s < m, units j < h1: one wave per sample (lanes =
 // units, 64 at a time), rows read coalesced from the unpadded [272][h1] weight (the torch parameter itself).
@@ -454,6 +610,9 @@ void launch_deep_act(const DeepPolArgs& a, int act, int rng, int grid, hipStream
 
 namespace g2048_internal {   // g2048.hip
 int set_error(int code, const char* msg);
+int device_tables(const uint8_t*& tab, int& cus);
+int check_env_cfg(const g2048_env_cfg* c);
+g2048::RewardCfg reward_cfg_of(const g2048_env_cfg& c);
 }  // namespace g2048_internal
 
 namespace {
@@ -542,6 +701,70 @@ int g2048_deep_policy(const float* packed, int n_hidden, const int32_t* hidden, 
     if (obs_mode == G2048_OBS_ONEHOT) launch_deep_act<G2048_OBS_ONEHOT>(a, activation, rng_mode, grid, s);
     else if (obs_mode == G2048_OBS_LOG2) launch_deep_act<G2048_OBS_LOG2>(a, activation, rng_mode, grid, s);
     else launch_deep_act<G2048_OBS_RAW>(a, activation, rng_mode, grid, s);
+    return check_hip();
+}
+
+int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden, int activation, const g2048_env_cfg* cfg,
+                       int greedy, uint64_t* env_state, const uint64_t* env_inc, uint64_t* env_buf, uint64_t* pol_state,
+                       const uint64_t* pol_inc, uint64_t* pol_buf, uint32_t* queue, const int32_t* order,
+                       int64_t n_order, int resume, const g2048_suspend* sus, int64_t n, int64_t cap,
+                       const g2048_traj* traj, void* stream) {
+    int rc = g2048_internal::check_env_cfg(cfg);
+    if (rc) return rc;
+    if (n < 0 || n > (int64_t)0x7FFFFFFF) return dfail(G2048_EINVAL, "n out of range");
+    if (n_order < 0 || n_order > n || (!order && n_order != n) || (resume && !order))
+        return dfail(G2048_EINVAL, "deep rollout: order must list n_order <= n episodes (all n when NULL; resume needs a list)");
+    if (cap < 1 || cap > (int64_t)0x7FFFFFFF || n * cap > ((int64_t)1 << 40)) return dfail(G2048_EINVAL, "deep rollout: bad cap");
+    DeepNet net;
+    if (!deep_layout(n_hidden, hidden, cfg->obs_mode == G2048_OBS_ONEHOT, net))
+        return dfail(G2048_EINVAL, "deep policy: 1..4 hidden layers of 1..256 units");
+    if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
+        return dfail(G2048_EINVAL, "Unsupported activation");
+    if (!packed || !env_state || !env_inc || !env_buf || !pol_state || !pol_inc || !pol_buf || !queue || !sus || !traj ||
+        !sus->board || !sus->meta || !sus->total || !sus->list || !sus->count || !traj->boards || !traj->actions ||
+        !traj->rewards || !traj->flags || !traj->lengths || !traj->totals || !traj->max_tile || !traj->final_board)
+        return dfail(G2048_EINVAL, "deep rollout: a required buffer is NULL");
+    if (n_order == 0) return G2048_OK;
+    const uint8_t* tab = nullptr;
+    int cus = 256;
+    if ((rc = g2048_internal::device_tables(tab, cus))) return rc;
+    DeepRollArgs a;
+    a.net = net;
+    a.packed = packed;
+    a.tab = tab;
+    a.rc = g2048_internal::reward_cfg_of(*cfg);
+    a.max_steps = cfg->max_steps;
+    a.obs_scale = cfg->obs_log2_scale;
+    a.use_mask = cfg->use_action_mask;
+    a.greedy = greedy;
+    a.env_rs = env_state;
+    a.env_inc = env_inc;
+    a.env_buf = env_buf;
+    a.pol_rs = pol_state;
+    a.pol_inc = pol_inc;
+    a.pol_buf = pol_buf;
+    a.next = queue;
+    a.order = order;
+    a.n_order = (uint32_t)n_order;
+    a.resume = resume;
+    a.sus = *sus;
+    a.tr = *traj;
+    a.n = (uint32_t)n;
+    a.cap = (uint32_t)cap;
+    int64_t grid = (n_order + 31) / 32;
+    if (grid > 2 * (int64_t)cus) grid = 2 * (int64_t)cus;   // persistent; the slots refill from the queue
+    hipStream_t s = (hipStream_t)stream;
+    const int obs = cfg->obs_mode;
+    if (obs == G2048_OBS_ONEHOT) {
+        if (activation == G2048_ACT_RELU) hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_ONEHOT, 0>), dim3(grid), dim3(kDeepBlock), 0, s, a);
+        else hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_ONEHOT, 1>), dim3(grid), dim3(kDeepBlock), 0, s, a);
+    } else if (obs == G2048_OBS_LOG2) {
+        if (activation == G2048_ACT_RELU) hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_LOG2, 0>), dim3(grid), dim3(kDeepBlock), 0, s, a);
+        else hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_LOG2, 1>), dim3(grid), dim3(kDeepBlock), 0, s, a);
+    } else {
+        if (activation == G2048_ACT_RELU) hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_RAW, 0>), dim3(grid), dim3(kDeepBlock), 0, s, a);
+        else hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_RAW, 1>), dim3(grid), dim3(kDeepBlock), 0, s, a);
+    }
     return check_hip();
 }
 

@@ -195,3 +195,66 @@ def test_onehot_dw1_matches_fp64(h1, m, per):
     seen = torch.zeros(272, dtype=torch.bool, device=DEV)
     seen[(torch.arange(16, device=DEV) * 17 + torch.from_numpy(e).to(DEV)).reshape(-1)] = True
     assert bool((acc[:272 * h1].view(272, h1)[~seen] == 0).all())
+
+
+REFCONF_ENV = dict(obs_mode="onehot", obs_log2_scale=1.0, reward_mode="log2", base_reward_scale=1.0,
+                   use_action_mask=True, invalid_action_penalty=-1.0, max_steps=None, empty_tile_reward=0.05)
+
+
+def _agent(env: dict, hidden, act="ReLU", **acfg):
+    from rl2048_amd import Game2048EnvConfig
+    from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig
+    from rl2048_amd.mlp import MLPConfig
+
+    return ReinforceAgent(Game2048EnvConfig(**env), MLPConfig(hidden_sizes=hidden, activation=act,
+                                                              init_distribution="HeNormal"),
+                          ReinforceAgentConfig(**acfg), device=DEV)
+
+
+@pytest.mark.parametrize("env,hidden", [(REFCONF_ENV, [256, 128, 64]),
+                                        (dict(obs_mode="log2", obs_log2_scale=0.0625, max_steps=None), [256, 256]),
+                                        (dict(REFCONF_ENV, max_steps=70), [40, 33, 20, 10])])
+def test_deep_rollout_suspend_resume_equals_stepwise(env, hidden):
+    """g2048_deep_rollout with a tiny first capacity (every episode is suspended and resumed several times as the
+    buffer doubles) == the per-step path (g2048_deep_policy + g2048_step) on the same seeds: every board, action,
+    fp64 reward, flag, probability, length, total, max tile and final board; sampled episodes replayed in the oracle
+    (env + numpy Generator.choice on the recorded probabilities)."""
+    from oracle import oracle as O
+    from rl2048_amd import _lib as L
+
+    n = 3001
+    es = np.arange(50_000, 50_000 + n, dtype=np.int64)
+    ps = es + 10 ** 9
+    a = _agent(env, hidden)
+    a.deep_rollout_cap0 = 8
+    b1 = a.rollout_batch(es, ps, record_probs=True)
+    assert a.last_paths()["rollout"].startswith("g2048_deep_rollout")
+    a.use_fused_rollout = False
+    b2 = a.rollout_batch(es, ps, record_probs=True)
+    assert "g2048_deep_policy" in a.last_paths()["rollout"] or "g2048_policy" in a.last_paths()["rollout"]
+    assert b1.T == b2.T and b1.T > 8
+    assert torch.equal(b1.lengths, b2.lengths)
+    valid = torch.arange(b1.T, device=DEV).unsqueeze(1) < b1.lengths.unsqueeze(0)
+    for name in ("boards", "actions", "rewards"):
+        x, y = getattr(b1, name), getattr(b2, name)
+        assert torch.equal(x[valid], y[valid]), name
+    assert torch.equal((b1.flags & ~L.F_INACTIVE)[valid], (b2.flags & ~L.F_INACTIVE)[valid])
+    assert torch.equal(b1.probs[valid], b2.probs[valid])
+    assert torch.equal(b1.total_reward, b2.total_reward) and torch.equal(b1.max_tile, b2.max_tile)
+    assert torch.equal(b1.final_boards, b2.final_boards)
+    ocfg = {k: v for k, v in env.items()}
+    lens = b1.lengths.cpu().numpy()
+    for i in [0, 1, n // 2, n - 1] + list(np.random.default_rng(0).choice(n, 20, replace=False)):
+        e, pol = O.Env(**ocfg), O.PCG64(int(ps[i]))
+        e.reset(int(es[i]))
+        total = 0.0
+        bb, aa = b1.boards[:, i].cpu().numpy().view(np.uint64), b1.actions[:, i].cpu().numpy()
+        rr, pp = b1.rewards[:, i].cpu().numpy(), b1.probs[:, i].cpu().numpy()
+        for t in range(int(lens[i])):
+            assert bb[t] == O.pack_exponents(O.values_to_exponents(e.board)), (i, t)
+            assert pol.choice4(pp[t]) == aa[t], (i, t)
+            r = e.step(int(aa[t]))
+            assert rr[t] == r["reward"], (i, t)
+            total += r["reward"]
+            assert (r["terminated"] or r["truncated"]) == (t == lens[i] - 1), (i, t)
+        assert float(b1.total_reward[i]) == total
