@@ -234,9 +234,13 @@ int64_t g2048_grad_partial_size(int h1, int h2);
 /* Pack W2 [h1 x h2] (src/MLP.py layout) for the input-delta product; re-pack after every update. */
 int g2048_grad_pack(const float* W2, int h1, int h2, float* packed, int64_t packed_len, void* stream);
 int g2048_actor_grad_waves(void);
+/* d2_form 2 (ReLU actor): instead of d2 columns, d2t receives one 1 KiB record per 16-column block c: bytes
+ * [0, 2 H2p) the mask words as for the critic's d2_form 1, bytes [512, 768) the 4 values of g (the logit gradient)
+ * of each of the block's 16 columns (float4 per column); g2048_dw2_actor rebuilds d2 from it bit for bit. */
 int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
                      float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions, const float* coef,
-                     int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, void* stream);
+                     int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, int d2_form,
+                     void* stream);
 /* The critic branch of update_batch (src/reinforce_agent.py:403-498, _get_grad_logits_critic :884-910) on the same
  * kernel: the critic packed like the actor with its value head [h2 x 1] / [1] as output 0 of a 4-wide layer (outputs
  * 1..3 zero); per sample the value V(s), the TD error delta_out = target - V (target = r + gamma V(s') m from the
@@ -273,6 +277,12 @@ int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int64_t ld, in
 int g2048_dw2_factored(const float* a1t, const float* records, const float* w3, int h1, int h2, int64_t ld,
                        int64_t col0, int64_t ncols, int64_t cols_per_part, float* partials, int64_t nparts,
                        void* stream);
+/* g2048_dw2 for the ReLU actor's records (g2048_actor_grad d2_form 2): d2 of column k, unit j is rebuilt as
+ * fl(fl(fl(fl(g0 W3[j,0]) + g1 W3[j,1]) + g2 W3[j,2]) + g3 W3[j,3]) (fused multiply-adds) times the mask bit --
+ * bit for bit the d2 g2048_actor_grad computes -- then summed as g2048_dw2 sums d2 columns; w3 = W3 [H2p][4]
+ * zero-padded (64 B per sample read instead of 1 KiB). */
+int g2048_dw2_actor(const float* a1t, const float* records, const float* w3, int h1, int h2, int64_t ld, int64_t col0,
+                    int64_t ncols, int64_t cols_per_part, float* partials, int64_t nparts, void* stream);
 /* acc[i] += sum over p < nparts of partials[p * slab + i] (i < slab), the sum taken in fp64 in a fixed order: folds
  * g2048_dw2's slabs (slab = (H1p + 1) H2p) or any per-wave fp32 partials into an fp64 accumulator on the device
  * (the fp64 chunk sums of update_from_batch; no fp32 -> fp64 conversion pass). */

@@ -168,12 +168,13 @@ def _declare(L):
     L.g2048_grad_partial_size.restype = i64
     L.g2048_grad_pack.argtypes = [vp, i32, i32, vp, i64, vp]
     L.g2048_actor_grad_waves.argtypes = []
-    L.g2048_actor_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, vp, vp, vp, i64, i64, vp, vp, vp, i64, vp]
+    L.g2048_actor_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, vp, vp, vp, i64, i64, vp, vp, vp, i64, i32, vp]
     L.g2048_critic_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, f, vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, vp,
                                     vp, i32, i64, i32, vp]
     L.g2048_dw2.argtypes = [vp, vp, i32, i32, i64, i64, i64, i64, vp, i64, vp]
     L.g2048_fold_partials.argtypes = [vp, i64, i64, vp, vp]
     L.g2048_dw2_factored.argtypes = [vp, vp, vp, i32, i32, i64, i64, i64, i64, vp, i64, vp]
+    L.g2048_dw2_actor.argtypes = [vp, vp, vp, i32, i32, i64, i64, i64, i64, vp, i64, vp]
     L.g2048_deep_packed_size.argtypes = [i32, i32, vp]
     L.g2048_deep_packed_size.restype = i64
     L.g2048_deep_pack.argtypes = [vp, vp, i32, i32, vp, i32, vp, i64, vp]
@@ -188,7 +189,7 @@ def _declare(L):
     for name in ("g2048_init", "g2048_seed_pcg64", "g2048_reset", "g2048_step", "g2048_obs", "g2048_move",
                  "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy",
                  "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad",
-                 "g2048_dw2", "g2048_fold_partials", "g2048_dw2_factored", "g2048_deep_pack", "g2048_deep_policy",
+                 "g2048_dw2", "g2048_fold_partials", "g2048_dw2_factored", "g2048_dw2_actor", "g2048_deep_pack", "g2048_deep_policy",
                  "g2048_deep_rollout", "g2048_onehot_layer1", "g2048_onehot_dw1"):
         getattr(L, name).restype = ctypes.c_int
 
@@ -198,7 +199,7 @@ EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g204
                     "g2048_policy_packed_size", "g2048_policy_pack", "g2048_policy", "g2048_rollout",
                     "g2048_grad_packed_size", "g2048_grad_partial_size", "g2048_grad_pack", "g2048_actor_grad_waves",
                     "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2", "g2048_fold_partials",
-                    "g2048_dw2_factored", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
+                    "g2048_dw2_factored", "g2048_dw2_actor", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
                     "g2048_deep_rollout", "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1")
 
 

@@ -119,6 +119,23 @@ def _unrecord(rec: torch.Tensor, w3: torch.Tensor, c0: int, m: int) -> torch.Ten
     return ((g[cols][:, None] * w3[None, :]) * bits.to(torch.float32)).t()
 
 
+def _unrecord_actor(rec: torch.Tensor, w3: torch.Tensor, c0: int, m: int) -> torch.Tensor:
+    """The d2 columns [c0, c0 + m) that the actor's block records (g2048_actor_grad d2_form 2) stand for, [H2p, m]:
+    fl(fl(fl(fl(g0 W3[j,0]) + g1 W3[j,1]) + g2 W3[j,2]) + g3 W3[j,3]) where unit j's mask bit is set (w3: [H2p, 4])."""
+    H2p = w3.shape[0]
+    blocks = rec.view(-1, 256)
+    words = blocks.view(torch.int16).view(-1, 512)[:, :H2p].to(torch.int32) & 0xFFFF   # [blocks, H2p]
+    g = blocks[:, 128:192].reshape(-1, 4)                                                # [blocks * 16, 4]
+    cols = torch.arange(c0, c0 + m, device=rec.device)
+    bits = (words[cols >> 4] >> (cols & 15)[:, None]) & 1                                 # [m, H2p]
+    gc = g[cols]
+    # the kernel's operation order, one rounding per step (fmaf = one rounding: evaluated in fp64, then rounded)
+    dh = (gc[:, 0:1] * w3[None, :, 0])
+    for k in (1, 2, 3):
+        dh = (gc[:, k:k + 1].double() * w3[None, :, k].double() + dh.double()).to(torch.float32)
+    return (dh * bits.to(torch.float32)).t()
+
+
 def _unblock(buf: torch.Tensor, rows: int, c0: int, m: int) -> torch.Tensor:
     """Rows [0, rows) x columns [c0, c0 + m) of a column buffer stored in 16-column blocks (include/g2048.h) as a
     row-major copy (diagnostics: ReinforceAgent.grad_probe)."""
@@ -247,6 +264,7 @@ class ReinforceAgent:
         # ... and the fused critic per time row, V(s') taken from the next row's pass (large batches)
         self.use_critic_rows = True
         self.critic_factored_d2 = True   # ReLU critic rows: the factored d2 records + g2048_dw2_factored
+        self.actor_d2_records = True     # ReLU actor: d2 block records (mask + g) + g2048_dw2_actor
         self.grad_chunk_steps = 1 << 20
         # diagnostics (tests): called as grad_probe(slot, k, sample_idx, a1_cols, d2_cols) with the column buffers
         # of every fused-gradient launch before they are reused -- sample_idx indexes the batch's valid steps
@@ -588,6 +606,22 @@ class ReinforceAgent:
                                              cpp, L.ptr(part), nparts, self._stream))
         self._fold(part, acc)
 
+    def _dw2_actor(self, a1t: torch.Tensor, rec: torch.Tensor, w3: torch.Tensor, h1: int, h2: int, ncols: int,
+                   acc: torch.Tensor) -> None:
+        """_dw2 for the ReLU actor's d2 block records (g2048_actor_grad d2_form 2): g2048_dw2_actor rebuilds d2 from
+        the mask words and g with W3 (w3: [H2p, 4] padded) bit for bit, then sums as g2048_dw2."""
+        H1p, H2p = _padded_units(h1), _padded_units(h2)
+        if ncols == 0:
+            return
+        assert rec.numel() * 4 >= (ncols // 16) * 1024 and tuple(w3.shape) == (H2p, 4) and acc.shape == (H1p + 1, H2p)
+        cus = int(self._lib.g2048_actor_grad_waves()) // 4
+        cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * cus)) * 16)
+        nparts = -(-ncols // cpp)
+        part = torch.empty(nparts, H1p + 1, H2p, dtype=torch.float32, device=self.device)
+        L.check(self._lib.g2048_dw2_actor(L.ptr(a1t), L.ptr(rec), L.ptr(w3), h1, h2, int(a1t.shape[1]), 0, ncols, cpp,
+                                          L.ptr(part), nparts, self._stream))
+        self._fold(part, acc)
+
     def _actor_grad_fused(self, steps: "_Steps", adv: torch.Tensor, step_w: torch.Tensor, K: int,
                           gW: list[torch.Tensor], gb: list[torch.Tensor], spec) -> None:
         """The actor branch of update_batch (src/reinforce_agent.py:502-555) for every valid step and symmetry k:
@@ -595,15 +629,16 @@ class ReinforceAgent:
         plus g2048_dw2 for the layer-2 weight and bias gradient over the a1^T / d2^T columns the kernel writes.
         Accumulates into gW / gb like mlp_backward_."""
         use_mask = int(bool(self.env_config.use_action_mask))
+        records = spec[2] == L.ACT_RELU and self.actor_d2_records
 
         def launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale):
             a = steps.actions_k(sel, k).to(torch.uint8).contiguous()
             coef = (adv[k, sel] * step_w[sel]).contiguous()
             L.check(self._lib.g2048_actor_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, use_mask,
                                                L.ptr(b), L.ptr(a), L.ptr(coef), m, ld, L.ptr(a1t), L.ptr(d2t),
-                                               L.ptr(part), waves, self._stream))
+                                               L.ptr(part), waves, 2 if records else 0, self._stream))
 
-        self._fused_grad(self.params, "actor", spec, steps, K, gW, gb, 4, launch)
+        self._fused_grad(self.params, "actor", spec, steps, K, gW, gb, 4, launch, records=records)
 
     def _critic_grad_fused(self, steps: "_Steps", step_w: torch.Tensor, K: int, gW: list[torch.Tensor],
                            gb: list[torch.Tensor], deltas: torch.Tensor, spec) -> None:
@@ -786,7 +821,7 @@ class ReinforceAgent:
         gb[2] += small[17 * H1p + 4 * H2p:][:1]
 
     def _fused_grad(self, params, slot: str, spec, steps: "_Steps", K: int, gW: list[torch.Tensor],
-                    gb: list[torch.Tensor], out_dim: int, launch) -> None:
+                    gb: list[torch.Tensor], out_dim: int, launch, records: bool = False) -> None:
         """Chunked driver of the fused gradient kernels: per chunk of valid steps (symmetry k) `launch` runs the
         kernel, then the layer-2 weight + bias gradient a1^T d2 over the kernel's column buffers is g2048_dw2
         (_dw2: bf16 three-plane MFMA, one fp32 slab per workgroup folded into fp64) and the per-wave partials are
@@ -803,6 +838,9 @@ class ReinforceAgent:
         big = torch.zeros(H1p + 1, H2p, dtype=torch.float64, device=self.device)
         obs_code, scale = _OBS_CODE[self.env_config.obs_mode], float(self.env_config.obs_log2_scale)
         flat = steps.boards.reshape(-1)
+        if records:   # W3 [H2p, 4] zero-padded: g2048_dw2_actor rebuilds d2 with it
+            w3 = torch.zeros(H2p, 4, dtype=torch.float32, device=self.device)
+            w3[:h2, :out_dim] = params["W"][2]
         for k in range(K):
             for s0 in range(0, steps.N, self.grad_chunk_steps):
                 m = min(self.grad_chunk_steps, steps.N - s0)
@@ -813,11 +851,19 @@ class ReinforceAgent:
                 # column buffers: the kernel writes every column < ld (those past m as zero-coefficient padding)
                 ld = -(-m // 32) * 32
                 a1t = torch.empty(R, ld, dtype=torch.float32, device=self.device)     # 16-column blocks
-                d2t = torch.empty(R, ld, dtype=torch.float32, device=self.device)
+                if records:   # one 1 KiB record per 16 columns instead of d2 columns
+                    d2t = torch.empty(ld // 16 * 256, dtype=torch.float32, device=self.device)
+                else:
+                    d2t = torch.empty(R, ld, dtype=torch.float32, device=self.device)
                 launch(k, s0, sel, b, m, ld, a1t, d2t, part, waves, packed, gpacked, h1, h2, act, obs_code, scale)
                 if self.grad_probe is not None:
-                    self.grad_probe(slot, k, sel, _unblock(a1t, H1p, 0, m), _unblock(d2t, H2p, 0, m))
-                self._dw2(a1t, d2t, h1, h2, ld, big)       # layer-2 weight + bias gradient, chunks summed in fp64
+                    d2c = _unrecord_actor(d2t, w3, 0, m) if records else _unblock(d2t, H2p, 0, m)
+                    self.grad_probe(slot, k, sel, _unblock(a1t, H1p, 0, m), d2c)
+                # layer-2 weight + bias gradient, chunks summed in fp64
+                if records:
+                    self._dw2_actor(a1t, d2t, w3, h1, h2, ld, big)
+                else:
+                    self._dw2(a1t, d2t, h1, h2, ld, big)
                 self._fold(part, small)
         big, small = big.to(torch.float32), small.to(torch.float32)
         gW[0] += small[:16 * H1p].view(16, H1p)[:, :h1]

@@ -60,8 +60,11 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
 #endif
 }
 
-template <int NT1, int NT2, bool FAC>
+// MODE: 0 = d2 columns; 1 = the ReLU critic's factored records (mask words + scalar g); 2 = the ReLU actor's
+// records (mask words + the 4 values of g per sample; d2 rebuilt here)
+template <int NT1, int NT2, int MODE>
 struct Dw2 {
+    static constexpr bool FAC = MODE != 0;             // a record per block instead of d2 rows
     static constexpr int H1 = 32 * NT1, H2 = 32 * NT2;
     static constexpr int RB = H1 > H2 ? H1 : H2;        // rows per 16-column block of both column buffers
     static constexpr int kRows = FAC ? H1 : H1 + H2;    // staged rows: a1 rows, then d2 rows (FAC: a1 rows only)
@@ -77,7 +80,7 @@ struct Dw2 {
 struct Dw2Args {
     const float* a1t;   // a1^T, 16-column blocks of RB rows
     const float* d2t;   // d2^T, the same layout (factored form: the 1 KiB block records)
-    const float* w3;    // factored form: W3[:, 0] padded to H2p
+    const float* w3;    // MODE 1: W3[:, 0] padded to H2p; MODE 2: W3 [H2p][4] padded
     float* part;        // [nparts][H1p + 1][H2p]
     uint32_t ld, col0, ncols, kb;   // column range [col0, col0 + ncols); workgroup p takes kb columns from col0 + p kb
 };
@@ -109,9 +112,10 @@ __device__ __forceinline__ void read_frag(const float* stage, int row, int h, fl
 // FAC: the ReLU critic's factored form (g2048_critic_grad d2_form 1): d2 = m * (W3 g) with a 0/1 mask m and a scalar
 // g per sample, so dW2 = W3[j] * sum (a1 g) m^T and db2 = W3[j] * sum g m: the A operand is a1 * g (one fp32 product,
 // split exactly into three planes), the B operand the mask (exact in bf16), three MFMAs per step instead of six.
-template <int NT1, int NT2, bool FAC>
+template <int NT1, int NT2, int MODE>
 __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
-    using G = Dw2<NT1, NT2, FAC>;
+    using G = Dw2<NT1, NT2, MODE>;
+    constexpr bool FAC = G::FAC;
     __shared__ float S[kStages * G::kStageFloats];   // the only LDS object (see the glds / second-object rule)
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, r = lane & 31;
     const int wr = w >> 1, wc = w & 1;
@@ -162,6 +166,22 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     const int drow = G::H1 + (t < G::H2 ? t : G::H2 - 1);
     const int dunit = t < G::H2 ? t : G::H2 - 1;
     float dsum = 0.0f;
+    // MODE 2: the W3 rows this thread rebuilds d2 with -- its db2 unit and its B-fragment units
+    float4 w3d = make_float4(0.f, 0.f, 0.f, 0.f), w3c[G::TC];
+    if constexpr (MODE == 2) {
+        const float4* w3v = reinterpret_cast<const float4*>(a.w3);
+        w3d = w3v[dunit];
+#pragma unroll
+        for (int j = 0; j < G::TC; j++) w3c[j] = w3v[32 * ((NT2 >= 2 ? wc : 0) * G::TC + j) + r];
+    }
+    // d2 = act'(a2) (W3 g) exactly as grad_kernel forms it: fl(g0 w0), three fmaf, times 1.0 or 0.0
+    const auto d2_of = [](const float4 g, const float4 w, bool m) {
+        float dh = g.x * w.x;
+        dh = fmaf(g.y, w.y, dh);
+        dh = fmaf(g.z, w.z, dh);
+        dh = fmaf(g.w, w.w, dh);
+        return dh * (m ? 1.0f : 0.0f);
+    };
 
     // the bf16 planes of one stage's operand fragments (this wave's A rows and B rows), double-buffered: the loop
     // reads and splits stage it + 1 while the MFMAs of stage it run from registers
@@ -170,7 +190,37 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     };
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const auto load = [&](const float* st, Planes& p) {
-        if constexpr (FAC) {
+        if constexpr (MODE == 2) {
+            const float* rec = st + G::kRows * kBK;
+            const uint16_t* mw = reinterpret_cast<const uint16_t*>(rec);
+            const float4* gv = reinterpret_cast<const float4*>(rec + 128);   // byte 512: g of sample s at gv[s]
+            {   // db2: the d2 of unit `dunit` over the block's 16 samples, in sample order (as the column sum)
+                const uint32_t m = mw[dunit];
+#pragma unroll
+                for (int e = 0; e < 16; e++) dsum += d2_of(gv[e], w3d, (m >> e) & 1u);
+            }
+            if (rows_mine && cols_mine) {
+#pragma unroll
+                for (int i = 0; i < G::TR; i++) {
+                    float v[8];
+                    read_frag(st, 32 * (wr * G::TR + i) + r, h, v);
+                    split3(v, p.a0[i], p.a1[i], p.a2[i]);
+                }
+                float4 gk[8];
+#pragma unroll
+                for (int e = 0; e < 8; e++) gk[e] = gv[8 * h + e];
+#pragma unroll
+                for (int j = 0; j < G::TC; j++) {
+                    const uint32_t m = (uint32_t)mw[32 * (wc * G::TC + j) + r] >> (8 * h);
+                    float v[8];
+#pragma unroll
+                    for (int e = 0; e < 8; e++) v[e] = d2_of(gk[e], w3c[j], (m >> e) & 1u);
+                    split3(v, p.b0[j], p.b1[j], p.b2[j]);
+                }
+            }
+            return;
+        }
+        if constexpr (MODE == 1) {
             const float* rec = st + G::kRows * kBK;
             const uint16_t* mw = reinterpret_cast<const uint16_t*>(rec);
             const float* gv = rec + 128;   // byte 512: g of the block's 16 samples
@@ -240,7 +290,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
 #pragma unroll
                 for (int j = 0; j < G::TC; j++) {
                     floatx16 c = acc[i][j];   // smallest terms first
-                    if constexpr (FAC) {      // (a1 g) m: the mask is exact in one plane
+                    if constexpr (MODE == 1) {   // (a1 g) m: the mask is exact in one plane
                         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a2[i], p.b0[j], c, 0, 0, 0);
                         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a1[i], p.b0[j], c, 0, 0, 0);
                         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a0[i], p.b0[j], c, 0, 0, 0);
@@ -269,7 +319,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
         asm volatile("" ::: "memory");
         load(S + ((it + 1) % kStages) * G::kStageFloats, nxt);
         mfma(cur);
-        constexpr int kMfma = (FAC ? 3 : 6) * G::TR * G::TC;
+        constexpr int kMfma = (MODE == 1 ? 3 : 6) * G::TR * G::TC;
         __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // DS read: the first fragments' reads up front
 #pragma unroll
         for (int m = 0; m < kMfma; m++) {
@@ -308,26 +358,33 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     if (rows_mine && cols_mine) {
 #pragma unroll
         for (int j = 0; j < G::TC; j++) {
-            const float ws = FAC ? a.w3[32 * (wc * G::TC + j) + r] : 1.0f;
+            const float ws = MODE == 1 ? a.w3[32 * (wc * G::TC + j) + r] : 1.0f;
 #pragma unroll
             for (int i = 0; i < G::TR; i++)
 #pragma unroll
                 for (int q = 0; q < 16; q++)
                     out[(size_t)(32 * (wr * G::TR + i) + acc_row(q, h)) * G::H2 + 32 * (wc * G::TC + j) + r] =
-                        FAC ? acc[i][j][q] * ws : acc[i][j][q];
+                        MODE == 1 ? acc[i][j][q] * ws : acc[i][j][q];
         }
     }
-    if (t < G::H2) out[(size_t)G::H1 * G::H2 + t] = FAC ? dsum * a.w3[t] : dsum;
+    if (t < G::H2) out[(size_t)G::H1 * G::H2 + t] = MODE == 1 ? dsum * a.w3[t] : dsum;
 }
 
-template <int NT1, bool FAC>
+template <int NT1, int MODE>
 void launch_nt2(const Dw2Args& a, int nt2, int grid, hipStream_t s) {
     switch (nt2) {
-        case 1: hipLaunchKernelGGL((dw2_kernel<NT1, 1, FAC>), dim3(grid), dim3(kThreads), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((dw2_kernel<NT1, 2, FAC>), dim3(grid), dim3(kThreads), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((dw2_kernel<NT1, 4, FAC>), dim3(grid), dim3(kThreads), 0, s, a); break;
-        default: hipLaunchKernelGGL((dw2_kernel<NT1, 8, FAC>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((dw2_kernel<NT1, 1, MODE>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((dw2_kernel<NT1, 2, MODE>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((dw2_kernel<NT1, 4, MODE>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        default: hipLaunchKernelGGL((dw2_kernel<NT1, 8, MODE>), dim3(grid), dim3(kThreads), 0, s, a); break;
     }
+}
+
+template <int NT1>
+void launch_mode(const Dw2Args& a, int mode, int nt2, int grid, hipStream_t s) {
+    if (mode == 1) launch_nt2<NT1, 1>(a, nt2, grid, s);
+    else if (mode == 2) launch_nt2<NT1, 2>(a, nt2, grid, s);
+    else launch_nt2<NT1, 0>(a, nt2, grid, s);
 }
 
 int tiles_of(int hsize) {   // as g2048_policy.hip: 32-unit tiles rounded up to 1, 2, 4 or 8
@@ -370,11 +427,11 @@ namespace g2048_internal {
 int set_error(int code, const char* msg);
 }
 
-static int dw2_launch(const float* a1t, const float* d2t, const float* w3, bool fac, int h1, int h2, int64_t ld,
+static int dw2_launch(const float* a1t, const float* d2t, const float* w3, int mode, int h1, int h2, int64_t ld,
                       int64_t col0, int64_t ncols, int64_t cols_per_part, float* partials, int64_t nparts, void* stream) {
     using g2048_internal::set_error;
     if (h1 < 1 || h1 > 256 || h2 < 1 || h2 > 256) return set_error(G2048_EINVAL, "dw2: hidden sizes must be in 1..256");
-    if (!a1t || !d2t || !partials || (fac && !w3)) return set_error(G2048_EINVAL, "dw2: NULL buffer");
+    if (!a1t || !d2t || !partials || (mode && !w3)) return set_error(G2048_EINVAL, "dw2: NULL buffer");
     if (ld <= 0 || (ld & 15) || ld > ((int64_t)1 << 28)) return set_error(G2048_EINVAL, "dw2: ld must be a positive multiple of 16");
     if (col0 < 0 || (col0 & 15) || ncols < 0 || (ncols & 15) || col0 + ncols > ld)
         return set_error(G2048_EINVAL, "dw2: column range must be multiples of 16 inside ld");
@@ -387,10 +444,10 @@ static int dw2_launch(const float* a1t, const float* d2t, const float* w3, bool 
     hipStream_t s = (hipStream_t)stream;
     const int grid = (int)nparts;
     switch (nt1) {
-        case 1: fac ? launch_nt2<1, true>(a, nt2, grid, s) : launch_nt2<1, false>(a, nt2, grid, s); break;
-        case 2: fac ? launch_nt2<2, true>(a, nt2, grid, s) : launch_nt2<2, false>(a, nt2, grid, s); break;
-        case 4: fac ? launch_nt2<4, true>(a, nt2, grid, s) : launch_nt2<4, false>(a, nt2, grid, s); break;
-        default: fac ? launch_nt2<8, true>(a, nt2, grid, s) : launch_nt2<8, false>(a, nt2, grid, s); break;
+        case 1: launch_mode<1>(a, mode, nt2, grid, s); break;
+        case 2: launch_mode<2>(a, mode, nt2, grid, s); break;
+        case 4: launch_mode<4>(a, mode, nt2, grid, s); break;
+        default: launch_mode<8>(a, mode, nt2, grid, s); break;
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(G2048_EHIP, hipGetErrorString(e));
@@ -399,13 +456,19 @@ static int dw2_launch(const float* a1t, const float* d2t, const float* w3, bool 
 
 extern "C" int g2048_dw2(const float* a1t, const float* d2t, int h1, int h2, int64_t ld, int64_t col0, int64_t ncols,
                          int64_t cols_per_part, float* partials, int64_t nparts, void* stream) {
-    return dw2_launch(a1t, d2t, nullptr, false, h1, h2, ld, col0, ncols, cols_per_part, partials, nparts, stream);
+    return dw2_launch(a1t, d2t, nullptr, 0, h1, h2, ld, col0, ncols, cols_per_part, partials, nparts, stream);
 }
 
 extern "C" int g2048_dw2_factored(const float* a1t, const float* records, const float* w3, int h1, int h2, int64_t ld,
                                   int64_t col0, int64_t ncols, int64_t cols_per_part, float* partials, int64_t nparts,
                                   void* stream) {
-    return dw2_launch(a1t, records, w3, true, h1, h2, ld, col0, ncols, cols_per_part, partials, nparts, stream);
+    return dw2_launch(a1t, records, w3, 1, h1, h2, ld, col0, ncols, cols_per_part, partials, nparts, stream);
+}
+
+extern "C" int g2048_dw2_actor(const float* a1t, const float* records, const float* w3, int h1, int h2, int64_t ld,
+                               int64_t col0, int64_t ncols, int64_t cols_per_part, float* partials, int64_t nparts,
+                               void* stream) {
+    return dw2_launch(a1t, records, w3, 2, h1, h2, ld, col0, ncols, cols_per_part, partials, nparts, stream);
 }
 
 extern "C" int g2048_fold_partials(const float* partials, int64_t nparts, int64_t slab, double* acc, void* stream) {

@@ -680,8 +680,8 @@ struct GradArgs {
     // col_off .. col_off + 32 ngroups - 1; those past n are written as zero-coefficient padding)
     uint32_t col_off, ngroups;
     int part_accum;          // add this launch's per-wave partials to `part` instead of overwriting it
-    int d2_form;             // 1 (critic, ReLU): d2t receives the factored record of each 16-column block instead
-                             // of d2 columns (g2048_critic_grad in include/g2048.h; the FAC kernel variant)
+    int d2_form;             // 1 (critic, ReLU) / 2 (actor, ReLU): d2t receives one 1 KiB record per 16-column block
+                             // instead of d2 columns (include/g2048.h; the FAC kernel variants)
 };
 
 template <int NT1, int NT2>
@@ -735,6 +735,8 @@ __device__ __forceinline__ float4 frag_load(__amdgpu_buffer_rsrc_t r, uint32_t v
 // kernel writes, per 16-column block, a 1 KiB record: the ReLU mask as one 16-bit word per second-layer unit (bit k =
 // sample 16 c + k) at bytes [0, 2 H2p), and g of the 16 samples at bytes [512, 576); g2048_dw2_factored rebuilds
 // dW2 = W3 * sum (a1 g) m^T from it (64 B per sample written and read instead of 1 KiB).
+// FAC 2 (actor, ReLU): the same mask words plus the 4 values of g per sample (float4 at byte 512 + 16 (c & 15));
+// g2048_dw2_actor rebuilds d2 = fl(fl(g0 W3[j,0]) + g1 W3[j,1] ...) * m exactly as below (64 B per sample).
 template <int NT1, int NT2, int ACT, int OBS, int FAC = 0>
 __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
     typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -943,10 +945,16 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
         }
         GRAD_PH(2);
         // ---- d2 = act'(a2) * (W3 g), in place; d2^T columns (FAC: the block records' mask words and g instead)
-        if constexpr (FAC) {
+        if constexpr (FAC == 1) {
             if (h == 0) {   // g of this lane's sample at byte 512 + 4 (cj & 15) of its block's record
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g[0]), rd2, (int)((cj >> 4) * 1024u + 512u + (cj & 15u) * 4u),
                                                       0, 0);
+            }
+        } else if constexpr (FAC == 2) {
+            if (h == 0) {   // the 4 values of g of this lane's sample at byte 512 + 16 (cj & 15)
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 gv = {__float_as_uint(g[0]), __float_as_uint(g[1]), __float_as_uint(g[2]), __float_as_uint(g[3])};
+                __builtin_amdgcn_raw_buffer_store_b128(gv, rd2, (int)((cj >> 4) * 1024u + 512u + (cj & 15u) * 16u), 0, 0);
             }
         }
 #pragma unroll
@@ -1090,9 +1098,12 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
 
 template <int NT1, int NT2>
 void launch_grad(const GradArgs& a, int act, int obs, int grid, hipStream_t s) {
-    if (act == G2048_ACT_RELU && a.d2_form) {
+    if (act == G2048_ACT_RELU && a.d2_form == 1) {
         if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_LOG2, 1>), dim3(grid), dim3(kPolBlock), 0, s, a);
         else hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_RAW, 1>), dim3(grid), dim3(kPolBlock), 0, s, a);
+    } else if (act == G2048_ACT_RELU && a.d2_form == 2) {
+        if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_LOG2, 2>), dim3(grid), dim3(kPolBlock), 0, s, a);
+        else hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_RAW, 2>), dim3(grid), dim3(kPolBlock), 0, s, a);
     } else if (act == G2048_ACT_RELU) {
         if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_LOG2>), dim3(grid), dim3(kPolBlock), 0, s, a);
         else hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_RAW>), dim3(grid), dim3(kPolBlock), 0, s, a);
@@ -1298,8 +1309,9 @@ static int actor_or_critic_grad(const float* packed, const float* grad_packed, i
     if (!packed || !grad_packed || !a1t || !d2t || !partials || (n > 0 && (!boards || !coef)))
         return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
     if (waves != g2048_actor_grad_waves()) return pfail(G2048_EINVAL, "fused gradient: waves != g2048_actor_grad_waves()");
-    if (d2_form != 0 && (d2_form != 1 || !critic || activation != G2048_ACT_RELU))
-        return pfail(G2048_EINVAL, "fused gradient: d2_form 1 (factored) is for the ReLU critic only");
+    if (d2_form != 0 && (d2_form != (critic ? 1 : 2) || activation != G2048_ACT_RELU))
+        return pfail(G2048_EINVAL, "fused gradient: the factored d2 records are d2_form 1 for the ReLU critic, 2 for "
+                                   "the ReLU actor");
     GradArgs a;
     a.net = packed;
     a.w2b = grad_packed;
@@ -1339,11 +1351,12 @@ static int actor_or_critic_grad(const float* packed, const float* grad_packed, i
 
 int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,
                      float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions, const float* coef,
-                     int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, void* stream) {
+                     int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, int d2_form,
+                     void* stream) {
     if (n > 0 && !actions) return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
     return actor_or_critic_grad(packed, grad_packed, h1, h2, activation, obs_mode, obs_scale, use_mask, boards, actions,
                                 coef, n, ld, 0, ld, a1t, d2t, partials, 0, waves, stream, 0, 0, 0.0f, nullptr, nullptr,
-                                nullptr);
+                                nullptr, d2_form);
 }
 
 int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int h2, int activation, int obs_mode,

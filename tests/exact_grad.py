@@ -283,3 +283,146 @@ def grad_errors(got: dict, ref: dict) -> dict:
         for j, (g, e) in enumerate(zip(gs, ref[which])):
             errs[f"{which}{j}"] = _rel(g, e)
     return errs
+
+
+# ----------------------------------------------------------------------------------------------- any depth
+def fwd64_deep(W, b, x, act: str, masks=None):
+    """fp64 forward of a net of any depth: returns (pre-activations z_l, layer inputs a_0..a_L, output); masks
+    (ReLU): the activation pattern of each hidden layer to impose, or None."""
+    zs, acts = [], [x]
+    a = x
+    for l in range(len(W)):
+        z = a @ W[l] + b[l]
+        if l == len(W) - 1:
+            return zs, acts, z
+        if act == "ReLU" and masks is not None:
+            z = torch.where(masks[l], z.abs().clamp_min(1e-300), -z.abs())
+        zs.append(z)
+        a = torch.relu(z) if act == "ReLU" else torch.sigmoid(z)
+        acts.append(a)
+    raise AssertionError("unreachable")
+
+
+def bwd64_deep(W, zs, acts, g, acc, act: str):
+    """_backpropagation (src/reinforce_agent.py:639-678) of any depth, fp64, summed over rows into
+    acc = [dW_0..dW_L, db_0..db_L]."""
+    L1 = len(W)
+    d = g
+    for l in range(L1 - 1, -1, -1):
+        acc[l] += acts[l].t() @ d
+        acc[L1 + l] += d.sum(0)
+        if l:
+            dh = d @ W[l].t()
+            d = dh * ((zs[l - 1] > 0).to(dh.dtype) if act == "ReLU" else acts[l] * (1.0 - acts[l]))
+
+
+def pattern_flip_check_deep(W, b, x, zs, masks, stats: dict, key: str) -> None:
+    """pattern_flip_check for every hidden layer of a net of any depth (x exact -- one-hot or log2 obs): layer l's
+    fp32 pre-activation is within e_l = gamma_{n_l + 1} ((a_{l-1} + e_{l-1}) |W_l| + |b_l|) + e_{l-1} |W_l| of the
+    exact one (e_0 = 0 on the exact input; n_l = the layer's fan-in).  Rows whose pattern is all-zero in a layer
+    are compared too (the kernels' patterns here come from the activations themselves, not from d2)."""
+    st = stats.setdefault(key, dict(n=[0] * len(zs), tot=[0] * len(zs), viol=[0] * len(zs), max_ratio=0.0))
+    e_prev = torch.zeros_like(x)
+    a_prev = x
+    for l, z in enumerate(zs):
+        Wa = W[l].abs()
+        e = _gamma(W[l].shape[0] + 1) * ((a_prev + e_prev) @ Wa + b[l].abs()) + e_prev @ Wa
+        d = (z > 0) != masks[l]
+        st["n"][l] += int(d.sum())
+        st["tot"][l] += d.numel()
+        st["viol"][l] += int((d & (z.abs() > e)).sum())
+        if bool(d.any()):
+            st["max_ratio"] = max(st["max_ratio"], float((z.abs()[d] / e[d]).max()))
+        e_prev, a_prev = e, torch.relu(z)
+
+
+def exact_update_grads_deep(agent, batch, params, patterns: str | None = "plain", flip_stats: dict | None = None):
+    """Pre-clip gradients {"actor", "critic"} of update_batch on `batch` in fp64 for a net of ANY depth and obs
+    (one-hot included), the obs materialised by g2048_obs.  patterns="plain": the ReLU pattern of the product's own
+    fp32 path (ReinforceAgent._forward_kept_steps on the same chunks: the one-hot gather + hipBLASLt GEMMs), imposed
+    on the fp64 evaluation; flip_stats: also bound that pattern against fp64's own (pattern_flip_check_deep).
+    Covers the configurations the GPU tests use: MSE / Huber critic, baselines off / batch / batch_norm, no
+    augmentation, no rank weights."""
+    from rl2048_amd.agent import _Steps
+
+    actor_p, critic_p = params
+    c = agent.agent_config
+    act = agent.mlp_config.activation
+    assert not c.augmentation and not c.reward_rank_weights
+    dev = agent.device
+    steps = _Steps(agent, batch.lengths, batch.actions, batch.rewards, boards=batch.boards)
+    n, N = steps.n, steps.N
+    lens = steps.lengths
+    w_step = 1.0 / (lens[steps.lane].double() * n)
+    use_mask = bool(agent.env_config.use_action_mask)
+
+    def net64(P):
+        return [w.double() for w in P["W"]], [v.double() for v in P["b"]]
+
+    def x64(sel, nxt=False):
+        b = steps.boards_at(sel, 0, nxt)
+        x, mk = agent._obs_from_boards(b)
+        return x.double(), mk
+
+    def masks_of(P, sel):
+        if patterns is None or act != "ReLU":
+            return None
+        with torch.no_grad():
+            _, kept, _, _ = agent._forward_kept_steps(P, steps, sel, 0)
+        return [a > 0 for a in kept[1:]]
+
+    out = {}
+    if c.use_critic:
+        Wc, bc = net64(critic_p)
+        accc = [torch.zeros_like(p) for p in Wc + bc]
+        delta = torch.empty(N, dtype=torch.float64, device=dev)
+        for sel in agent._chunks(N):
+            x, _ = x64(sel)
+            m = masks_of(critic_p, sel)
+            zs, acts, v = fwd64_deep(Wc, bc, x, act, m)
+            if flip_stats is not None and m is not None:
+                pattern_flip_check_deep(Wc, bc, x, fwd64_deep(Wc, bc, x, act)[0], m, flip_stats, "critic")
+            xn, _ = x64(sel, nxt=True)
+            vn = fwd64_deep(Wc, bc, xn, act)[2][:, 0]
+            hn = steps.has_next[sel]
+            tgt = steps.rewards[sel].double() + c.gamma * vn * hn.double()
+            delta[sel] = tgt - v[:, 0]
+            diff = v[:, 0] - tgt
+            if c.critic_loss_type == "huber":
+                diff = torch.where(diff.abs() <= c.huber_delta, diff, c.huber_delta * torch.sign(diff))
+            bwd64_deep(Wc, zs, acts, (diff * w_step[sel]).unsqueeze(1), accc, act)
+        out["critic"] = accc
+        values = delta.float().double()
+    else:
+        T = steps.T
+        G = torch.zeros(n, dtype=torch.float64, device=dev)
+        Gt = torch.empty(T, n, dtype=torch.float64, device=dev)
+        R64 = batch.rewards.double()
+        for tt in reversed(range(T)):
+            G = R64[tt] + c.gamma * G
+            Gt[tt] = G
+        values = Gt.float().double().reshape(-1)[steps.vidx]
+    mode = c.baseline_mode
+    if mode in ("batch", "batch_norm"):
+        mu = values.mean()
+        adv = values - mu
+        if mode == "batch_norm":
+            adv = adv / ((values - mu).pow(2).mean().sqrt()).clamp_min(1e-8)
+    else:
+        assert mode == "off", mode
+        adv = values
+    W, b = net64(actor_p)
+    acc = [torch.zeros_like(p) for p in W + b]
+    for sel in agent._chunks(N):
+        x, mk = x64(sel)
+        m = masks_of(actor_p, sel)
+        zs, acts, lg = fwd64_deep(W, b, x, act, m)
+        if flip_stats is not None and m is not None:
+            pattern_flip_check_deep(W, b, x, fwd64_deep(W, b, x, act)[0], m, flip_stats, "actor")
+        if use_mask:
+            lg = torch.where(mk.bool(), lg, torch.full_like(lg, -1e9))
+        p = torch.softmax(lg, dim=1)
+        oh = torch.nn.functional.one_hot(steps.actions[sel], 4).double()
+        bwd64_deep(W, zs, acts, (oh - p) * (adv[sel] * w_step[sel]).unsqueeze(1), acc, act)
+    out["actor"] = acc
+    return out

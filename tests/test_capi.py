@@ -31,7 +31,7 @@ def test_header_declares_expected_api():
         "g2048_obs", "g2048_move", "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_packed_size",
         "g2048_policy_pack", "g2048_policy", "g2048_rollout", "g2048_grad_packed_size", "g2048_grad_partial_size",
         "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2",
-        "g2048_fold_partials", "g2048_dw2_factored", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
+        "g2048_fold_partials", "g2048_dw2_factored", "g2048_dw2_actor", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
         "g2048_deep_rollout", "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1"])
 
 
@@ -116,7 +116,7 @@ def test_argument_validation_without_gpu(L):
     assert lib.g2048_grad_partial_size(256, 256) == 17 * 256 + 4 * 256 + 4
     assert lib.g2048_grad_partial_size(20, 40) == 17 * 32 + 4 * 64 + 4
     assert lib.g2048_grad_pack(p, 32, 32, p, 10, None) == L.G2048_EINVAL and b"too small" in lib.g2048_last_error()
-    gargs = [p, p, 32, 32, L.ACT_RELU, L.OBS_LOG2, 1.0, 1, p, p, p, 40, 48, p, p, p, 1024, None]
+    gargs = [p, p, 32, 32, L.ACT_RELU, L.OBS_LOG2, 1.0, 1, p, p, p, 40, 48, p, p, p, 1024, 0, None]
     assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL and b"ld" in lib.g2048_last_error()   # ld % 32 != 0
     gargs[12] = 32
     assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL   # ld < n
