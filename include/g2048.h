@@ -357,6 +357,30 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
                        const uint64_t* pol_inc, uint64_t* pol_buf, uint32_t* queue, const int32_t* order,
                        int64_t n_order, int resume, const g2048_suspend* sus, int64_t n, int64_t cap,
                        const g2048_traj* traj, void* stream);
+/* The activations of hidden layer `layer` as the deep kernels compute them: out[j * ld + u], u < its padded width
+ * (tests and diagnostics: the kernels' own activation pattern). */
+int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, int activation, int obs_mode,
+                      float obs_scale, const uint64_t* boards, int64_t n, int layer, float* out, int64_t ld,
+                      void* stream);
+/* update_batch's actor or critic gradient (src/reinforce_agent.py:403-555, _backpropagation :639-678) fused for a
+ * packed deep net (forward + loss gradient + backward in one kernel, 32 samples per workgroup step), covered when
+ * g2048_deep_grad_slab() >= 0 (at most 48 dense 32x32 weight-gradient tiles: [256, 128, 64] and smaller).
+ * grad_packed: g2048_deep_grad_pack (the dense layers' weights in backward-fragment order; re-pack after every
+ * update).  Actor: coef = advantage x step weight, actions; critic (critic = 1): coef = step weight, target =
+ * r + gamma V(s') m, loss 0 MSE / 1 Huber, delta_out = target - V, value_out = V (NULL ok).  partials [nparts][slab]
+ * (nparts = one per workgroup, e.g. the CU count): per workgroup, in floats -- for l = 0 .. n_hidden - 1: dW_l
+ * (l = 0: [16][H0p] on log2 / raw obs, nothing on one-hot obs; l >= 1: [H_{l-1}p][H_lp]) then db_l [H_lp]; then
+ * dW_out [H_{L-1}p][4] and db_out [4] (Hp = units rounded up to 32).  One-hot obs: d0_out [n][H0p] receives the
+ * first layer's deltas for g2048_onehot_dw1 (ld = H0p). */
+int64_t g2048_deep_grad_pack_size(int obs_mode, int n_hidden, const int32_t* hidden);
+int64_t g2048_deep_grad_slab(int obs_mode, int n_hidden, const int32_t* hidden);
+int g2048_deep_grad_pack(const float* const* W, int obs_mode, int n_hidden, const int32_t* hidden, float* packed,
+                         int64_t packed_len, void* stream);
+int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden, const int32_t* hidden,
+                    int activation, int obs_mode, float obs_scale, int use_mask, const uint64_t* boards,
+                    const uint8_t* actions, const float* coef, int critic, int loss, float huber_delta,
+                    const float* target, float* delta_out, float* value_out, float* d0_out, int64_t n,
+                    float* partials, int64_t nparts, void* stream);
 /* The update's one-hot first layer: out[s * ld + j] = act(b1[j] + sum_c W1[17 c + e_c(s), j]) for s < m, j < h1
  * (W1 the [272, h1] parameter) -- the kept layer-1 activations of _backpropagation (src/reinforce_agent.py:639-678)
  * without the [m, 272] one-hot obs. */

@@ -182,6 +182,14 @@ def _declare(L):
                                     vp, i64, vp]
     L.g2048_deep_rollout.argtypes = [vp, i32, vp, i32, P(EnvCfg), i32, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32,
                                      P(Suspend), i64, i64, P(Traj), vp]
+    L.g2048_deep_hidden.argtypes = [vp, i32, vp, i32, i32, f, vp, i64, i32, vp, i64, vp]
+    L.g2048_deep_grad_pack_size.argtypes = [i32, i32, vp]
+    L.g2048_deep_grad_pack_size.restype = i64
+    L.g2048_deep_grad_slab.argtypes = [i32, i32, vp]
+    L.g2048_deep_grad_slab.restype = i64
+    L.g2048_deep_grad_pack.argtypes = [vp, i32, i32, vp, vp, i64, vp]
+    L.g2048_deep_grad.argtypes = [vp, vp, i32, vp, i32, i32, f, i32, vp, vp, vp, i32, i32, f, vp, vp, vp, vp, i64, vp,
+                                  i64, vp]
     L.g2048_onehot_layer1.argtypes = [vp, vp, i32, i32, vp, i64, i64, vp, vp]
     L.g2048_onehot_dw1_slab.argtypes = [i32]
     L.g2048_onehot_dw1_slab.restype = i64
@@ -190,7 +198,8 @@ def _declare(L):
                  "g2048_sample", "g2048_returns", "g2048_symmetries", "g2048_policy_pack", "g2048_policy",
                  "g2048_rollout", "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad",
                  "g2048_dw2", "g2048_fold_partials", "g2048_dw2_factored", "g2048_dw2_actor", "g2048_deep_pack", "g2048_deep_policy",
-                 "g2048_deep_rollout", "g2048_onehot_layer1", "g2048_onehot_dw1"):
+                 "g2048_deep_rollout", "g2048_deep_hidden", "g2048_deep_grad_pack", "g2048_deep_grad",
+                 "g2048_onehot_layer1", "g2048_onehot_dw1"):
         getattr(L, name).restype = ctypes.c_int
 
 
@@ -200,7 +209,9 @@ EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g204
                     "g2048_grad_packed_size", "g2048_grad_partial_size", "g2048_grad_pack", "g2048_actor_grad_waves",
                     "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2", "g2048_fold_partials",
                     "g2048_dw2_factored", "g2048_dw2_actor", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
-                    "g2048_deep_rollout", "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1")
+                    "g2048_deep_rollout", "g2048_deep_hidden", "g2048_deep_grad_pack_size", "g2048_deep_grad_slab",
+                    "g2048_deep_grad_pack", "g2048_deep_grad", "g2048_onehot_layer1", "g2048_onehot_dw1_slab",
+                    "g2048_onehot_dw1")
 
 
 def lib():

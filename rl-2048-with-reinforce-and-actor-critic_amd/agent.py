@@ -143,6 +143,11 @@ def _unblock(buf: torch.Tensor, rows: int, c0: int, m: int) -> torch.Tensor:
     return buf.reshape(ld // 16, R, 16).permute(1, 0, 2).reshape(R, ld)[:rows, c0:c0 + m]
 
 
+def _round32(h: int) -> int:
+    """Hidden units as the any-depth kernels pad them (g2048_deep.hip): whole 32-unit tiles."""
+    return 32 * ((h + 31) // 32)
+
+
 def _padded_units(h: int) -> int:
     """Hidden units as the fused kernels pad them: whole 32-unit MFMA tiles, 1, 2, 4 or 8 of them (tiles_for in
     csrc/g2048_policy.hip)."""
@@ -518,10 +523,11 @@ class ReinforceAgent:
         out, kept = mlp_forward_kept(params, x, act)
         return out, kept, None, mk
 
-    def _onehot_dw1_into(self, boards: torch.Tensor, d1: torch.Tensor, acc: torch.Tensor) -> None:
+    def _onehot_dw1_into(self, boards: torch.Tensor, d1: torch.Tensor, acc: torch.Tensor, h1: int | None = None) -> None:
         """acc (fp64 [273 h1]: dW1 rows, then db1) += the one-hot first layer's weight / bias gradient of the deltas
-        d1 [m, h1] (g2048_onehot_dw1 partial slabs folded in fp64)."""
-        m, h1 = d1.shape
+        d1 [m, ld] (units < h1, default ld; g2048_onehot_dw1 partial slabs folded in fp64)."""
+        m, ld = d1.shape
+        h1 = ld if h1 is None else h1
         if m == 0:
             return
         d1 = d1.contiguous()
@@ -530,9 +536,110 @@ class ReinforceAgent:
         per = max(1024, -(-m * slices // (2 * cus)))
         nparts = -(-m // per)
         part = torch.empty(nparts, int(self._lib.g2048_onehot_dw1_slab(h1)), dtype=torch.float32, device=self.device)
-        L.check(self._lib.g2048_onehot_dw1(L.ptr(boards), L.ptr(d1), h1, m, h1, per, L.ptr(part), nparts,
+        L.check(self._lib.g2048_onehot_dw1(L.ptr(boards), L.ptr(d1), h1, m, ld, per, L.ptr(part), nparts,
                                            self._stream))
         self._fold(part, acc)
+
+    def _deep_grad_spec(self, params, out_dim: int):
+        """_deep_spec when g2048_deep_grad covers the net (at most 48 dense 32x32 weight-gradient tiles), else None."""
+        if not self.use_fused_grad:
+            return None
+        d = self._deep_spec(params, out_dim)
+        if d is None or int(self._lib.g2048_deep_grad_slab(d[0], len(d[1]), d[3])) < 0:
+            return None
+        return d
+
+    def _pack_deep_grad(self, params, dspec, slot: str) -> torch.Tensor:
+        """g2048_deep_grad_pack (the dense layers' backward fragments), cached per slot until a parameter changes."""
+        Ws = params["W"]
+        key = (self._params_version,) + tuple((t.data_ptr(), t._version) for t in Ws)
+        entry = self._pack_cache.setdefault(slot + "/deepgrad", [None, None, None])
+        if key != entry[1]:
+            obs_code, hidden, _, harr = dspec
+            size = int(self._lib.g2048_deep_grad_pack_size(obs_code, len(hidden), harr))
+            if entry[0] is None or entry[0].numel() < size:
+                entry[0] = torch.empty(size, dtype=torch.float32, device=self.device)
+            ws = [t.contiguous() for t in Ws]
+            wp = (ctypes.c_void_p * len(ws))(*[t.data_ptr() for t in ws])
+            L.check(self._lib.g2048_deep_grad_pack(wp, obs_code, len(hidden), harr, L.ptr(entry[0]), size,
+                                                   self._stream))
+            entry[1] = key
+            entry[2] = ws
+        return entry[0]
+
+    @staticmethod
+    def _deep_slab_layout(hidden, onehot: bool):
+        """(pw, pb) float offsets of g2048_deep_grad's partial slab (include/g2048.h)."""
+        Hp = [_round32(h) for h in hidden]
+        pw, pb, off = [], [], 0
+        for l in range(len(hidden)):
+            pw.append(off)
+            off += (0 if onehot else 16 * Hp[0]) if l == 0 else Hp[l - 1] * Hp[l]
+            pb.append(off)
+            off += Hp[l]
+        pw.append(off)
+        off += Hp[-1] * 4
+        pb.append(off)
+        return pw, pb
+
+    def _deep_grad_fused(self, params, slot: str, dspec, steps: "_Steps", K: int, gW: list[torch.Tensor],
+                         gb: list[torch.Tensor], out_dim: int, adv=None, step_w=None, deltas=None) -> None:
+        """update_batch's actor (adv given) or critic (deltas given) branch for a deep / one-hot net through
+        g2048_deep_grad (forward + loss gradient + backward fused, dense weight gradients in registers), chunked;
+        the critic's V(s') by g2048_deep_policy's forward; one-hot first layers by the g2048_onehot_dw1 scatter of
+        the kernel's layer-0 deltas.  Accumulates into gW / gb like mlp_backward_."""
+        c = self.agent_config
+        obs_code, hidden, act, harr = dspec
+        onehot = obs_code == L.OBS_ONEHOT
+        critic = deltas is not None
+        packed = self._pack_deep(params, dspec, slot, out_dim)
+        bpacked = self._pack_deep_grad(params, dspec, slot)
+        nparts = int(self._lib.g2048_actor_grad_waves()) // 4          # one workgroup per CU
+        slab = int(self._lib.g2048_deep_grad_slab(obs_code, len(hidden), harr))
+        part = torch.empty(nparts, slab, dtype=torch.float32, device=self.device)
+        acc = torch.zeros(slab, dtype=torch.float64, device=self.device)
+        h0, H0p = hidden[0], _round32(hidden[0])
+        acc1 = torch.zeros(273 * h0, dtype=torch.float64, device=self.device) if onehot else None
+        use_mask = int(bool(self.env_config.use_action_mask))
+        loss = {"mse": 0, "huber": 1}[c.critic_loss_type] if critic else 0
+        scale = float(self.env_config.obs_log2_scale)
+        for k in range(K):
+            for s0 in range(0, steps.N, self.grad_chunk_steps):
+                m = min(self.grad_chunk_steps, steps.N - s0)
+                sel = torch.arange(s0, s0 + m, device=self.device)
+                b = steps.boards_at(sel, k)
+                acts = tgt = None
+                if critic:
+                    hn = steps.has_next[sel]
+                    vn = self._deep_forward(params, dspec, slot, steps.boards_at(sel, k, nxt=True), 1)[:, 0]
+                    tgt = (steps.rewards[sel] + (float(c.gamma) * vn) * hn.to(torch.float32)).contiguous()
+                    coef = step_w[sel].contiguous()
+                else:
+                    acts = steps.actions_k(sel, k).to(torch.uint8).contiguous()
+                    coef = (adv[k, sel] * step_w[sel]).contiguous()
+                d0 = torch.empty(m, H0p, dtype=torch.float32, device=self.device) if onehot else None
+                L.check(self._lib.g2048_deep_grad(L.ptr(packed), L.ptr(bpacked), len(hidden), harr, act, obs_code,
+                                                  scale, use_mask, L.ptr(b), L.ptr(acts), L.ptr(coef), int(critic),
+                                                  loss, float(c.huber_delta), L.ptr(tgt),
+                                                  L.ptr(deltas[k, s0:s0 + m]) if critic else None, None, L.ptr(d0),
+                                                  m, L.ptr(part), nparts, self._stream))
+                self._fold(part, acc)
+                if onehot:
+                    self._onehot_dw1_into(b, d0, acc1, h1=h0)
+        pw, pb = self._deep_slab_layout(hidden, onehot)
+        Hp = [_round32(h) for h in hidden]
+        acc = acc.to(torch.float32)
+        nh = len(hidden)
+        if onehot:
+            gW[0] += acc1[:272 * h0].view(272, h0).to(torch.float32)
+        else:
+            gW[0] += acc[pw[0]:pw[0] + 16 * Hp[0]].view(16, Hp[0])[:, :h0]
+        gb[0] += acc[pb[0]:pb[0] + Hp[0]][:h0]
+        for l in range(1, nh):
+            gW[l] += acc[pw[l]:pw[l] + Hp[l - 1] * Hp[l]].view(Hp[l - 1], Hp[l])[:hidden[l - 1], :hidden[l]]
+            gb[l] += acc[pb[l]:pb[l] + Hp[l]][:hidden[l]]
+        gW[nh] += acc[pw[nh]:pw[nh] + Hp[-1] * 4].view(Hp[-1], 4)[:hidden[-1], :out_dim]
+        gb[nh] += acc[pb[nh]:pb[nh] + 4][:out_dim]
 
     def _packed_policy(self, spec) -> torch.Tensor:
         """The actor packed in MFMA fragment order (g2048_policy_pack), re-packed whenever a parameter tensor is
@@ -566,6 +673,14 @@ class ReinforceAgent:
     # columns per g2048_dw2 workgroup: one workgroup per CU at 2^20 columns, never fewer than this many columns each
     dw2_min_cols_per_part = 2048
 
+    def _dw2_parts(self, ncols: int, h2: int) -> tuple[int, int]:
+        """(columns per part, parts) of a g2048_dw2* call: about one workgroup per CU -- a 256-wide second layer
+        runs two workgroups per part (its output column halves), so half as many parts."""
+        cus = int(self._lib.g2048_actor_grad_waves()) // 4
+        per_part_wgs = 2 if _padded_units(h2) == 256 else 1
+        cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * max(cus // per_part_wgs, 1))) * 16)
+        return cpp, -(-ncols // cpp)
+
     def _fold(self, part: torch.Tensor, acc: torch.Tensor) -> None:
         """acc (fp64, contiguous) += the sum of part's rows, taken in fp64 on the device (g2048_fold_partials)."""
         assert acc.dtype == torch.float64 and acc.is_contiguous() and part.is_contiguous()
@@ -582,9 +697,7 @@ class ReinforceAgent:
             return
         assert a1t.numel() == d2t.numel() and a1t.shape[0] == max(H1p, H2p)
         assert acc.shape == (H1p + 1, H2p)
-        cus = int(self._lib.g2048_actor_grad_waves()) // 4
-        cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * cus)) * 16)
-        nparts = -(-ncols // cpp)
+        cpp, nparts = self._dw2_parts(ncols, h2)
         part = torch.empty(nparts, H1p + 1, H2p, dtype=torch.float32, device=self.device)
         L.check(self._lib.g2048_dw2(L.ptr(a1t), L.ptr(d2t), h1, h2, int(a1t.shape[1]), 0, ncols, cpp, L.ptr(part),
                                     nparts, self._stream))
@@ -598,9 +711,7 @@ class ReinforceAgent:
         if ncols == 0:
             return
         assert rec.numel() * 4 >= (ncols // 16) * 1024 and w3.numel() == H2p and acc.shape == (H1p + 1, H2p)
-        cus = int(self._lib.g2048_actor_grad_waves()) // 4
-        cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * cus)) * 16)
-        nparts = -(-ncols // cpp)
+        cpp, nparts = self._dw2_parts(ncols, h2)
         part = torch.empty(nparts, H1p + 1, H2p, dtype=torch.float32, device=self.device)
         L.check(self._lib.g2048_dw2_factored(L.ptr(a1t), L.ptr(rec), L.ptr(w3), h1, h2, int(a1t.shape[1]), 0, ncols,
                                              cpp, L.ptr(part), nparts, self._stream))
@@ -614,9 +725,7 @@ class ReinforceAgent:
         if ncols == 0:
             return
         assert rec.numel() * 4 >= (ncols // 16) * 1024 and tuple(w3.shape) == (H2p, 4) and acc.shape == (H1p + 1, H2p)
-        cus = int(self._lib.g2048_actor_grad_waves()) // 4
-        cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * cus)) * 16)
-        nparts = -(-ncols // cpp)
+        cpp, nparts = self._dw2_parts(ncols, h2)
         part = torch.empty(nparts, H1p + 1, H2p, dtype=torch.float32, device=self.device)
         L.check(self._lib.g2048_dw2_actor(L.ptr(a1t), L.ptr(rec), L.ptr(w3), h1, h2, int(a1t.shape[1]), 0, ncols, cpp,
                                           L.ptr(part), nparts, self._stream))
@@ -1342,6 +1451,15 @@ class ReinforceAgent:
             if cspec is not None:
                 with torch.no_grad():
                     self._critic_grad_fused(steps, step_w, K, critic_g[:ncW], critic_g[ncW:], deltas, cspec)
+            cdg = (self._deep_grad_spec(self.critic_params, 1) if cspec is None and steps.boards is not None and
+                   c.critic_loss_type in ("mse", "huber") else None)
+            if cdg is not None:
+                self._paths["critic_grad"] = "g2048_deep_grad" + (" + g2048_onehot_dw1" if
+                                                                 cdg[0] == L.OBS_ONEHOT else "")
+                with torch.no_grad():
+                    self._deep_grad_fused(self.critic_params, "critic", cdg, steps, K, critic_g[:ncW], critic_g[ncW:],
+                                          1, step_w=step_w, deltas=deltas)
+                cspec = cdg      # handled: skip the torch loop below
             cdspec = self._deep_spec(self.critic_params, 1) if cspec is None and steps.boards is not None else None
             oh1 = self._onehot_first_layer(steps) and cspec is None
             acc1c = torch.zeros(273 * int(self.critic_params["W"][0].shape[1]), dtype=torch.float64,
@@ -1395,9 +1513,16 @@ class ReinforceAgent:
         nW = len(self.params["W"])
         gspec = self._fused_grad_spec() if steps.boards is not None else None
         self._paths["actor_grad"] = "g2048_actor_grad + g2048_dw2" if gspec is not None else "hipBLASLt backprop"
+        adg = self._deep_grad_spec(self.params, 4) if gspec is None and steps.boards is not None else None
         with torch.no_grad():
             if gspec is not None:
                 self._actor_grad_fused(steps, adv, step_w, K, actor_g[:nW], actor_g[nW:], gspec)
+            elif adg is not None:
+                self._paths["actor_grad"] = "g2048_deep_grad" + (" + g2048_onehot_dw1" if adg[0] == L.OBS_ONEHOT
+                                                                 else "")
+                self._deep_grad_fused(self.params, "actor", adg, steps, K, actor_g[:nW], actor_g[nW:], 4, adv=adv,
+                                      step_w=step_w)
+                gspec = adg      # handled: skip the torch loop below
             oh1 = gspec is None and self._onehot_first_layer(steps)
             acc1 = torch.zeros(273 * int(self.params["W"][0].shape[1]), dtype=torch.float64,
                                device=self.device) if oh1 else None

@@ -362,6 +362,33 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_policy_kernel(DeepPolArgs 
     }
 }
 
+// The activations of hidden layer `layer` (the net truncated after it runs deep_forward; its output-layer partials
+// are unused): out[j * ld + u] for u < 32 nt[layer] -- bit for bit what deep_policy_kernel / deep_grad_kernel compute
+// (the same code path), for tests that impose the kernels' own activation pattern on an fp64 evaluation.
+template <int OBS, int ACT>
+__global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net, const float* packed,
+                                                                     const uint64_t* boards, uint32_t n, float obs_scale,
+                                                                     float* out, uint32_t ld) {
+    __shared__ DeepSmem S;
+    const uint32_t groups = (n + 31u) >> 5;
+    const int tid = threadIdx.x, layer = net.L - 1, H = 32 * net.nt[layer];
+    for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
+        if (tid < 32) {
+            const uint32_t j = gi * 32u + (uint32_t)tid;
+            S.board[tid] = boards[j < n ? j : n - 1u];
+        }
+        __syncthreads();
+        deep_forward<OBS, ACT>(net, packed, S, obs_scale);
+        const float* act = S.act[layer & 1];
+        for (int e = tid; e < 32 * H; e += kDeepBlock) {
+            const int b = e / H, u = e % H;
+            const uint32_t j = gi * 32u + (uint32_t)b;
+            if (j < n) out[(size_t)j * ld + u] = act[u * kActStride + b];
+        }
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------------------------ rollout
 // The whole batched rollout (ReinforceAgent.run_episode, src/reinforce_agent.py:195-252, for n (env_seed,
 // policy_seed) pairs) for a net of any depth / one-hot obs, in one persistent launch: a workgroup runs 32 episode
@@ -516,6 +543,465 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArg
         }
         if (tid < 64) claim();
     }
+}
+
+// ------------------------------------------------------------------------------------ update (fused, any depth)
+// The actor / critic branch of update_batch (src/reinforce_agent.py:403-555; _backpropagation :639-678) for a net
+// of any depth whose dense weight-gradient tiles fit the workgroup's accumulator registers (see kGradTilesPerWave):
+// one 256-thread workgroup per CU takes 32 samples at a time --
+//   * forward as deep_forward, every hidden layer's activations kept in LDS ([unit][sample], stride 33);
+//   * g = (onehot(a) - p) coef (actor: masked softmax of the logits) or dL/dV coef (critic: MSE / Huber on V - target);
+//   * output layer on VALU: dW_out += a^T g per thread (unit = thread), delta = (W_out g) act'(a) in place;
+//   * each dense layer l (top down): dW_l += a_{l-1}^T delta_l on v_mfma_f32_32x32x2_f32 with the 32 samples as the
+//     contraction (A = a_{l-1}, B = delta_l, both from LDS), accumulated in registers across the workgroup's groups
+//     (tile f of the flattened tile list belongs to wave f % 4); then delta_{l-1} = (W_l delta_l) act'(a_{l-1}) as
+//     the forward's MFMA chain on the backward fragments (W_l in A-fragment order, streamed from L2), written over
+//     a_{l-1} in LDS;
+//   * first layer: log2 / raw obs: dW_0 += x^T delta_0 on MFMA (x rebuilt from the boards); one-hot obs: delta_0 is
+//     written out ([n][H0p], row-major) for g2048_onehot_dw1's scatter;
+//   * biases: per-thread sums (unit = thread).
+// Every workgroup writes one fp32 partial slab (g2048_fold_partials sums them in fp64).
+constexpr int kGradTilesPerWave = 12;   // dense dW tiles per wave held in AGPRs (x 16 floats)
+
+struct DeepGradArgs {
+    DeepNet net;
+    const float* packed;          // forward layout (g2048_deep_pack)
+    const float* bpacked;         // backward fragments (g2048_deep_grad_pack)
+    int64_t boff[kMaxHidden];     // per dense layer l >= 1: offset of its backward fragments
+    int64_t pw[kMaxHidden + 1], pb[kMaxHidden + 1];   // partial-slab offsets: dW_l, db_l (l = L: the output layer)
+    int64_t pslab;                // floats per partial slab
+    const uint64_t* boards;
+    const uint8_t* actions;
+    const float* coef;            // actor: advantage x step weight; critic: step weight
+    int critic, huber;
+    float huber_delta;
+    const float* target;          // critic: r + gamma V(s') m
+    float* delta_out;             // critic: target - V (NULL ok)
+    float* v_out;                 // critic: V (NULL ok)
+    float* d0_out;                // one-hot: delta_0 [n][H0p] for g2048_onehot_dw1
+    float* part;                  // [gridDim.x][pslab]
+    float obs_scale;
+    uint32_t n;
+    int use_mask;
+    int ntiles;                   // dense dW tiles in all
+    int tile_begin[kMaxHidden];   // flattened tile index of layer l's first tile (l >= 1)
+    int aoff[kMaxHidden];         // LDS float offset of layer l's activations / deltas
+    int lds_tail;                 // LDS float offset of the output partials, g, boards and bias sums
+};
+
+template <int ACT>
+__device__ __forceinline__ float act_deriv(float a) {   // from the activation (src/reinforce_agent.py:624-636)
+    if constexpr (ACT == 0) return a > 0.0f ? 1.0f : 0.0f;
+    else return a * (1.0f - a);
+}
+
+template <int OBS, int ACT>
+__global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a) {
+    extern __shared__ float dyn[];
+    const DeepNet& net = a.net;
+    const int L = net.L;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31, w = tid >> 6;
+    // LDS: the hidden layers' activations (deltas overwrite them top down; layer l at aoff[l]), the output
+    // partials, g, the boards and each thread's bias-gradient sums
+    const auto actl = [&](int l) { return dyn + a.aoff[l]; };
+    float* lds_end = dyn + a.lds_tail;
+    float (*part)[32][4] = reinterpret_cast<float (*)[32][4]>(lds_end);          // [8][32][4]
+    float (*gs)[4] = reinterpret_cast<float (*)[4]>(lds_end + 8 * 32 * 4);       // [32][4]
+    uint64_t* bds = reinterpret_cast<uint64_t*>(lds_end + 8 * 32 * 4 + 32 * 4);  // [32]
+    float* dbs = lds_end + 8 * 32 * 4 + 32 * 4 + 64;                             // [kMaxHidden][256]: db_l of unit tid
+    for (int l = 0; l < kMaxHidden; l++) dbs[l * 256 + tid] = 0.0f;
+    const float* P = a.packed;
+    floatx16 acc[kGradTilesPerWave];
+#pragma unroll
+    for (int k = 0; k < kGradTilesPerWave; k++) acc[k] = floatx16{};
+    floatx16 acc0[2] = {floatx16{}, floatx16{}};   // log2 / raw first layer: dW_0^T tiles t = w, w + 4
+    float dwo[4] = {0.f, 0.f, 0.f, 0.f}, dbo = 0.f;   // dW_out row tid; db_out (threads 0..3: output tid)
+    const int HL = 32 * net.nt[L - 1];
+    const float4* wout = reinterpret_cast<const float4*>(P + net.w[L]);
+    const uint32_t groups = (a.n + 31u) >> 5;
+    for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
+        const uint32_t j = gi * 32u + (uint32_t)(tid & 31);
+        const bool valid = j < a.n;
+        if (tid < 32) bds[tid] = valid ? a.boards[j] : 0ull;
+        __syncthreads();
+        // ---- forward: layer 0
+        {
+            float* out = actl(0);
+            const int nt0 = net.nt[0];
+            if constexpr (OBS == G2048_OBS_ONEHOT) {
+                const int bb = 8 * w + (lane >> 3), k = lane & 7;
+                const uint64_t b = bds[bb];
+                const int H = 32 * nt0;
+                const float* tab = P + net.w[0] + 4 * k;
+                float4 ac[8];
+#pragma unroll
+                for (int m = 0; m < 8; m++) ac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+                for (int c = 0; c < 16; c++) {
+                    const float* row = tab + (int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * H;
+#pragma unroll
+                    for (int m = 0; m < 8; m++) {
+                        if (m < nt0) {
+                            const float4 v = *reinterpret_cast<const float4*>(row + 32 * m);
+                            ac[m].x += v.x;
+                            ac[m].y += v.y;
+                            ac[m].z += v.z;
+                            ac[m].w += v.w;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    if (m < nt0) {
+                        const int u = 32 * m + 4 * k;
+                        const float4 bv = *reinterpret_cast<const float4*>(P + net.b[0] + u);
+                        out[(u + 0) * kActStride + bb] = activate<ACT>(ac[m].x + bv.x);
+                        out[(u + 1) * kActStride + bb] = activate<ACT>(ac[m].y + bv.y);
+                        out[(u + 2) * kActStride + bb] = activate<ACT>(ac[m].z + bv.z);
+                        out[(u + 3) * kActStride + bb] = activate<ACT>(ac[m].w + bv.w);
+                    }
+                }
+            } else {
+                const uint64_t b = bds[col];
+                float x[8];
+#pragma unroll
+                for (int s2 = 0; s2 < 8; s2++) x[s2] = obs_value<OBS>(b, 2 * s2 + h, a.obs_scale);
+                const float* w1f = P + net.w[0];
+                for (int t = w; t < nt0; t += 4) {
+                    floatx16 c = {};
+#pragma unroll
+                    for (int s2 = 0; s2 < 8; s2++)
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(w1f[(t * 8 + s2) * 64 + lane], x[s2], c, 0, 0, 0);
+                    const float* bb = P + net.b[0] + 32 * t;
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const int u = tile_row(r, h);
+                        out[(32 * t + u) * kActStride + col] = activate<ACT>(c[r] + bb[u]);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // ---- forward: dense layers (each into its own region)
+        for (int l = 1; l < L; l++) {
+            const float* in = actl(l - 1);
+            float* out = actl(l);
+            const int ntin = net.nt[l - 1], ntout = net.nt[l];
+            const float4* __restrict__ frag = reinterpret_cast<const float4*>(P + net.w[l]) + lane;
+            const float* bias = P + net.b[l];
+            for (int o = w; o < ntout; o += 4) {
+                floatx16 c = {};
+                const float4* fo = frag + (int64_t)o * ntin * 256;
+                float4 fa[4], fb[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) fa[q] = fo[q * 64];
+                for (int t = 0; t < ntin; t++) {
+                    const float4* nx = fo + (t + 1 < ntin ? t + 1 : t) * 256;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
+                    const float* ib = in + (32 * t + h) * kActStride + col;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, ib[(8 * q + 0) * kActStride], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, ib[(8 * q + 2) * kActStride], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, ib[(8 * q + 4) * kActStride], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, ib[(8 * q + 6) * kActStride], c, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) fa[q] = fb[q];
+                }
+                const float* bb = bias + 32 * o;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int u = tile_row(r, h);
+                    out[(32 * o + u) * kActStride + col] = activate<ACT>(c[r] + bb[u]);
+                }
+            }
+            __syncthreads();
+        }
+        // ---- output layer partials (as deep_forward)
+        {
+            const float* in = actl(L - 1);
+            const int pp = tid >> 5, bb = tid & 31, per = HL >> 3;
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+            for (int u = pp * per; u < (pp + 1) * per; u++) {
+                const float x = in[u * kActStride + bb];
+                const float4 wv = wout[u];
+                s0 = fmaf(x, wv.x, s0);
+                s1 = fmaf(x, wv.y, s1);
+                s2 = fmaf(x, wv.z, s2);
+                s3 = fmaf(x, wv.w, s3);
+            }
+            part[pp][bb][0] = s0;
+            part[pp][bb][1] = s1;
+            part[pp][bb][2] = s2;
+            part[pp][bb][3] = s3;
+        }
+        __syncthreads();
+        // ---- logits -> g (threads 0..31, one sample each)
+        if (tid < 32) {
+            const float* bo = P + net.b[L];
+            float lg[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                float v = part[0][tid][k];
+#pragma unroll
+                for (int q = 1; q < 8; q++) v += part[q][tid][k];
+                lg[k] = v + bo[k];
+            }
+            const float cf = valid ? a.coef[j] : 0.0f;
+            float g[4];
+            if (!a.critic) {
+                // logits_to_probs (src/MLP.py:139-156) and the policy-gradient logits delta (:328-354)
+                const uint32_t mw = a.use_mask ? mask_word_of(bds[tid]) : 0x01010101u;
+                const uint32_t act = valid ? a.actions[j] : 0u;
+                float l4[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) l4[k] = ((mw >> (8 * k)) & 0xFFu) ? lg[k] : -1e9f;
+                const float mx = fmaxf(fmaxf(l4[0], l4[1]), fmaxf(l4[2], l4[3]));
+                float e[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) e[k] = expf(l4[k] - mx);
+                const float es = ((e[0] + e[1]) + e[2]) + e[3];
+#pragma unroll
+                for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf;
+            } else {
+                // the critic's value-loss gradient (update_batch :403-498, _get_grad_logits_critic :884-910)
+                const float tg = valid ? a.target[j] : 0.0f;
+                const float diff = lg[0] - tg;
+                const float gd = (a.huber && fabsf(diff) > a.huber_delta) ? copysignf(a.huber_delta, diff) : diff;
+                g[0] = gd * cf;
+                g[1] = g[2] = g[3] = 0.0f;
+                if (valid && a.delta_out) a.delta_out[j] = tg - lg[0];
+                if (valid && a.v_out) a.v_out[j] = lg[0];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) gs[tid][k] = g[k];
+        }
+        __syncthreads();
+        // ---- output layer backward: dW_out row tid, db_out, delta_{L-1} in place (thread = unit)
+        if (tid < HL) {
+            float* arow = actl(L - 1) + tid * kActStride;
+            const float4 wv = wout[tid];
+            float d0 = dwo[0], d1 = dwo[1], d2 = dwo[2], d3 = dwo[3], db = dbs[(L - 1) * 256 + tid];
+            for (int n2 = 0; n2 < 32; n2++) {
+                const float x = arow[n2];
+                const float4 g4 = *reinterpret_cast<const float4*>(gs[n2]);
+                d0 = fmaf(x, g4.x, d0);
+                d1 = fmaf(x, g4.y, d1);
+                d2 = fmaf(x, g4.z, d2);
+                d3 = fmaf(x, g4.w, d3);
+                float dh = g4.x * wv.x;
+                dh = fmaf(g4.y, wv.y, dh);
+                dh = fmaf(g4.z, wv.z, dh);
+                dh = fmaf(g4.w, wv.w, dh);
+                const float dl = dh * act_deriv<ACT>(x);
+                db += dl;
+                arow[n2] = dl;
+            }
+            dwo[0] = d0; dwo[1] = d1; dwo[2] = d2; dwo[3] = d3;
+            dbs[(L - 1) * 256 + tid] = db;
+        }
+        if (tid < 4) {
+            float sgo = 0.f;
+            for (int n2 = 0; n2 < 32; n2++) sgo += gs[n2][tid];
+            dbo += sgo;
+        }
+        __syncthreads();
+        // ---- dense layers top down: dW_l (MFMA over the 32 samples), then delta_{l-1} (MFMA chain) in place
+        for (int l = L - 1; l >= 1; l--) {
+            const float* A = actl(l - 1);
+            const float* D = actl(l);
+            const int ntin = net.nt[l - 1], ntout = net.nt[l];
+            const int f0 = a.tile_begin[l], f1 = f0 + ntin * ntout;
+#pragma unroll
+            for (int k = 0; k < kGradTilesPerWave; k++) {
+                const int f = w + 4 * k;
+                if (f >= f0 && f < f1) {                     // wave-uniform
+                    const int ti = (f - f0) / ntout, tj = (f - f0) % ntout;
+                    const float* ap = A + (32 * ti + col) * kActStride + h;
+                    const float* dp = D + (32 * tj + col) * kActStride + h;
+                    floatx16 c = acc[k];
+#pragma unroll
+                    for (int s2 = 0; s2 < 16; s2++)
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[2 * s2], dp[2 * s2], c, 0, 0, 0);
+                    acc[k] = c;
+                }
+            }
+            __syncthreads();                               // every read of a_{l-1} by the dW tiles is done
+            // delta_{l-1} = (W_l delta_l) act'(a_{l-1}): output tiles = layer l-1's units, k = layer l's units
+            const float4* __restrict__ frag = reinterpret_cast<const float4*>(a.bpacked + a.boff[l]) + lane;
+            float* Aw = actl(l - 1);
+            for (int o = w; o < ntin; o += 4) {
+                floatx16 c = {};
+                const float4* fo = frag + (int64_t)o * ntout * 256;
+                float4 fa[4], fb[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) fa[q] = fo[q * 64];
+                for (int t = 0; t < ntout; t++) {
+                    const float4* nx = fo + (t + 1 < ntout ? t + 1 : t) * 256;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
+                    const float* ib = D + (32 * t + h) * kActStride + col;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, ib[(8 * q + 0) * kActStride], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, ib[(8 * q + 2) * kActStride], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, ib[(8 * q + 4) * kActStride], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, ib[(8 * q + 6) * kActStride], c, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) fa[q] = fb[q];
+                }
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    float* pa = Aw + (32 * o + tile_row(r, h)) * kActStride + col;
+                    *pa = c[r] * act_deriv<ACT>(*pa);
+                }
+            }
+            __syncthreads();
+            // db_{l-1} of unit tid
+            if (tid < 32 * ntin) {
+                const float* drow = Aw + tid * kActStride;
+                float db = dbs[(l - 1) * 256 + tid];
+                for (int n2 = 0; n2 < 32; n2++) db += drow[n2];
+                dbs[(l - 1) * 256 + tid] = db;
+            }
+        }
+        // ---- first layer's weight gradient
+        if constexpr (OBS == G2048_OBS_ONEHOT) {
+            // delta_0 out for the one-hot scatter (g2048_onehot_dw1): row j, unit tid (coalesced rows)
+            const int H0 = 32 * net.nt[0];
+            if (tid < H0) {
+                const float* drow = actl(0) + tid * kActStride;
+                for (int n2 = 0; n2 < 32; n2++) {
+                    const uint32_t jj = gi * 32u + (uint32_t)n2;
+                    if (jj < a.n) a.d0_out[(size_t)jj * H0 + tid] = drow[n2];
+                }
+            }
+        } else {
+            // dW_0^T tile t (32 units x 32 features, features >= 16 zero): A = delta_0 [unit][sample], B = x [sample][feature]
+            const float* D0 = actl(0);
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int t = w + 4 * k;
+                if (t < net.nt[0]) {
+                    floatx16 c = acc0[k];
+                    const float* dp = D0 + (32 * t + col) * kActStride + h;
+#pragma unroll
+                    for (int s2 = 0; s2 < 16; s2++) {
+                        const float xv = col < 16 ? obs_value<OBS>(bds[2 * s2 + h], col, a.obs_scale) : 0.0f;
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(dp[2 * s2], xv, c, 0, 0, 0);
+                    }
+                    acc0[k] = c;
+                }
+            }
+        }
+        __syncthreads();   // the next group rewrites the boards and layer 0
+    }
+    // ---- this workgroup's partial slab
+    float* out = a.part + (size_t)blockIdx.x * a.pslab;
+#pragma unroll
+    for (int k = 0; k < kGradTilesPerWave; k++) {
+        const int f = w + 4 * k;
+        if (f < a.ntiles) {
+            int l = 1;
+            while (l + 1 < L && f >= a.tile_begin[l + 1]) l++;
+            const int ntout = net.nt[l], f0 = a.tile_begin[l];
+            const int ti = (f - f0) / ntout, tj = (f - f0) % ntout;
+            const int Ho = 32 * ntout;
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                out[a.pw[l] + (int64_t)(32 * ti + tile_row(r, h)) * Ho + 32 * tj + col] = acc[k][r];
+        }
+    }
+    if constexpr (OBS != G2048_OBS_ONEHOT) {
+        const int H0 = 32 * net.nt[0];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int t = w + 4 * k;
+            if (t < net.nt[0] && col < 16) {               // C[unit][feature]: dW_0[feature][unit]
+#pragma unroll
+                for (int r = 0; r < 16; r++) out[a.pw[0] + (int64_t)col * H0 + 32 * t + tile_row(r, h)] = acc0[k][r];
+            }
+        }
+    }
+    for (int l = 0; l < L; l++)
+        if (tid < 32 * net.nt[l]) out[a.pb[l] + tid] = dbs[l * 256 + tid];
+    if (tid < HL) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) out[a.pw[L] + (int64_t)tid * 4 + k] = dwo[k];
+    }
+    if (tid < 4) out[a.pb[L] + tid] = dbo;
+}
+
+// backward fragments of the dense layers: layer l (1..L-1) at boff[l], [nt_{l-1}][nt_l][4][64][4]: output tile o
+// (a unit tile of layer l-1), k-tile t (of layer l), lane, k-step s = 4 q + u -> W_l[32 o + (lane & 31)][32 t + 2 s + (lane >> 5)]
+struct DeepGradPackArgs {
+    const float* W[kMaxHidden];
+    int h[kMaxHidden];
+    int nt[kMaxHidden];
+    int64_t boff[kMaxHidden + 1];
+    int L;
+    float* dst;
+};
+
+__global__ void __launch_bounds__(256) deep_grad_pack_kernel(DeepGradPackArgs a) {
+    const int64_t total = a.boff[a.L];
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+        int l = a.L - 1;
+        while (l > 1 && q < a.boff[l]) l--;
+        const int64_t x = q - a.boff[l];
+        const int u = (int)(x & 3), lane = (int)((x >> 2) & 63), qq = (int)((x >> 8) & 3);
+        const int64_t tt = x >> 10;
+        const int t = (int)(tt % a.nt[l]), o = (int)(tt / a.nt[l]);
+        const int i = 32 * o + (lane & 31), k = 32 * t + 2 * (4 * qq + u) + (lane >> 5);
+        a.dst[q] = (i < a.h[l - 1] && k < a.h[l]) ? a.W[l][(int64_t)i * a.h[l] + k] : 0.0f;
+    }
+}
+
+// partial-slab layout of deep_grad_kernel: dense dW_l [H_{l-1}p][H_lp] + db_l for l >= 1, dW_0 ([16][H0p], log2 /
+// raw only) + db_0, dW_out [H_{L-1}p][4] + db_out [4]
+struct DeepGradLayout {
+    int64_t pw[kMaxHidden + 1], pb[kMaxHidden + 1], pslab;
+    int64_t boff[kMaxHidden + 1];
+    int ntiles;
+    int tile_begin[kMaxHidden];
+};
+
+DeepGradLayout deep_grad_layout(const DeepNet& n) {
+    DeepGradLayout g{};
+    int64_t off = 0;
+    for (int l = 0; l < n.L; l++) {
+        g.pw[l] = off;
+        if (l == 0) off += n.onehot ? 0 : (int64_t)16 * 32 * n.nt[0];
+        else off += (int64_t)32 * n.nt[l - 1] * 32 * n.nt[l];
+        g.pb[l] = off;
+        off += 32 * n.nt[l];
+    }
+    g.pw[n.L] = off;
+    off += (int64_t)32 * n.nt[n.L - 1] * 4;
+    g.pb[n.L] = off;
+    off += 4;
+    g.pslab = off;
+    int64_t bo = 0;
+    int tiles = 0;
+    for (int l = 1; l < n.L; l++) {
+        g.boff[l] = bo;
+        bo += (int64_t)n.nt[l - 1] * n.nt[l] * 1024;
+        g.tile_begin[l] = tiles;
+        tiles += n.nt[l - 1] * n.nt[l];
+    }
+    g.boff[n.L] = bo;
+    if (n.L == 1) g.boff[1] = 0;
+    g.ntiles = tiles;
+    return g;
+}
+
+int64_t deep_grad_lds_bytes(const DeepNet& n) {
+    int64_t units = 0;
+    for (int l = 0; l < n.L; l++) units += 32 * n.nt[l];
+    return (units * kActStride + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256) * 4;
 }
 
 // ------------------------------------------------------------------------------------ one-hot layer 1 (update)
@@ -766,6 +1252,162 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
         else hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_RAW, 1>), dim3(grid), dim3(kDeepBlock), 0, s, a);
     }
     return check_hip();
+}
+
+int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, int activation, int obs_mode,
+                      float obs_scale, const uint64_t* boards, int64_t n, int layer, float* out, int64_t ld,
+                      void* stream) {
+    DeepNet net;
+    if (obs_mode != G2048_OBS_LOG2 && obs_mode != G2048_OBS_RAW && obs_mode != G2048_OBS_ONEHOT)
+        return dfail(G2048_EINVAL, "deep policy: obs_mode must be log2, raw or onehot");
+    if (!deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, net))
+        return dfail(G2048_EINVAL, "deep policy: 1..4 hidden layers of 1..256 units");
+    if (layer < 0 || layer >= n_hidden || ld < 32 * net.nt[layer] || n < 0 || n > (int64_t)0xFFFFFFE0)
+        return dfail(G2048_EINVAL, "deep hidden: bad layer / ld / n");
+    if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
+        return dfail(G2048_EINVAL, "Unsupported activation");
+    if (!packed || (n > 0 && (!boards || !out))) return dfail(G2048_EINVAL, "deep hidden: NULL buffer");
+    if (n == 0) return G2048_OK;
+    net.L = layer + 1;   // truncated: deep_forward stops after `layer` (offsets of the kept layers unchanged)
+    const int64_t groups = (n + 31) / 32, cap = 2 * (int64_t)device_cus();
+    const int grid = (int)(groups < cap ? groups : cap);
+    hipStream_t s = (hipStream_t)stream;
+#define G2048_HIDDEN(O, A) hipLaunchKernelGGL((deep_hidden_kernel<O, A>), dim3(grid), dim3(kDeepBlock), 0, s, net, packed, \
+                                             boards, (uint32_t)n, obs_scale, out, (uint32_t)ld)
+    if (obs_mode == G2048_OBS_ONEHOT) {
+        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_ONEHOT, 0); else G2048_HIDDEN(G2048_OBS_ONEHOT, 1);
+    } else if (obs_mode == G2048_OBS_LOG2) {
+        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_LOG2, 0); else G2048_HIDDEN(G2048_OBS_LOG2, 1);
+    } else {
+        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_RAW, 0); else G2048_HIDDEN(G2048_OBS_RAW, 1);
+    }
+#undef G2048_HIDDEN
+    return check_hip();
+}
+
+int64_t g2048_deep_grad_pack_size(int obs_mode, int n_hidden, const int32_t* hidden) {
+    DeepNet n;
+    if (!deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, n)) return -1;
+    const int64_t s = deep_grad_layout(n).boff[n.L];
+    return s > 0 ? s : 1;
+}
+
+int64_t g2048_deep_grad_slab(int obs_mode, int n_hidden, const int32_t* hidden) {
+    DeepNet n;
+    if (obs_mode != G2048_OBS_LOG2 && obs_mode != G2048_OBS_RAW && obs_mode != G2048_OBS_ONEHOT) return -1;
+    if (!deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, n)) return -1;
+    const DeepGradLayout g = deep_grad_layout(n);
+    if (g.ntiles > 4 * kGradTilesPerWave || deep_grad_lds_bytes(n) > 160 * 1024) return -1;   // not covered
+    return g.pslab;
+}
+
+int g2048_deep_grad_pack(const float* const* W, int obs_mode, int n_hidden, const int32_t* hidden, float* packed,
+                         int64_t packed_len, void* stream) {
+    DeepNet n;
+    if (!deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, n))
+        return dfail(G2048_EINVAL, "deep gradient: 1..4 hidden layers of 1..256 units");
+    const DeepGradLayout g = deep_grad_layout(n);
+    if (!W || !packed) return dfail(G2048_EINVAL, "deep gradient: NULL buffer");
+    if (packed_len < g.boff[n.L]) return dfail(G2048_EINVAL, "deep gradient: packed buffer too small");
+    if (g.boff[n.L] == 0) return G2048_OK;   // one hidden layer: no dense backward fragments
+    DeepGradPackArgs a{};
+    for (int l = 0; l < n_hidden; l++) {
+        if (l >= 1 && !W[l]) return dfail(G2048_EINVAL, "deep gradient: NULL weight");
+        a.W[l] = W[l];
+        a.h[l] = hidden[l];
+        a.nt[l] = n.nt[l];
+    }
+    for (int l = 0; l <= n_hidden; l++) a.boff[l] = g.boff[l];
+    a.L = n_hidden;
+    a.dst = packed;
+    const int64_t total = g.boff[n.L];
+    const int grid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(deep_grad_pack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    return check_hip();
+}
+
+}  // extern "C"
+
+namespace {
+template <int OBS, int ACT>
+int launch_deep_grad(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t s) {
+    static bool attr_set = false;   // per instantiation (the attribute is per kernel; setting it twice is harmless)
+    if (!attr_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&deep_grad_kernel<OBS, ACT>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+            return dfail(G2048_EHIP, "deep gradient: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((deep_grad_kernel<OBS, ACT>), dim3(grid), dim3(kDeepBlock), (unsigned)lds, s, a);
+    return check_hip();
+}
+}  // namespace
+
+extern "C" {
+
+int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden, const int32_t* hidden,
+                    int activation, int obs_mode, float obs_scale, int use_mask, const uint64_t* boards,
+                    const uint8_t* actions, const float* coef, int critic, int loss, float huber_delta,
+                    const float* target, float* delta_out, float* value_out, float* d0_out, int64_t n,
+                    float* partials, int64_t nparts, void* stream) {
+    if (n < 0 || n > (int64_t)0x7FFFFFE0) return dfail(G2048_EINVAL, "n out of range");
+    if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
+        return dfail(G2048_EINVAL, "Unsupported activation");
+    if (g2048_deep_grad_slab(obs_mode, n_hidden, hidden) < 0)
+        return dfail(G2048_EINVAL, "deep gradient: net not covered (obs mode, 1..4 layers of 1..256 units, at most "
+                                   "48 dense 32x32 weight-gradient tiles)");
+    if (critic && loss != 0 && loss != 1) return dfail(G2048_EINVAL, "Unknown critic loss type");
+    if (!packed || !partials || (n > 0 && (!boards || !coef)) || (n > 0 && !critic && !actions) ||
+        (n > 0 && critic && !target) || (n > 0 && obs_mode == G2048_OBS_ONEHOT && !d0_out))
+        return dfail(G2048_EINVAL, "deep gradient: NULL buffer");
+    if (nparts < 1 || nparts > 65535) return dfail(G2048_EINVAL, "deep gradient: nparts out of range");
+    DeepNet net;
+    deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, net);
+    const DeepGradLayout g = deep_grad_layout(net);
+    if (g.boff[net.L] > 0 && !grad_packed) return dfail(G2048_EINVAL, "deep gradient: NULL backward fragments");
+    DeepGradArgs a{};
+    a.net = net;
+    a.packed = packed;
+    a.bpacked = grad_packed;
+    int off = 0;
+    for (int l = 0; l < net.L; l++) {
+        a.boff[l] = g.boff[l];
+        a.tile_begin[l] = g.tile_begin[l];
+        a.aoff[l] = off;
+        off += 32 * net.nt[l] * kActStride;
+    }
+    a.lds_tail = off;
+    for (int l = 0; l <= net.L; l++) {
+        a.pw[l] = g.pw[l];
+        a.pb[l] = g.pb[l];
+    }
+    a.pslab = g.pslab;
+    a.ntiles = g.ntiles;
+    a.boards = boards;
+    a.actions = actions;
+    a.coef = coef;
+    a.critic = critic;
+    a.huber = loss == 1;
+    a.huber_delta = huber_delta;
+    a.target = target;
+    a.delta_out = delta_out;
+    a.v_out = value_out;
+    a.d0_out = d0_out;
+    a.part = partials;
+    a.obs_scale = obs_scale;
+    a.n = (uint32_t)n;
+    a.use_mask = use_mask;
+    const int64_t lds = deep_grad_lds_bytes(net);
+    hipStream_t s = (hipStream_t)stream;
+    const int grid = (int)nparts;   // every workgroup writes its slab (zeros when it gets no group)
+    if (obs_mode == G2048_OBS_ONEHOT)
+        return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_ONEHOT, 0>(a, grid, lds, s)
+                                            : launch_deep_grad<G2048_OBS_ONEHOT, 1>(a, grid, lds, s);
+    if (obs_mode == G2048_OBS_LOG2)
+        return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_LOG2, 0>(a, grid, lds, s)
+                                            : launch_deep_grad<G2048_OBS_LOG2, 1>(a, grid, lds, s);
+    return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_RAW, 0>(a, grid, lds, s)
+                                        : launch_deep_grad<G2048_OBS_RAW, 1>(a, grid, lds, s);
 }
 
 int g2048_onehot_layer1(const float* W1, const float* b1, int h1, int activation, const uint64_t* boards, int64_t m,

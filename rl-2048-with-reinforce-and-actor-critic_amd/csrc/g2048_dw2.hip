@@ -67,14 +67,19 @@ struct Dw2 {
     static constexpr bool FAC = MODE != 0;             // a record per block instead of d2 rows
     static constexpr int H1 = 32 * NT1, H2 = 32 * NT2;
     static constexpr int RB = H1 > H2 ? H1 : H2;        // rows per 16-column block of both column buffers
-    static constexpr int kRows = FAC ? H1 : H1 + H2;    // staged rows: a1 rows, then d2 rows (FAC: a1 rows only)
+    // output column halves: a 256-wide second layer is split over two workgroups (blockIdx.y), each owning 128
+    // output columns -- with all 256 in one workgroup every wave holds 16 tiles = 256 accumulators, the whole AGPR
+    // file, and the register allocator spilled them to scratch inside the loop (~145 VGPRs)
+    static constexpr int CS = NT2 >= 8 ? 2 : 1;
+    static constexpr int NT2h = NT2 / CS, H2h = H2 / CS;
+    static constexpr int kRows = FAC ? H1 : H1 + H2h;   // staged rows: a1 rows, then this half's d2 rows
     static constexpr int kRecFloats = FAC ? 256 : 0;    // FAC: the block's 1 KiB record (mask words, g)
     static constexpr int kStageFloats = kRows * kBK + kRecFloats;   // 64 B per staged row
     static constexpr int kRowGlds = kRows / 16;         // 1 KiB LDS-DMA instructions per stage (16 rows each)
     static constexpr int kGlds = kRowGlds + (FAC ? 1 : 0);          // + the record
     static constexpr int kGldsPerWave = (kGlds + 3) / 4;
     static constexpr int TR = NT1 >= 2 ? NT1 / 2 : 1;   // row tiles per wave (2 x 2 wave grid)
-    static constexpr int TC = NT2 >= 2 ? NT2 / 2 : 1;   // column tiles per wave
+    static constexpr int TC = NT2h >= 2 ? NT2h / 2 : 1;   // column tiles per wave
 };
 
 struct Dw2Args {
@@ -122,6 +127,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     const uint32_t k_begin = a.col0 + blockIdx.x * a.kb;
     const uint32_t k_end = min(k_begin + a.kb, a.col0 + a.ncols);
     const int iters = k_end > k_begin ? (int)((k_end - k_begin) / kBK) : 0;
+    const int c0 = (int)blockIdx.y * G::H2h;            // this workgroup's first output column (unit of layer 2)
 
     // this lane's LDS-DMA sources: instruction g (wave w issues g = w, w + 4, ...; past the end: the last one
     // again, an identical rewrite) covers staged rows 16 g .. 16 g + 15; lane -> row 16 g + (lane >> 2), slot
@@ -142,7 +148,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
         } else {
             const int row = 16 * g + (lane >> 2);
             const int chunk = (lane & 3) ^ ((lane >> 4) & 3);
-            const float* base = row < G::H1 ? a.a1t + row * kBK : a.d2t + (row - G::H1) * kBK;
+            const float* base = row < G::H1 ? a.a1t + row * kBK : a.d2t + (row - G::H1 + c0) * kBK;
             src[i] = base + (size_t)(k_begin / kBK) * G::RB * kBK + 4 * chunk;   // block k_begin / 16
         }
     }
@@ -161,10 +167,11 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     for (int i = 0; i < G::TR; i++)
 #pragma unroll
         for (int j = 0; j < G::TC; j++) acc[i][j] = floatx16{};
-    const bool rows_mine = NT1 >= 2 || wr == 0, cols_mine = NT2 >= 2 || wc == 0;
-    // db2: thread t sums d2 row t (threads past H2 sum row H2 - 1 and never store: no branch in the loop body)
-    const int drow = G::H1 + (t < G::H2 ? t : G::H2 - 1);
-    const int dunit = t < G::H2 ? t : G::H2 - 1;
+    const bool rows_mine = NT1 >= 2 || wr == 0, cols_mine = G::NT2h >= 2 || wc == 0;
+    // db2: thread t sums d2 row c0 + t (threads past H2h sum the half's last row and never store: no branch in the
+    // loop body)
+    const int drow = G::H1 + (t < G::H2h ? t : G::H2h - 1);
+    const int dunit = c0 + (t < G::H2h ? t : G::H2h - 1);
     float dsum = 0.0f;
     // MODE 2: the W3 rows this thread rebuilds d2 with -- its db2 unit and its B-fragment units
     float4 w3d = make_float4(0.f, 0.f, 0.f, 0.f), w3c[G::TC];
@@ -172,7 +179,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
         const float4* w3v = reinterpret_cast<const float4*>(a.w3);
         w3d = w3v[dunit];
 #pragma unroll
-        for (int j = 0; j < G::TC; j++) w3c[j] = w3v[32 * ((NT2 >= 2 ? wc : 0) * G::TC + j) + r];
+        for (int j = 0; j < G::TC; j++) w3c[j] = w3v[c0 + 32 * ((G::NT2h >= 2 ? wc : 0) * G::TC + j) + r];
     }
     // d2 = act'(a2) (W3 g) exactly as grad_kernel forms it: fl(g0 w0), three fmaf, times 1.0 or 0.0
     const auto d2_of = [](const float4 g, const float4 w, bool m) {
@@ -211,7 +218,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
                 for (int e = 0; e < 8; e++) gk[e] = gv[8 * h + e];
 #pragma unroll
                 for (int j = 0; j < G::TC; j++) {
-                    const uint32_t m = (uint32_t)mw[32 * (wc * G::TC + j) + r] >> (8 * h);
+                    const uint32_t m = (uint32_t)mw[c0 + 32 * (wc * G::TC + j) + r] >> (8 * h);
                     float v[8];
 #pragma unroll
                     for (int e = 0; e < 8; e++) v[e] = d2_of(gk[e], w3c[j], (m >> e) & 1u);
@@ -249,7 +256,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
                 }
 #pragma unroll
                 for (int j = 0; j < G::TC; j++) {   // mask bits 8h .. 8h+7 of unit n as bf16 1.0 (0x3F80) / 0
-                    const uint32_t m = (uint32_t)mw[32 * (wc * G::TC + j) + r] >> (8 * h);
+                    const uint32_t m = (uint32_t)mw[c0 + 32 * (wc * G::TC + j) + r] >> (8 * h);
                     u32x4 q;
 #pragma unroll
                     for (int e = 0; e < 4; e++)
@@ -358,25 +365,25 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     if (rows_mine && cols_mine) {
 #pragma unroll
         for (int j = 0; j < G::TC; j++) {
-            const float ws = MODE == 1 ? a.w3[32 * (wc * G::TC + j) + r] : 1.0f;
+            const float ws = MODE == 1 ? a.w3[c0 + 32 * (wc * G::TC + j) + r] : 1.0f;
 #pragma unroll
             for (int i = 0; i < G::TR; i++)
 #pragma unroll
                 for (int q = 0; q < 16; q++)
-                    out[(size_t)(32 * (wr * G::TR + i) + acc_row(q, h)) * G::H2 + 32 * (wc * G::TC + j) + r] =
+                    out[(size_t)(32 * (wr * G::TR + i) + acc_row(q, h)) * G::H2 + c0 + 32 * (wc * G::TC + j) + r] =
                         MODE == 1 ? acc[i][j][q] * ws : acc[i][j][q];
         }
     }
-    if (t < G::H2) out[(size_t)G::H1 * G::H2 + t] = MODE == 1 ? dsum * a.w3[t] : dsum;
+    if (t < G::H2h) out[(size_t)G::H1 * G::H2 + dunit] = MODE == 1 ? dsum * a.w3[dunit] : dsum;
 }
 
 template <int NT1, int MODE>
 void launch_nt2(const Dw2Args& a, int nt2, int grid, hipStream_t s) {
-    switch (nt2) {
-        case 1: hipLaunchKernelGGL((dw2_kernel<NT1, 1, MODE>), dim3(grid), dim3(kThreads), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((dw2_kernel<NT1, 2, MODE>), dim3(grid), dim3(kThreads), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((dw2_kernel<NT1, 4, MODE>), dim3(grid), dim3(kThreads), 0, s, a); break;
-        default: hipLaunchKernelGGL((dw2_kernel<NT1, 8, MODE>), dim3(grid), dim3(kThreads), 0, s, a); break;
+    switch (nt2) {   // grid.y = the output column halves (Dw2::CS)
+        case 1: hipLaunchKernelGGL((dw2_kernel<NT1, 1, MODE>), dim3(grid, Dw2<NT1, 1, MODE>::CS), dim3(kThreads), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((dw2_kernel<NT1, 2, MODE>), dim3(grid, Dw2<NT1, 2, MODE>::CS), dim3(kThreads), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((dw2_kernel<NT1, 4, MODE>), dim3(grid, Dw2<NT1, 4, MODE>::CS), dim3(kThreads), 0, s, a); break;
+        default: hipLaunchKernelGGL((dw2_kernel<NT1, 8, MODE>), dim3(grid, Dw2<NT1, 8, MODE>::CS), dim3(kThreads), 0, s, a); break;
     }
 }
 

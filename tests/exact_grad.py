@@ -336,11 +336,32 @@ def pattern_flip_check_deep(W, b, x, zs, masks, stats: dict, key: str) -> None:
         e_prev, a_prev = e, torch.relu(z)
 
 
+def deep_kernel_masks(agent, P, boards, out_dim: int):
+    """The ReLU pattern of every hidden layer as g2048_deep_policy / g2048_deep_grad compute it, read through
+    g2048_deep_hidden (bool [m, h_l] per layer)."""
+    from rl2048_amd import _lib as L
+
+    dspec = agent._deep_spec(P, out_dim)
+    obs_code, hidden, act, harr = dspec
+    packed = agent._pack_deep(P, dspec, "probe%d" % out_dim, out_dim)
+    m = boards.numel()
+    out = []
+    for l, h in enumerate(hidden):
+        Hp = 32 * ((h + 31) // 32)
+        a = torch.empty(m, Hp, dtype=torch.float32, device=boards.device)
+        L.check(L.lib().g2048_deep_hidden(L.ptr(packed), len(hidden), harr, act, obs_code,
+                                          float(agent.env_config.obs_log2_scale), L.ptr(boards), m, l, L.ptr(a), Hp,
+                                          L.stream_handle(boards.device)))
+        out.append(a[:, :h] > 0)
+    return out
+
+
 def exact_update_grads_deep(agent, batch, params, patterns: str | None = "plain", flip_stats: dict | None = None):
     """Pre-clip gradients {"actor", "critic"} of update_batch on `batch` in fp64 for a net of ANY depth and obs
     (one-hot included), the obs materialised by g2048_obs.  patterns="plain": the ReLU pattern of the product's own
     fp32 path (ReinforceAgent._forward_kept_steps on the same chunks: the one-hot gather + hipBLASLt GEMMs), imposed
-    on the fp64 evaluation; flip_stats: also bound that pattern against fp64's own (pattern_flip_check_deep).
+    on the fp64 evaluation; patterns="deep": the pattern of the fused deep kernels (deep_kernel_masks); flip_stats:
+    also bound that pattern against fp64's own (pattern_flip_check_deep).
     Covers the configurations the GPU tests use: MSE / Huber critic, baselines off / batch / batch_norm, no
     augmentation, no rank weights."""
     from rl2048_amd.agent import _Steps
@@ -367,6 +388,8 @@ def exact_update_grads_deep(agent, batch, params, patterns: str | None = "plain"
     def masks_of(P, sel):
         if patterns is None or act != "ReLU":
             return None
+        if patterns == "deep":      # the fused kernels' own forward (g2048_deep_hidden: the same code path)
+            return deep_kernel_masks(agent, P, steps.boards_at(sel, 0), 1 if P is critic_p else 4)
         with torch.no_grad():
             _, kept, _, _ = agent._forward_kept_steps(P, steps, sel, 0)
         return [a > 0 for a in kept[1:]]

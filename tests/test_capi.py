@@ -32,7 +32,8 @@ def test_header_declares_expected_api():
         "g2048_policy_pack", "g2048_policy", "g2048_rollout", "g2048_grad_packed_size", "g2048_grad_partial_size",
         "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2",
         "g2048_fold_partials", "g2048_dw2_factored", "g2048_dw2_actor", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
-        "g2048_deep_rollout", "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1"])
+        "g2048_deep_rollout", "g2048_deep_hidden", "g2048_deep_grad_pack_size", "g2048_deep_grad_slab",
+        "g2048_deep_grad_pack", "g2048_deep_grad", "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1"])
 
 
 def test_library_exports_every_declared_symbol(L):

@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--lib", nargs="*", default=[None])
     ap.add_argument("--cols", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--parts", type=int, nargs="*", default=[256])
     args = ap.parse_args()
     import torch
 
@@ -35,31 +36,32 @@ def main():
         lib = L.lib()
         L._inited_devices.clear()
         L.ensure_device(dev)
-        cpp = max(2048, -(-n // (16 * 256)) * 16)
-        nparts = -(-n // cpp)
-        part = torch.empty(nparts, 257, 256, device=dev)
-        s = L.stream_handle(dev)
+        for P in args.parts:
+            cpp = max(2048, -(-n // (16 * P)) * 16)
+            nparts = -(-n // cpp)
+            part = torch.empty(nparts, 257, 256, device=dev)
+            s = L.stream_handle(dev)
 
-        def call():
-            L.check(lib.g2048_dw2(L.ptr(a1t), L.ptr(d2t), 256, 256, n, 0, n, cpp, L.ptr(part), nparts, s))
+            def call():
+                L.check(lib.g2048_dw2(L.ptr(a1t), L.ptr(d2t), 256, 256, n, 0, n, cpp, L.ptr(part), nparts, s))
 
-        for _ in range(3):
-            call()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.reps):
-            call()
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / args.reps * 1e3
-        ub = lambda X: X.reshape(n // 16, 256, 16).permute(1, 0, 2).reshape(256, n)  # noqa: E731 (block layout)
-        A, D = ub(a1t)[:, :cpp].double(), ub(d2t)[:, :cpp].double()
-        ref, bound = A @ D.t(), A.abs() @ D.abs().t()
-        err = float(((part[0, :256].double() - ref).abs() / bound.clamp_min(1e-30)).max())
-        print(json.dumps({"lib": lib_path or "shipped", "cols": n, "us": round(us, 1),
-                          "GBps": round(n * 2052 / us / 1e3, 1),
-                          "tflops_fp32_equiv": round(2 * 256 * 256 * n / us / 1e6, 1),
-                          "max_err_over_sum_abs": err}), flush=True)
+            for _ in range(3):
+                call()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                call()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / args.reps * 1e3
+            ub = lambda X: X.reshape(n // 16, 256, 16).permute(1, 0, 2).reshape(256, n)  # noqa: E731 (block layout)
+            A, D = ub(a1t)[:, :cpp].double(), ub(d2t)[:, :cpp].double()
+            ref, bound = A @ D.t(), A.abs() @ D.abs().t()
+            err = float(((part[0, :256].double() - ref).abs() / bound.clamp_min(1e-30)).max())
+            print(json.dumps({"lib": lib_path or "shipped", "cols": n, "parts": nparts, "us": round(us, 1),
+                              "GBps": round(n * 2052 / us / 1e3, 1),
+                              "tflops_fp32_equiv": round(2 * 256 * 256 * n / us / 1e6, 1),
+                              "max_err_over_sum_abs": err}), flush=True)
 
 
 if __name__ == "__main__":

@@ -11,6 +11,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if "--repo" in sys.argv:   # time another checkout's package (e.g. the round-3 tree) with this script
+    ROOT = os.path.abspath(sys.argv[sys.argv.index("--repo") + 1])
 sys.path.insert(0, ROOT)
 
 FLOP_FWD = 2 * (16 * 256 + 256 * 256 + 256 * 4)      # per sample, actor forward
@@ -24,6 +26,7 @@ def main():
     ap.add_argument("--max-steps", type=int, default=1024)
     ap.add_argument("--repeats", type=int, default=2)
     ap.add_argument("--lib", default=None, help="another build of libg2048 (A/B scripts)")
+    ap.add_argument("--repo", default=None, help="import rl2048_amd from this checkout")
     args = ap.parse_args()
     import numpy as np
     import torch
