@@ -4,7 +4,7 @@
 # tree) and the reference runner config (round-3 checkout = before, this tree = after).  Outputs under gpurun_out/r4c3/.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r4c3
+O=gpurun_out/r4c4
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests/test_gpu_deep.py tests/test_gpu_grad.py tests/test_capi.py tests/test_gpu_ref_fixtures.py \
     -m gpu -v -s -p no:cacheprovider -k "not runner_matches" --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -60 $O/tests.log; exit 1; }
