@@ -139,6 +139,59 @@ def test_argument_validation_without_gpu(L):
     assert lib.g2048_dw2_factored(*dargs) == L.G2048_EINVAL and b"NULL" in lib.g2048_last_error()
 
 
+def test_deep_sizes_and_validation_without_gpu(L):
+    """The any-depth / one-hot entry points (g2048_deep.hip): packed sizes and slab layouts agree with the host's
+    own layout (agent._deep_slab_layout), the coverage limits (<= 4 hidden layers of <= 256 units; the fused
+    gradient: <= 48 dense 32x32 weight-gradient tiles) and the argument checks, all before any launch."""
+    import ctypes
+
+    from rl2048_amd.agent import ReinforceAgent, _round32
+
+    lib = L.lib()
+    arr = lambda hs: (ctypes.c_int32 * len(hs))(*hs)   # noqa: E731
+
+    def packed(obs, hs):
+        t = [_round32(h) // 32 for h in hs]
+        n = (272 * 32 * t[0] if obs == L.OBS_ONEHOT else t[0] * 512) + 32 * t[0]
+        for l in range(1, len(hs)):
+            n += 1024 * t[l] * t[l - 1] + 32 * t[l]
+        return n + 32 * t[-1] * 4 + 4
+
+    for obs, hs in ((L.OBS_ONEHOT, [256, 128, 64]), (L.OBS_LOG2, [40, 33, 20, 10]), (L.OBS_RAW, [1]),
+                    (L.OBS_ONEHOT, [128, 64])):
+        assert lib.g2048_deep_packed_size(obs, len(hs), arr(hs)) == packed(obs, hs), (obs, hs)
+    for obs, hs in ((L.OBS_LOG2, [16] * 5), (L.OBS_LOG2, [257]), (L.OBS_LOG2, [0, 8]), (7, [32])):
+        assert lib.g2048_deep_packed_size(obs, len(hs), arr(hs)) == -1, (obs, hs)
+    # the fused gradient's partial slab == the layout the host folds it with; nets past its tile budget -> -1
+    for obs, hs in ((L.OBS_ONEHOT, [256, 128, 64]), (L.OBS_LOG2, [64, 48, 32]), (L.OBS_RAW, [40, 33, 20, 10]),
+                    (L.OBS_LOG2, [128, 128, 128])):
+        pw, pb = ReinforceAgent._deep_slab_layout(hs, obs == L.OBS_ONEHOT)
+        assert lib.g2048_deep_grad_slab(obs, len(hs), arr(hs)) == pb[-1] + 4, (obs, hs)
+        t = [_round32(h) // 32 for h in hs]
+        nb = sum(t[l] * t[l - 1] * 1024 for l in range(1, len(hs)))
+        assert lib.g2048_deep_grad_pack_size(obs, len(hs), arr(hs)) == max(nb, 1)
+    for obs, hs in ((L.OBS_ONEHOT, [256, 256, 256]), (L.OBS_LOG2, [256, 256]), (L.OBS_LOG2, [32] * 5)):
+        assert lib.g2048_deep_grad_slab(obs, len(hs), arr(hs)) == -1, (obs, hs)
+    assert lib.g2048_onehot_dw1_slab(256) == 273 * 256 and lib.g2048_onehot_dw1_slab(0) == -1
+    assert lib.g2048_onehot_dw1_slab(257) == -1
+    p = ctypes.c_void_p(8)
+    hs = arr([32, 32])
+    assert lib.g2048_deep_pack(p, p, L.OBS_LOG2, 5, arr([32] * 5), 4, p, 1 << 20, None) == L.G2048_EINVAL
+    assert b"hidden layers" in lib.g2048_last_error()
+    assert lib.g2048_deep_pack(p, p, L.OBS_LOG2, 2, hs, 3, p, 1 << 20, None) == L.G2048_EINVAL
+    assert b"output width" in lib.g2048_last_error()
+    assert lib.g2048_deep_pack(p, p, L.OBS_LOG2, 2, hs, 4, p, 10, None) == L.G2048_EINVAL
+    assert b"too small" in lib.g2048_last_error()
+    assert lib.g2048_deep_grad_pack(p, L.OBS_LOG2, 2, hs, p, 10, None) == L.G2048_EINVAL
+    assert lib.g2048_onehot_layer1(p, p, 32, 7, p, 4, 32, p, None) == L.G2048_EINVAL
+    assert b"activation" in lib.g2048_last_error()
+    assert lib.g2048_onehot_layer1(p, p, 32, L.ACT_RELU, p, 4, 16, p, None) == L.G2048_EINVAL   # ld < h1
+    assert lib.g2048_onehot_dw1(p, p, 64, 100, 64, 30, p, 3, None) == L.G2048_EINVAL           # 3 != ceil(100/30)
+    assert b"nparts" in lib.g2048_last_error()
+    assert lib.g2048_onehot_dw1(p, p, 300, 100, 300, 30, p, 4, None) == L.G2048_EINVAL
+    assert lib.g2048_onehot_layer1(p, p, 32, L.ACT_RELU, None, 0, 32, None, None) == L.G2048_OK   # m == 0: no-op
+
+
 def test_config_validation_messages():
     from rl2048_amd.config import Game2048EnvConfig, env_cfg_struct
 
