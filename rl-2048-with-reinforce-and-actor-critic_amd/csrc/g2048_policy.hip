@@ -16,6 +16,7 @@
 // exact: a padded unit's outgoing weights are zero.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 
 #include "g2048.h"
 #include "g2048_core.h"
@@ -1096,8 +1097,425 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------- gradient, cooperative
+// grad_coop_kernel: grad_kernel's computation and outputs (a1^T columns, d2^T columns or records, the per-row
+// partials) with the 4 waves of a workgroup splitting each 32-sample group's MFMAs instead of each wave taking a group
+// of its own.  Wave w owns the layer-1 / input-delta tiles and the layer-2 output tiles congruent to w mod 4; the
+// layer-1 activations and d2 are exchanged through LDS in B-fragment order and the partial logits through LDS (four
+// workgroup barriers per group).  A wave then holds a quarter of grad_kernel's per-group registers, so TWO
+// workgroups run per CU (2 waves per SIMD): one workgroup's MFMAs run while the other's epilogues, softmax, column
+// stores and barriers do, where grad_kernel's single wave per SIMD leaves the MFMAs idle for those phases (the
+// rollout kernel's arrangement).  Dynamic LDS (CoopLds: 74 KiB at 256 x 256).  Partials: workgroup b writes rows 2b
+// and 2b + 1 -- wave w adds its own tiles' entries to row 2b + (w >> 1) and (unless accumulating) zeros the same
+// entries of the other row -- so the row count is g2048_actor_grad_waves() as for grad_kernel.  The logits are the
+// sum of the four waves' partials in wave order (grad_kernel sums the output tiles in order), so the two kernels'
+// forwards round differently; each is checked against fp64 under its own ReLU pattern (tests/exact_grad.py).
+template <int NT1, int NT2>
+struct CoopLds {
+    static constexpr PolLayout P = pol_layout(NT1, NT2);
+    static constexpr int kA = NT1 * 1024 > 4 * 32 * 33 ? NT1 * 1024 : 4 * 32 * 33;   // h1f, later the transpose tiles
+    static constexpr int oD2 = kA;                                                   // d2f [NT2][4][64] float4
+    static constexpr int oPart = oD2 + NT2 * 1024;                                   // [4][32][4] partial logits
+    static constexpr int oG = oPart + 4 * 32 * 4;                                    // [4][32][4] per-wave g
+    static constexpr int oB1 = oG + 4 * 32 * 4;                                      // b1p
+    static constexpr int oB2 = oB1 + (int)(P.w2f - P.b1p);                           // b2p, w3p, b3
+    static constexpr int kFloats = oB2 + (int)(P.total - P.b2p);
+    static constexpr int kBytes = kFloats * 4;
+};
+
+template <int NT1, int NT2, int ACT, int OBS, int FAC>
+__global__ void __launch_bounds__(kPolBlock, 2) grad_coop_kernel(GradArgs a) {
+    static_assert(NT1 % 4 == 0 && NT2 % 4 == 0, "every wave owns NT / 4 tiles of each layer");
+    typedef float floatx4 __attribute__((ext_vector_type(4)));
+    using C = CoopLds<NT1, NT2>;
+    constexpr int H1p = 32 * NT1, H2p = 32 * NT2, KO1 = NT1 / 4, KO2 = NT2 / 4;
+    constexpr int KF = KO2 * NT1, KB = KO1 * NT2;     // this wave's forward / input-delta k-tiles
+    extern __shared__ float coop_lds[];
+    float4* h1f = reinterpret_cast<float4*>(coop_lds);              // [t][q][lane]: registers 4q..4q+3 of a1 tile t
+    float4* d2f = reinterpret_cast<float4*>(coop_lds + C::oD2);     // [t2][q][lane]: the same for d2
+    float (*part)[32][4] = reinterpret_cast<float (*)[32][4]>(coop_lds + C::oPart);
+    float (*gs)[32][4] = reinterpret_cast<float (*)[32][4]>(coop_lds + C::oG);
+    const float* b1p = coop_lds + C::oB1;
+    const float* b2p = coop_lds + C::oB2;
+    const float* w3p = b2p + (C::P.w3p - C::P.b2p);
+    const float* b3 = b2p + (C::P.b3 - C::P.b2p);
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int l16 = lane & 15, q16 = lane >> 4;
+    float (*T)[33] = reinterpret_cast<float (*)[33]>(coop_lds + w * 32 * 33);   // inside h1f: used after layer 2
+    for (int k = threadIdx.x; k < C::kFloats - C::oB1; k += kPolBlock)
+        coop_lds[C::oB1 + k] = k < C::oB2 - C::oB1 ? a.net[C::P.b1p + k] : a.net[C::P.b2p + (k - (C::oB2 - C::oB1))];
+    // this wave's layer-1 A fragments (tiles w + 4k), resident for the whole launch
+    float w1own[KO1][8];
+#pragma unroll
+    for (int k = 0; k < KO1; k++)
+#pragma unroll
+        for (int s = 0; s < 8; s++) w1own[k][s] = a.net[C::P.w1f + ((w + 4 * k) * 8 + s) * 64 + lane];
+    // The wave-dependent parts of every address go into per-wave bases (fragment resources starting at the wave's
+    // first own tile, the column offset advanced by its first own row block), so the per-fragment / per-row offsets
+    // are compile-time constants: with `w` in them the compiler hoists ~150 distinct scalar offsets out of the
+    // group loop and spills them.
+    const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.net + C::P.w2f + (size_t)w * NT1 * 1024), 0, (NT2 - w) * NT1 * 1024 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rwb = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.w2b + (size_t)w * NT2 * 1024), 0, (NT1 - w) * NT2 * 1024 * 4, 0x00020000);
+    const uint32_t fvo = (uint32_t)lane * 16u;
+    constexpr uint32_t RB = 32u * (NT1 > NT2 ? NT1 : NT2);
+    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc(a.a1t, 0, (int)(RB * a.ld * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd2 = __builtin_amdgcn_make_buffer_rsrc(
+        a.d2t, 0, FAC ? (int)((a.ld >> 4) * 1024u) : (int)(RB * a.ld * 4u), 0x00020000);
+    floatx4 dw1acc[2 * KO1], dw3acc[2 * KO2];
+#pragma unroll
+    for (int k = 0; k < 2 * KO1; k++) dw1acc[k] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < 2 * KO2; k++) dw3acc[k] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    float db1r[KO1];
+#pragma unroll
+    for (int k = 0; k < KO1; k++) db1r[k] = 0.0f;
+    float gsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // db3 (wave 0, lanes of half 0)
+    // this wave's fragment stream: the forward's (own output tile w + 4 k2, k-tile) pairs, then the input delta's
+    // (own input tile w + 4 k1, k-tile), relative to the per-wave bases; past the end: fragment 0 again (unused)
+    const auto stream_frag = [&](int i, int q) -> float4 {
+        if (i < KF) return frag_load(rw2, fvo, (uint32_t)((4 * (i / NT1) * NT1 + i % NT1) * 4 + q));
+        if (i < KF + KB) {
+            const int ii = i - KF;
+            return frag_load(rwb, fvo, (uint32_t)((4 * (ii / NT2) * NT2 + ii % NT2) * 4 + q));
+        }
+        return frag_load(rw2, fvo, (uint32_t)q);
+    };
+    for (uint32_t gi = blockIdx.x; gi < a.ngroups; gi += gridDim.x) {   // workgroup-uniform
+        const uint32_t j = gi * 32u + (uint32_t)col;
+        asm volatile("" ::: "memory");
+        const uint32_t cj = a.col_off + j;
+        // this lane's column, rows 4h + 32 w (the wave's first own row block) on: own rows are 32 (4 k) + acc_row
+        const uint32_t off = (((cj >> 4) * RB + 4u * (uint32_t)h + 32u * (uint32_t)w) * 16u + (cj & 15u)) * 4u;
+        uint32_t ld4 = 64u;
+        const bool valid = j < a.n;
+        const uint64_t b = valid ? a.boards[j] : 0ull;
+        const uint32_t act = (valid && !a.critic) ? a.actions[j] : 0u;
+        const float cf = valid ? a.coef[j] : 0.0f;
+        float4 fa[4], fn[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            fa[q] = stream_frag(0, q);
+            fn[q] = stream_frag(1, q);
+        }
+        __syncthreads();   // every wave is done with the previous group's transpose tiles (in h1f) and d2f
+        // ---- layer 1: own tiles, kept in registers and published to h1f
+        float a1own[KO1][16];
+        {
+            float x[8];
+#pragma unroll
+            for (int s = 0; s < 8; s++) x[s] = obs_value<OBS>(b, 2 * s + h, a.obs_scale);
+#pragma unroll
+            for (int k = 0; k < KO1; k++) {
+                const int t = w + 4 * k;
+                floatx16 acc = {};
+#pragma unroll
+                for (int s = 0; s < 8; s++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1own[k][s], x[s], acc, 0, 0, 0);
+                const float4* bb = reinterpret_cast<const float4*>(b1p + (t * 2 + h) * 16);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4 bv = bb[q];
+                    a1own[k][4 * q + 0] = activate<ACT>(acc[4 * q + 0] + bv.x);
+                    a1own[k][4 * q + 1] = activate<ACT>(acc[4 * q + 1] + bv.y);
+                    a1own[k][4 * q + 2] = activate<ACT>(acc[4 * q + 2] + bv.z);
+                    a1own[k][4 * q + 3] = activate<ACT>(acc[4 * q + 3] + bv.w);
+                    h1f[(t * 4 + q) * 64 + lane] = make_float4(a1own[k][4 * q + 0], a1own[k][4 * q + 1],
+                                                               a1own[k][4 * q + 2], a1own[k][4 * q + 3]);
+                }
+            }
+        }
+        __syncthreads();   // h1f complete
+        // ---- layer 2: own output tiles (B = a1 from LDS, A streamed), folded into partial logits; the own a1
+        //      columns are stored through it (kS1 per k-tile)
+        constexpr int kS1 = (KO1 * 16 + KF - 1) / KF;
+        float h2[KO2][16];
+        float lgp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k2 = 0; k2 < KO2; k2++) {
+            const int o = w + 4 * k2;
+            floatx16 acc = {};
+#pragma unroll
+            for (int tt = 0; tt < NT1; tt++) {
+                const int i = k2 * NT1 + tt;
+                float4 fb[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) fb[q] = stream_frag(i + 2, q);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4 hb = h1f[(tt * 4 + q) * 64 + lane];
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, hb.x, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, hb.y, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, hb.z, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, hb.w, acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int v = i * kS1; v < (i + 1) * kS1; v++)
+                    if (v < KO1 * 16) {
+                        opaque_sgpr(ld4);
+                        col_store(ra1, 128 * (v / 16) + acc_row(v % 16, 0), ld4, off, a1own[v / 16][v % 16]);
+                    }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    fa[q] = fn[q];
+                    fn[q] = fb[q];
+                }
+            }
+            const float4* bb = reinterpret_cast<const float4*>(b2p + (o * 2 + h) * 16);
+            const float4* w3 = reinterpret_cast<const float4*>(w3p + (o * 2 + h) * 64);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 bv = bb[q];
+                h2[k2][4 * q + 0] = activate<ACT>(acc[4 * q + 0] + bv.x);
+                h2[k2][4 * q + 1] = activate<ACT>(acc[4 * q + 1] + bv.y);
+                h2[k2][4 * q + 2] = activate<ACT>(acc[4 * q + 2] + bv.z);
+                h2[k2][4 * q + 3] = activate<ACT>(acc[4 * q + 3] + bv.w);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const float4 wv = w3[4 * q + u];
+                    lgp[0] = fmaf(h2[k2][4 * q + u], wv.x, lgp[0]);
+                    lgp[1] = fmaf(h2[k2][4 * q + u], wv.y, lgp[1]);
+                    lgp[2] = fmaf(h2[k2][4 * q + u], wv.z, lgp[2]);
+                    lgp[3] = fmaf(h2[k2][4 * q + u], wv.w, lgp[3]);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) lgp[k] += __shfl_xor(lgp[k], 32, 64);
+        if (h == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) part[w][col][k] = lgp[k];
+        }
+        __syncthreads();   // partial logits complete; h1f is free from here (the transpose tiles live in it)
+        float lg[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) lg[k] = (((part[0][col][k] + part[1][col][k]) + part[2][col][k]) + part[3][col][k]) + b3[k];
+        float g[4];
+        if (!a.critic) {
+            const uint32_t mw = a.use_mask ? mask_word_of(b) : 0x01010101u;
+            float l[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) l[k] = ((mw >> (8 * k)) & 0xFFu) ? lg[k] : -1e9f;
+            const float mx = fmaxf(fmaxf(l[0], l[1]), fmaxf(l[2], l[3]));
+            float e[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) e[k] = expf(l[k] - mx);
+            const float es = ((e[0] + e[1]) + e[2]) + e[3];
+#pragma unroll
+            for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf;
+        } else {
+            const float tg = valid ? a.target[j] : 0.0f;
+            const float diff = lg[0] - tg;
+            const float gd = (a.huber && fabsf(diff) > a.huber_delta) ? copysignf(a.huber_delta, diff) : diff;
+            g[0] = gd * cf;
+            g[1] = g[2] = g[3] = 0.0f;
+            if (valid && w == 0 && h == 0 && a.delta_out) a.delta_out[j] = tg - lg[0];
+            if (valid && w == 0 && h == 0 && a.v_out) a.v_out[j] = lg[0];
+        }
+        if (h == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (w == 0) gsum[k] += g[k];
+                gs[w][col][k] = g[k];
+            }
+        }
+        // ---- dW3 += a2^T g over the own h2 tiles (a2 transposed through this wave's tile, 16x16x4 MFMAs)
+#pragma unroll
+        for (int k2 = 0; k2 < KO2; k2++) {
+            lds_fence();
+#pragma unroll
+            for (int r = 0; r < 16; r++) T[acc_row(r, h)][col] = h2[k2][r];
+            lds_fence();
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) {
+                const int s = 4 * kk + q16;
+                const float av = l16 < 4 ? gs[w][s][l16 & 3] : 0.0f;
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+                    dw3acc[2 * k2 + c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, T[16 * c + l16][s], dw3acc[2 * k2 + c], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- d2 = act'(a2) * (W3 g) over the own tiles -> d2f (and the records' mask words / g)
+        if constexpr (FAC == 1) {
+            if (w == 0 && h == 0)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g[0]), rd2, (int)((cj >> 4) * 1024u + 512u + (cj & 15u) * 4u),
+                                                      0, 0);
+        } else if constexpr (FAC == 2) {
+            if (w == 0 && h == 0) {
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 gv = {__float_as_uint(g[0]), __float_as_uint(g[1]), __float_as_uint(g[2]), __float_as_uint(g[3])};
+                __builtin_amdgcn_raw_buffer_store_b128(gv, rd2, (int)((cj >> 4) * 1024u + 512u + (cj & 15u) * 16u), 0, 0);
+            }
+        }
+#pragma unroll
+        for (int k2 = 0; k2 < KO2; k2++) {
+            const int o = w + 4 * k2;
+            if constexpr (FAC) {
+                uint32_t mv = 0u;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const uint64_t bal = __ballot(h2[k2][r] > 0.0f);
+                    const uint32_t hw = (uint32_t)(bal >> (32 * ((lane >> 1) & 1)));
+                    const uint32_t pt = (hw >> (16 * (lane & 1))) & 0xFFFFu;
+                    mv = (lane >> 2) == r ? pt : mv;
+                }
+                const uint32_t unit = 32u * (uint32_t)o + (uint32_t)acc_row(lane >> 2, (lane >> 1) & 1);
+                const uint32_t blk = ((a.col_off + gi * 32u) >> 4) + (uint32_t)(lane & 1);
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)mv, rd2, (int)(blk * 1024u + unit * 2u), 0, 0);
+            }
+            const float4* w3 = reinterpret_cast<const float4*>(w3p + (o * 2 + h) * 64);
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const float4 wv = w3[r];
+                float dh = g[0] * wv.x;
+                dh = fmaf(g[1], wv.y, dh);
+                dh = fmaf(g[2], wv.z, dh);
+                dh = fmaf(g[3], wv.w, dh);
+                h2[k2][r] = dh * activation_derivative<ACT>(h2[k2][r]);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                d2f[(o * 4 + q) * 64 + lane] = make_float4(h2[k2][4 * q + 0], h2[k2][4 * q + 1], h2[k2][4 * q + 2], h2[k2][4 * q + 3]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();   // d2f complete
+        // ---- d1 = act'(a1) * (W2 d2) over the own input tiles (B = d2 from LDS), then db1 and dW1 += x^T d1;
+        //      the own d2 columns (FAC 0) are stored through it (kS2 per k-tile)
+        float xa[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const uint64_t bs = shfl64_(b, 4 * kk + q16);
+            xa[kk] = obs_value<OBS>(bs, l16, a.obs_scale);
+        }
+        constexpr int kS2 = (KO2 * 16 + KB - 1) / KB;
+#pragma unroll
+        for (int k1 = 0; k1 < KO1; k1++) {
+            floatx16 acc = {};
+#pragma unroll
+            for (int t2 = 0; t2 < NT2; t2++) {
+                const int i = k1 * NT2 + t2;
+                float4 fb[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) fb[q] = stream_frag(KF + i + 2, q);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4 db = d2f[(t2 * 4 + q) * 64 + lane];
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, db.x, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, db.y, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, db.z, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, db.w, acc, 0, 0, 0);
+                }
+                if constexpr (!FAC) {
+#pragma unroll
+                    for (int v = i * kS2; v < (i + 1) * kS2; v++)
+                        if (v < KO2 * 16) {
+                            opaque_sgpr(ld4);
+                            col_store(rd2, 128 * (v / 16) + acc_row(v % 16, 0), ld4, off, h2[v / 16][v % 16]);
+                        }
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    fa[q] = fn[q];
+                    fn[q] = fb[q];
+                }
+            }
+            lds_fence();
+#pragma unroll
+            for (int r = 0; r < 16; r++) T[acc_row(r, h)][col] = acc[r] * activation_derivative<ACT>(a1own[k1][r]);
+            lds_fence();
+            float bs = 0.0f;   // db1 of unit col of this tile: samples 16h .. 16h + 15, then both halves
+#pragma unroll
+            for (int s = 0; s < 16; s++) bs += T[col][16 * h + s];
+            bs += __shfl_xor(bs, 32, 64);
+            db1r[k1] += bs;
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++)
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+                    dw1acc[2 * k1 + c] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[kk], T[16 * c + l16][4 * kk + q16],
+                                                                            dw1acc[2 * k1 + c], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // ---- partials: the own tiles' entries into row 2b + (w >> 1), zeros at the same entries of the other row
+    constexpr int64_t PF = grad_part_floats(NT1, NT2);
+    const bool accm = a.part_accum != 0;
+    float* out = a.part + (size_t)(2u * blockIdx.x + (uint32_t)(w >> 1)) * PF;
+    float* oth = a.part + (size_t)(2u * blockIdx.x + 1u - (uint32_t)(w >> 1)) * PF;
+    const auto put = [&](int64_t idx, float v) {
+        out[idx] = (accm ? out[idx] : 0.0f) + v;
+        if (!accm) oth[idx] = 0.0f;
+    };
+#pragma unroll
+    for (int k1 = 0; k1 < KO1; k1++)
+#pragma unroll
+        for (int c = 0; c < 2; c++)   // block 2 o1 + c: units 16 (2 o1 + c) + l16, feature rows 4 q16 + r
+#pragma unroll
+            for (int r = 0; r < 4; r++) put((int64_t)(4 * q16 + r) * H1p + 16 * (2 * (w + 4 * k1) + c) + l16, dw1acc[2 * k1 + c][r]);
+    if (h == 0) {
+#pragma unroll
+        for (int k1 = 0; k1 < KO1; k1++) put(16 * H1p + 32 * (w + 4 * k1) + col, db1r[k1]);
+    }
+    if (q16 == 0) {                     // rows 0..3 = actions
+#pragma unroll
+        for (int k2 = 0; k2 < KO2; k2++)
+#pragma unroll
+            for (int c = 0; c < 2; c++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) put(17 * H1p + (16 * (2 * (w + 4 * k2) + c) + l16) * 4 + r, dw3acc[2 * k2 + c][r]);
+    }
+    if (w == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            float v = h == 0 ? gsum[k] : 0.0f;
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+            if (lane == 0) put(17 * H1p + 4 * H2p + k, v);
+        }
+    }
+}
+
+// G2048_GRAD_COOP=0 in the environment selects grad_kernel for 256 x 256 nets too (tools/ A/B only)
+bool grad_coop_enabled() {
+    static const int v = [] {
+        const char* e = std::getenv("G2048_GRAD_COOP");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v != 0;
+}
+
+template <int ACT, int OBS, int FAC>
+void launch_coop(const GradArgs& a, int grid, hipStream_t s) {
+    constexpr int kBytes = CoopLds<8, 8>::kBytes;
+    static bool attr_set = false;   // a failure shows as the launch's error (hipGetLastError in the caller)
+    if (!attr_set && hipFuncSetAttribute(reinterpret_cast<const void*>(&grad_coop_kernel<8, 8, ACT, OBS, FAC>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, kBytes) == hipSuccess)
+        attr_set = true;
+    hipLaunchKernelGGL((grad_coop_kernel<8, 8, ACT, OBS, FAC>), dim3(grid), dim3(kPolBlock), (unsigned)kBytes, s, a);
+}
+
+template <int ACT, int FAC>
+void launch_coop_obs(const GradArgs& a, int obs, int grid, hipStream_t s) {
+    if (obs == G2048_OBS_LOG2) launch_coop<ACT, G2048_OBS_LOG2, FAC>(a, grid, s);
+    else launch_coop<ACT, G2048_OBS_RAW, FAC>(a, grid, s);
+}
+
+// grid = one workgroup per CU for grad_kernel (every wave one partial row); the cooperative kernel runs two per CU
+// with two rows per workgroup, the same row count
 template <int NT1, int NT2>
 void launch_grad(const GradArgs& a, int act, int obs, int grid, hipStream_t s) {
+    if constexpr (NT1 == 8 && NT2 == 8) {
+        if (grad_coop_enabled()) {
+            if (act == G2048_ACT_RELU && a.d2_form == 1) launch_coop_obs<0, 1>(a, obs, 2 * grid, s);
+            else if (act == G2048_ACT_RELU && a.d2_form == 2) launch_coop_obs<0, 2>(a, obs, 2 * grid, s);
+            else if (act == G2048_ACT_RELU) launch_coop_obs<0, 0>(a, obs, 2 * grid, s);
+            else launch_coop_obs<1, 0>(a, obs, 2 * grid, s);
+            return;
+        }
+    }
     if (act == G2048_ACT_RELU && a.d2_form == 1) {
         if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_LOG2, 1>), dim3(grid), dim3(kPolBlock), 0, s, a);
         else hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_RAW, 1>), dim3(grid), dim3(kPolBlock), 0, s, a);
