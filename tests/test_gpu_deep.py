@@ -61,6 +61,29 @@ def _fwd64(W, B, x, act):
     return a
 
 
+def _fwd64_bound(W, B, x, act):
+    """fp64 forward and a rigorous bound on an fp32 evaluation's error: every layer's pre-activation is a sum of
+    fan-in + 1 terms, summed in some order with one rounding per operation (the MFMA chain is a k-ordered fmaf chain;
+    the partial sums of the output layer add at most 8 more), so |z^ - z| <= gamma_n (|a^| |W| + |b|) + |W| |a^ - a|
+    with n = fan-in + 10; ReLU passes the error through (Lipschitz 1), Sigmoid scales it by 1/4 and adds its own
+    rounding (expf, one add, one divide: 4 ulp of a)."""
+    u = 2.0 ** -24
+    a, E = x, torch.zeros_like(x)
+    for i, (w, b) in enumerate(zip(W, B)):
+        wd, bd = w.double(), b.double()
+        n = w.shape[0] + 10
+        z = a @ wd + bd
+        Ez = (n * u / (1 - n * u)) * ((a.abs() + E) @ wd.abs() + bd.abs()) + E @ wd.abs()
+        if i == len(W) - 1:
+            return z, Ez
+        if act == "ReLU":
+            a, E = torch.relu(z), Ez
+        else:
+            a = torch.sigmoid(z)
+            E = 0.25 * Ez + 4 * u * a.abs()
+    raise AssertionError("unreachable")
+
+
 def _pack(L, W, B, obs_code, hidden, dout):
     lib = L.lib()
     harr = (ctypes.c_int32 * len(hidden))(*hidden)
@@ -93,11 +116,13 @@ def test_deep_forward_matches_fp64(mode, hidden, act, dout):
     L.check(L.lib().g2048_deep_policy(L.ptr(packed), len(hidden), harr, L.ACT_RELU if act == "ReLU" else L.ACT_SIGMOID,
                                       L.ptr(b), None, None, code, 0.0625, 0, 1, L.RNG_PCG64, None, None, None, 0, None,
                                       None, L.ptr(out), None, n, L.stream_handle(DEV)))
-    ref = _fwd64(W, B, _obs64(e, mode, 0.0625), act)
+    ref, bound = _fwd64_bound(W, B, _obs64(e, mode, 0.0625), act)
     got = out[:, :dout].double()
-    # fp32 accumulation: within a few ulps of the sum of magnitudes of the last layer's inputs
-    err = float((got - ref).abs().max() / ref.abs().max())
-    assert err < 2e-6, err
+    # every output within the fp32 forward-error bound of its fp64 value (raw obs reach 2^15, so a max-normalised
+    # tolerance would not be scale-free)
+    ratio = float(((got - ref).abs() / bound.clamp_min(1e-300)).max())
+    print(f"\n{mode} {hidden} {act}: max |err| / bound = {ratio:.3g}, max rel err {float((got - ref).abs().max() / ref.abs().max()):.3g}")
+    assert ratio <= 1.0, ratio
     if dout == 1:
         assert bool((out[:, 1:] == 0).all())
 
@@ -239,7 +264,10 @@ def test_deep_rollout_suspend_resume_equals_stepwise(env, hidden):
         x, y = getattr(b1, name), getattr(b2, name)
         assert torch.equal(x[valid], y[valid]), name
     assert torch.equal((b1.flags & ~L.F_INACTIVE)[valid], (b2.flags & ~L.F_INACTIVE)[valid])
-    assert torch.equal(b1.probs[valid], b2.probs[valid])
+    if "g2048_deep_policy" in a.last_paths()["rollout"]:   # the same forward code: bit for bit
+        assert torch.equal(b1.probs[valid], b2.probs[valid])
+    else:   # 2 hidden layers step by g2048_policy, whose output layer sums its partials in another order
+        torch.testing.assert_close(b1.probs[valid], b2.probs[valid], rtol=0, atol=2e-6)
     assert torch.equal(b1.total_reward, b2.total_reward) and torch.equal(b1.max_tile, b2.max_tile)
     assert torch.equal(b1.final_boards, b2.final_boards)
     ocfg = {k: v for k, v in env.items()}
