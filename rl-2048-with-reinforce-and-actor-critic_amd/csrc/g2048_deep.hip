@@ -1029,25 +1029,32 @@ __global__ void __launch_bounds__(256) onehot_l1_kernel(const float* __restrict_
 }
 
 // dW1 / db1 partials of a one-hot first layer: block (slice, part) owns units [64 slice, 64 slice + 64) and
-// samples [part * per, ...): acc[17 c + e_c(s)][lane] += d1[s][64 slice + lane] in sample order (one wave, LDS adds
-// in program order: deterministic), then slab rows 0..271 = dW1 and row 272 = db1 of its columns.
+// samples [part * per, ...): acc[17 c + e_c(s)][lane] += d1[s][64 slice + lane] in sample order, then slab rows
+// 0..271 = dW1 and row 272 = db1 of its columns.  The 8 waves of a block share the [272][64] accumulator by cells
+// (wave k: cells 2k, 2k + 1, whose rows no other wave touches), each adding its rows in sample order in program
+// order: deterministic, and the same per-row order as one wave doing all 16 cells.  (One 64-lane wave per block
+// held the CU to two waves -- the accumulator is 68 KiB -- and its LDS read-modify-writes were latency-bound.)
 constexpr int kDw1Rows = kOneHotRows + 1;
 
-__global__ void __launch_bounds__(64) onehot_dw1_kernel(const uint64_t* __restrict__ boards, const float* __restrict__ d1,
-                                                        int h1, int64_t m, int64_t ld, int64_t per,
-                                                        float* __restrict__ part) {
+constexpr int kDw1Waves = 8;   // wave k owns cells 2k, 2k + 1 = accumulator rows [34 k, 34 k + 34)
+__global__ void __launch_bounds__(64 * kDw1Waves) onehot_dw1_kernel(const uint64_t* __restrict__ boards,
+                                                                   const float* __restrict__ d1, int h1, int64_t m,
+                                                                   int64_t ld, int64_t per, float* __restrict__ part) {
     __shared__ float acc[kOneHotRows * 64];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int slice = blockIdx.x, p = blockIdx.y;
     const int j = 64 * slice + lane;
-    for (int r = 0; r < kOneHotRows; r++) acc[r * 64 + lane] = 0.0f;
+    const int r0 = 34 * w;                          // this wave's rows: cells 2w (17 rows) and 2w + 1 (17 rows)
+    for (int r = r0; r < r0 + 34; r++) acc[r * 64 + lane] = 0.0f;
     float db = 0.0f;
     const int64_t s0 = (int64_t)p * per, s1 = s0 + per < m ? s0 + per : m;
     const bool live = j < h1;
+    const uint32_t sh = 8u * (uint32_t)w;           // the two cells' nibbles
     const auto add = [&](uint64_t b, float v) {
-        db += v;
-#pragma unroll
-        for (int c = 0; c < 16; c++) acc[(17 * c + (int)((b >> (4 * c)) & 15u)) * 64 + lane] += v;
+        if (w == 0) db += v;
+        const uint32_t e = (uint32_t)(b >> sh);
+        acc[(r0 + (int)(e & 15u)) * 64 + lane] += v;
+        acc[(r0 + 17 + (int)((e >> 4) & 15u)) * 64 + lane] += v;
     };
     int64_t s = s0;
     for (; s + 4 <= s1; s += 4) {                   // the next 4 samples' loads in flight together
@@ -1064,8 +1071,8 @@ __global__ void __launch_bounds__(64) onehot_dw1_kernel(const uint64_t* __restri
     for (; s < s1; s++) add(boards[s], live ? d1[s * ld + j] : 0.0f);
     float* slab = part + (int64_t)p * kDw1Rows * h1;
     if (live) {
-        for (int r = 0; r < kOneHotRows; r++) slab[(int64_t)r * h1 + j] = acc[r * 64 + lane];
-        slab[(int64_t)kOneHotRows * h1 + j] = db;
+        for (int r = r0; r < r0 + 34; r++) slab[(int64_t)r * h1 + j] = acc[r * 64 + lane];
+        if (w == 0) slab[(int64_t)kOneHotRows * h1 + j] = db;
     }
 }
 
@@ -1435,7 +1442,7 @@ int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m,
     if (nparts != (m + per - 1) / per || nparts > 65535) return dfail(G2048_EINVAL, "one-hot dW1: nparts != ceil(m / per)");
     if (m > 0 && (!boards || !d1 || !partials)) return dfail(G2048_EINVAL, "one-hot dW1: NULL buffer");
     if (m == 0) return G2048_OK;
-    hipLaunchKernelGGL(onehot_dw1_kernel, dim3((h1 + 63) / 64, (unsigned)nparts), dim3(64), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(onehot_dw1_kernel, dim3((h1 + 63) / 64, (unsigned)nparts), dim3(64 * kDw1Waves), 0, (hipStream_t)stream,
                        boards, d1, h1, m, ld, per, partials);
     return check_hip();
 }

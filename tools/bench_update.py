@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--repeats", type=int, default=2)
     ap.add_argument("--lib", default=None, help="another build of libg2048 (A/B scripts)")
     ap.add_argument("--repo", default=None, help="import rl2048_amd from this checkout")
+    ap.add_argument("--no-actor-records", action="store_true",
+                    help="actor d2 as columns + g2048_dw2 instead of d2_form 2 records + g2048_dw2_actor (A/B)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -45,6 +47,8 @@ def main():
         agent = ReinforceAgent(Game2048EnvConfig(max_steps=args.max_steps),
                                MLPConfig(hidden_sizes=[256, 256], activation="ReLU", init_distribution="HeNormal"),
                                ReinforceAgentConfig(baseline_mode="batch", use_critic=args.critic), device=dev)
+        if args.no_actor_records:
+            agent.actor_d2_records = False
         for rep in range(args.repeats + 1):
             base = 1000 + rep * n
             es = np.arange(base, base + n, dtype=np.int64)   # seed arrays (SeedStream.take_array form)
