@@ -269,7 +269,10 @@ class ReinforceAgent:
         # ... and the fused critic per time row, V(s') taken from the next row's pass (large batches)
         self.use_critic_rows = True
         self.critic_factored_d2 = True   # ReLU critic rows: the factored d2 records + g2048_dw2_factored
-        self.actor_d2_records = True     # ReLU actor: d2 block records (mask + g) + g2048_dw2_actor
+        # ReLU actor: d2 block records (mask + g) + g2048_dw2_actor instead of d2 columns + g2048_dw2.  Off: the
+        # rebuild of d2 from 4 values of g adds VALU work to the MFMA-bound g2048_dw2 (configs[2] update 0.817-0.823
+        # against 0.789-0.794 s with the columns, profiles/round4/r4c6/), more than the 1 KiB / sample of HBM saved
+        self.actor_d2_records = False
         self.grad_chunk_steps = 1 << 20
         # diagnostics (tests): called as grad_probe(slot, k, sample_idx, a1_cols, d2_cols) with the column buffers
         # of every fused-gradient launch before they are reused -- sample_idx indexes the batch's valid steps

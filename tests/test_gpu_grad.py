@@ -163,20 +163,23 @@ def _check_fused_vs_plain(runs, act):
     assert all(v < 1e-5 for v in errs_p.values()), errs_p
 
 
-@pytest.mark.parametrize("act", ["Sigmoid", "ReLU"])
+@pytest.mark.parametrize("act,records", [("Sigmoid", False), ("ReLU", False), ("ReLU", True)])
 @pytest.mark.parametrize("chunk", [4096 + 17, 8192 * 17 + 5])
-def test_fused_critic_grad_ragged_chunks(chunk, act):
+def test_fused_critic_grad_ragged_chunks(chunk, act, records):
     """Regression for the round-1 hipErrorIllegalAddress seen after the 256x256 critic's V(s') launch
     ("Fault audit"): every chunk of the fused critic + actor gradient is ragged (m not a
     multiple of 32, so the last 32-sample group of each launch is partial), the last chunk is short, and the
     second size makes the split-K layer-2 GEMM run P = 17 column blocks; the device stays healthy (a
-    synchronising copy after each update).  Gradients: _check_fused_vs_plain (1e-5)."""
+    synchronising copy after each update).  records: the actor's d2 as block records (g2048_actor_grad d2_form 2 +
+    g2048_dw2_actor; measured slower than the columns, so off by default) instead of columns.  Gradients:
+    _check_fused_vs_plain (1e-5)."""
     acfg = dict(baseline_mode="batch", optimizer="sgd", gamma=0.97, use_critic=True, critic_loss_type="mse")
     runs = {}
     batch = None
     for mode in ("fused", "plain"):
         ag = _agent((256, 256), act, **acfg)
         ag.use_fused_grad = mode == "fused"
+        ag.actor_d2_records = records
         if batch is None:
             batch = ag.rollout_batch(list(range(3000, 3000 + 1200)), list(range(7000, 7000 + 1200)))
             runs["batch"] = batch
