@@ -548,20 +548,24 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArg
 // ------------------------------------------------------------------------------------ update (fused, any depth)
 // The actor / critic branch of update_batch (src/reinforce_agent.py:403-555; _backpropagation :639-678) for a net
 // of any depth whose dense weight-gradient tiles fit the workgroup's accumulator registers (see kGradTilesPerWave):
-// one 256-thread workgroup per CU takes 32 samples at a time --
+// one 512-thread workgroup (8 waves, 2 per SIMD) per CU takes 32 samples at a time --
 //   * forward as deep_forward, every hidden layer's activations kept in LDS ([unit][sample], stride 33);
 //   * g = (onehot(a) - p) coef (actor: masked softmax of the logits) or dL/dV coef (critic: MSE / Huber on V - target);
 //   * output layer on VALU: dW_out += a^T g per thread (unit = thread), delta = (W_out g) act'(a) in place;
 //   * each dense layer l (top down): dW_l += a_{l-1}^T delta_l on v_mfma_f32_32x32x2_f32 with the 32 samples as the
 //     contraction (A = a_{l-1}, B = delta_l, both from LDS), accumulated in registers across the workgroup's groups
-//     (tile f of the flattened tile list belongs to wave f % 4); then delta_{l-1} = (W_l delta_l) act'(a_{l-1}) as
+//     (tile f of the flattened tile list belongs to wave f % 8); then delta_{l-1} = (W_l delta_l) act'(a_{l-1}) as
 //     the forward's MFMA chain on the backward fragments (W_l in A-fragment order, streamed from L2), written over
 //     a_{l-1} in LDS;
 //   * first layer: log2 / raw obs: dW_0 += x^T delta_0 on MFMA (x rebuilt from the boards); one-hot obs: delta_0 is
 //     written out ([n][H0p], row-major) for g2048_onehot_dw1's scatter;
 //   * biases: per-thread sums (unit = thread).
 // Every workgroup writes one fp32 partial slab (g2048_fold_partials sums them in fp64).
-constexpr int kGradTilesPerWave = 12;   // dense dW tiles per wave held in AGPRs (x 16 floats)
+// 8 waves x 6 dense dW tiles held in accumulator registers (x 16 floats): two waves per SIMD, so one wave's MFMA
+// chains run while the other's gathers, epilogues and barriers do (a 4-wave workgroup with 12 tiles per wave took
+// the whole register file, one wave per SIMD)
+constexpr int kDeepGradWaves = 8, kDeepGradBlock = 64 * kDeepGradWaves;
+constexpr int kGradTilesPerWave = 6;
 
 struct DeepGradArgs {
     DeepNet net;
@@ -596,7 +600,7 @@ __device__ __forceinline__ float act_deriv(float a) {   // from the activation (
 }
 
 template <int OBS, int ACT>
-__global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a) {
+__global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradArgs a) {
     extern __shared__ float dyn[];
     const DeepNet& net = a.net;
     const int L = net.L;
@@ -609,12 +613,13 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
     float (*gs)[4] = reinterpret_cast<float (*)[4]>(lds_end + 8 * 32 * 4);       // [32][4]
     uint64_t* bds = reinterpret_cast<uint64_t*>(lds_end + 8 * 32 * 4 + 32 * 4);  // [32]
     float* dbs = lds_end + 8 * 32 * 4 + 32 * 4 + 64;                             // [kMaxHidden][256]: db_l of unit tid
-    for (int l = 0; l < kMaxHidden; l++) dbs[l * 256 + tid] = 0.0f;
+    if (tid < 256)
+        for (int l = 0; l < kMaxHidden; l++) dbs[l * 256 + tid] = 0.0f;
     const float* P = a.packed;
     floatx16 acc[kGradTilesPerWave];
 #pragma unroll
     for (int k = 0; k < kGradTilesPerWave; k++) acc[k] = floatx16{};
-    floatx16 acc0[2] = {floatx16{}, floatx16{}};   // log2 / raw first layer: dW_0^T tiles t = w, w + 4
+    floatx16 acc0 = {};   // log2 / raw first layer: dW_0^T tile t = w
     float dwo[4] = {0.f, 0.f, 0.f, 0.f}, dbo = 0.f;   // dW_out row tid; db_out (threads 0..3: output tid)
     const int HL = 32 * net.nt[L - 1];
     const float4* wout = reinterpret_cast<const float4*>(P + net.w[L]);
@@ -629,19 +634,20 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
             float* out = actl(0);
             const int nt0 = net.nt[0];
             if constexpr (OBS == G2048_OBS_ONEHOT) {
-                const int bb = 8 * w + (lane >> 3), k = lane & 7;
+                // waves w and w + 4: boards 8 (w & 3) .. + 7, 8 lanes per board; tiles 4 (w >> 2) .. + 3
+                const int bb = 8 * (w & 3) + (lane >> 3), k = lane & 7, m0 = 4 * (w >> 2);
                 const uint64_t b = bds[bb];
                 const int H = 32 * nt0;
-                const float* tab = P + net.w[0] + 4 * k;
-                float4 ac[8];
+                const float* tab = P + net.w[0] + 4 * k + 32 * m0;
+                float4 ac[4];
 #pragma unroll
-                for (int m = 0; m < 8; m++) ac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int m = 0; m < 4; m++) ac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 4
                 for (int c = 0; c < 16; c++) {
                     const float* row = tab + (int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * H;
 #pragma unroll
-                    for (int m = 0; m < 8; m++) {
-                        if (m < nt0) {
+                    for (int m = 0; m < 4; m++) {
+                        if (m0 + m < nt0) {
                             const float4 v = *reinterpret_cast<const float4*>(row + 32 * m);
                             ac[m].x += v.x;
                             ac[m].y += v.y;
@@ -651,9 +657,9 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
                     }
                 }
 #pragma unroll
-                for (int m = 0; m < 8; m++) {
-                    if (m < nt0) {
-                        const int u = 32 * m + 4 * k;
+                for (int m = 0; m < 4; m++) {
+                    if (m0 + m < nt0) {
+                        const int u = 32 * (m0 + m) + 4 * k;
                         const float4 bv = *reinterpret_cast<const float4*>(P + net.b[0] + u);
                         out[(u + 0) * kActStride + bb] = activate<ACT>(ac[m].x + bv.x);
                         out[(u + 1) * kActStride + bb] = activate<ACT>(ac[m].y + bv.y);
@@ -667,7 +673,7 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
 #pragma unroll
                 for (int s2 = 0; s2 < 8; s2++) x[s2] = obs_value<OBS>(b, 2 * s2 + h, a.obs_scale);
                 const float* w1f = P + net.w[0];
-                for (int t = w; t < nt0; t += 4) {
+                for (int t = w; t < nt0; t += kDeepGradWaves) {
                     floatx16 c = {};
 #pragma unroll
                     for (int s2 = 0; s2 < 8; s2++)
@@ -689,7 +695,7 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
             const int ntin = net.nt[l - 1], ntout = net.nt[l];
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(P + net.w[l]) + lane;
             const float* bias = P + net.b[l];
-            for (int o = w; o < ntout; o += 4) {
+            for (int o = w; o < ntout; o += kDeepGradWaves) {
                 floatx16 c = {};
                 const float4* fo = frag + (int64_t)o * ntin * 256;
                 float4 fa[4], fb[4];
@@ -719,8 +725,8 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
             }
             __syncthreads();
         }
-        // ---- output layer partials (as deep_forward)
-        {
+        // ---- output layer partials (as deep_forward; threads 0..255)
+        if (tid < 256) {
             const float* in = actl(L - 1);
             const int pp = tid >> 5, bb = tid & 31, per = HL >> 3;
             float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -816,7 +822,7 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
             const int f0 = a.tile_begin[l], f1 = f0 + ntin * ntout;
 #pragma unroll
             for (int k = 0; k < kGradTilesPerWave; k++) {
-                const int f = w + 4 * k;
+                const int f = w + kDeepGradWaves * k;
                 if (f >= f0 && f < f1) {                     // wave-uniform
                     const int ti = (f - f0) / ntout, tj = (f - f0) % ntout;
                     const float* ap = A + (32 * ti + col) * kActStride + h;
@@ -832,7 +838,7 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
             // delta_{l-1} = (W_l delta_l) act'(a_{l-1}): output tiles = layer l-1's units, k = layer l's units
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(a.bpacked + a.boff[l]) + lane;
             float* Aw = actl(l - 1);
-            for (int o = w; o < ntin; o += 4) {
+            for (int o = w; o < ntin; o += kDeepGradWaves) {
                 floatx16 c = {};
                 const float4* fo = frag + (int64_t)o * ntout * 256;
                 float4 fa[4], fb[4];
@@ -882,19 +888,16 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
         } else {
             // dW_0^T tile t (32 units x 32 features, features >= 16 zero): A = delta_0 [unit][sample], B = x [sample][feature]
             const float* D0 = actl(0);
+            const int t = w;
+            if (t < net.nt[0]) {
+                floatx16 c = acc0;
+                const float* dp = D0 + (32 * t + col) * kActStride + h;
 #pragma unroll
-            for (int k = 0; k < 2; k++) {
-                const int t = w + 4 * k;
-                if (t < net.nt[0]) {
-                    floatx16 c = acc0[k];
-                    const float* dp = D0 + (32 * t + col) * kActStride + h;
-#pragma unroll
-                    for (int s2 = 0; s2 < 16; s2++) {
-                        const float xv = col < 16 ? obs_value<OBS>(bds[2 * s2 + h], col, a.obs_scale) : 0.0f;
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(dp[2 * s2], xv, c, 0, 0, 0);
-                    }
-                    acc0[k] = c;
+                for (int s2 = 0; s2 < 16; s2++) {
+                    const float xv = col < 16 ? obs_value<OBS>(bds[2 * s2 + h], col, a.obs_scale) : 0.0f;
+                    c = __builtin_amdgcn_mfma_f32_32x32x2f32(dp[2 * s2], xv, c, 0, 0, 0);
                 }
+                acc0 = c;
             }
         }
         __syncthreads();   // the next group rewrites the boards and layer 0
@@ -903,7 +906,7 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
     float* out = a.part + (size_t)blockIdx.x * a.pslab;
 #pragma unroll
     for (int k = 0; k < kGradTilesPerWave; k++) {
-        const int f = w + 4 * k;
+        const int f = w + kDeepGradWaves * k;
         if (f < a.ntiles) {
             int l = 1;
             while (l + 1 < L && f >= a.tile_begin[l + 1]) l++;
@@ -917,13 +920,10 @@ __global__ void __launch_bounds__(kDeepBlock, 1) deep_grad_kernel(DeepGradArgs a
     }
     if constexpr (OBS != G2048_OBS_ONEHOT) {
         const int H0 = 32 * net.nt[0];
+        const int t = w;
+        if (t < net.nt[0] && col < 16) {                   // C[unit][feature]: dW_0[feature][unit]
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const int t = w + 4 * k;
-            if (t < net.nt[0] && col < 16) {               // C[unit][feature]: dW_0[feature][unit]
-#pragma unroll
-                for (int r = 0; r < 16; r++) out[a.pw[0] + (int64_t)col * H0 + 32 * t + tile_row(r, h)] = acc0[k][r];
-            }
+            for (int r = 0; r < 16; r++) out[a.pw[0] + (int64_t)col * H0 + 32 * t + tile_row(r, h)] = acc0[r];
         }
     }
     for (int l = 0; l < L; l++)
@@ -1304,7 +1304,7 @@ int64_t g2048_deep_grad_slab(int obs_mode, int n_hidden, const int32_t* hidden) 
     if (obs_mode != G2048_OBS_LOG2 && obs_mode != G2048_OBS_RAW && obs_mode != G2048_OBS_ONEHOT) return -1;
     if (!deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, n)) return -1;
     const DeepGradLayout g = deep_grad_layout(n);
-    if (g.ntiles > 4 * kGradTilesPerWave || deep_grad_lds_bytes(n) > 160 * 1024) return -1;   // not covered
+    if (g.ntiles > kDeepGradWaves * kGradTilesPerWave || deep_grad_lds_bytes(n) > 160 * 1024) return -1;   // not covered
     return g.pslab;
 }
 
@@ -1345,7 +1345,7 @@ int launch_deep_grad(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t s
             return dfail(G2048_EHIP, "deep gradient: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
         attr_set = true;
     }
-    hipLaunchKernelGGL((deep_grad_kernel<OBS, ACT>), dim3(grid), dim3(kDeepBlock), (unsigned)lds, s, a);
+    hipLaunchKernelGGL((deep_grad_kernel<OBS, ACT>), dim3(grid), dim3(kDeepGradBlock), (unsigned)lds, s, a);
     return check_hip();
 }
 }  // namespace

@@ -60,6 +60,10 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
 #endif
 }
 
+#ifndef G2048_DW2_SPLIT
+#define G2048_DW2_SPLIT 1   // 0: one workgroup per column range for 256-wide second layers too (tools/ A/B build)
+#endif
+
 // MODE: 0 = d2 columns; 1 = the ReLU critic's factored records (mask words + scalar g); 2 = the ReLU actor's
 // records (mask words + the 4 values of g per sample; d2 rebuilt here)
 template <int NT1, int NT2, int MODE>
@@ -70,7 +74,7 @@ struct Dw2 {
     // output column halves: a 256-wide second layer is split over two workgroups (blockIdx.y), each owning 128
     // output columns -- with all 256 in one workgroup every wave holds 16 tiles = 256 accumulators, the whole AGPR
     // file, and the register allocator spilled them to scratch inside the loop (~145 VGPRs)
-    static constexpr int CS = NT2 >= 8 ? 2 : 1;
+    static constexpr int CS = G2048_DW2_SPLIT && NT2 >= 8 ? 2 : 1;
     static constexpr int NT2h = NT2 / CS, H2h = H2 / CS;
     static constexpr int kRows = FAC ? H1 : H1 + H2h;   // staged rows: a1 rows, then this half's d2 rows
     static constexpr int kRecFloats = FAC ? 256 : 0;    // FAC: the block's 1 KiB record (mask words, g)
