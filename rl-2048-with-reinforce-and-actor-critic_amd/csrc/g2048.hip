@@ -466,14 +466,43 @@ static_assert(kTabVec % kBlock == 0, "table fill: whole chunks per thread");
 // of a 1M-board step per CU cost one pass of one wave instead of one divergent pass in most of the 16 waves.
 // (A dynamic schedule -- chunks claimed with device-scope atomics -- measured slower on MI355X: under this
 // kernel's streaming load an atomic's return takes microseconds, and same-address atomics serialize.)
+// G2048_STEP_XCD = d > 0 (tools/ A/B builds only): an XCD-aware static partition instead
+// of the strided one -- block b takes a contiguous range of 64-board chunks, base + d of them when its XCD group
+// (b % 8) is one of the early-dispatched 0..3 and base - d for 4..7 (profiles/round3/step_diag: groups 4..7 enter
+// up to 1.9 us later), its waves taking the range's chunks w, w + 16, ...  Falls back to equal ranges when the
+// chunk count does not divide evenly.
+#ifndef G2048_STEP_XCD
+#define G2048_STEP_XCD 0
+#endif
 template <int OBS, int RNG, bool LDS, int XO, int U, int RK>
 __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     static_assert(U == 1, "one board per lane per sweep");
     __shared__ uint4 tab_lds[LDS ? kStepLdsVec : 1];
     const int lane = threadIdx.x & 63;
+#if G2048_STEP_XCD
+    uint32_t w_first, wend;
+    const uint32_t wstride = kBlock;
+    {
+        const uint32_t nc = (a.n + 63u) >> 6, G = gridDim.x, base = nc / G, d = G2048_STEP_XCD;
+        uint32_t cs, ce;
+        if ((G & 7u) == 0u && nc % G == 0u && base > 2u * d && base + d <= 64u * (kBlock / 64)) {
+            const uint32_t x = blockIdx.x & 7u, i = blockIdx.x >> 3;
+            cs = i * 8u * base + (x < 4u ? x * (base + d) : 4u * (base + d) + (x - 4u) * (base - d));
+            ce = cs + (x < 4u ? base + d : base - d);
+        } else {
+            cs = (uint32_t)(((uint64_t)nc * blockIdx.x) / G);
+            ce = (uint32_t)(((uint64_t)nc * (blockIdx.x + 1u)) / G);
+        }
+        w_first = (cs + (threadIdx.x >> 6)) * 64u;
+        wend = ce * 64u < a.n ? ce * 64u : a.n;
+    }
+    const uint32_t last = (wend > 0u ? wend : 1u) - 1u;
+#else
     const uint32_t w_first = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
     const uint32_t wstride = gridDim.x * kBlock;
+    const uint32_t wend = a.n;
     const uint32_t last = a.n - 1u;           // n >= 1 (the launcher never launches n == 0)
+#endif
     const auto lane_at = [&](uint32_t w) { return w + lane < last ? w + lane : last; };
     G2048_TS(0);
     LaneIn A, B, C;
@@ -503,15 +532,15 @@ __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     const CodeFn code{tab + (LDS || RK == 0 ? 2 * kLines : kMxOff)};
     uint64_t pending = 0, pseed = 0;
     uint32_t k = 0;
-    while (w0 < a.n) {                         // wave-uniform
+    while (w0 < wend) {                        // wave-uniform
         const uint32_t w2 = w1 + wstride;
         load_lane<RNG>(a, lane_at(w2), C);
         sweep<OBS, RNG, XO, RK>(a, w0, lane, A, lut, code, pending, pseed, k);
-        if (w1 >= a.n) break;
+        if (w1 >= wend) break;
         const uint32_t w3 = w2 + wstride;
         load_lane<RNG>(a, lane_at(w3), A);
         sweep<OBS, RNG, XO, RK>(a, w1, lane, B, lut, code, pending, pseed, k + 1);
-        if (w2 >= a.n) break;
+        if (w2 >= wend) break;
         const uint32_t w4 = w3 + wstride;
         load_lane<RNG>(a, lane_at(w4), B);
         sweep<OBS, RNG, XO, RK>(a, w2, lane, C, lut, code, pending, pseed, k + 2);

@@ -16,7 +16,7 @@ CLOCK_GHZ, SIMDS = 2.4, 1024
 
 
 def kname(n):
-    for k in ("grad_kernel", "dw2_kernel", "policy_kernel", "rollout_kernel", "Cijk"):
+    for k in ("grad_coop_kernel", "grad_kernel", "dw2_kernel", "fold_kernel", "policy_kernel", "rollout_kernel", "Cijk"):
         if k in n:
             return k
     return None
