@@ -677,11 +677,10 @@ class ReinforceAgent:
     dw2_min_cols_per_part = 2048
 
     def _dw2_parts(self, ncols: int, h2: int) -> tuple[int, int]:
-        """(columns per part, parts) of a g2048_dw2* call: about one workgroup per CU -- a 256-wide second layer
-        runs two workgroups per part (its output column halves), so half as many parts."""
+        """(columns per part, parts) of a g2048_dw2* call: one workgroup per part, about one per CU (a 256-wide
+        second layer runs one 8-wave workgroup per part)."""
         cus = int(self._lib.g2048_actor_grad_waves()) // 4
-        per_part_wgs = 2 if _padded_units(h2) == 256 else 1
-        cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * max(cus // per_part_wgs, 1))) * 16)
+        cpp = max(self.dw2_min_cols_per_part, -(-ncols // (16 * max(cus, 1))) * 16)
         return cpp, -(-ncols // cpp)
 
     def _fold(self, part: torch.Tensor, acc: torch.Tensor) -> None:

@@ -60,9 +60,18 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
 #endif
 }
 
-#ifndef G2048_DW2_SPLIT
-#define G2048_DW2_SPLIT 1   // 0: one workgroup per column range for 256-wide second layers too (tools/ A/B build)
+// 256-wide second layers: G2048_DW2_WIDE 1 (default) -- one 8-wave workgroup per column range (2 waves per SIMD,
+// 8 accumulator tiles each, one register set of planes); 0 -- the 4-wave kernel with the output columns split over
+// two workgroups (each re-reads the a1 rows); the 4-wave kernel with all 256 columns spills (tools/ A/B builds:
+// G2048_DW2_WIDE=0, and G2048_DW2_SPLIT=0 for the spilling form)
+#ifndef G2048_DW2_WIDE
+#define G2048_DW2_WIDE 1
 #endif
+#ifndef G2048_DW2_SPLIT
+#define G2048_DW2_SPLIT 1
+#endif
+
+__host__ __device__ constexpr int dw2_threads(int nt2) { return G2048_DW2_WIDE && nt2 >= 8 ? 512 : 256; }
 
 // MODE: 0 = d2 columns; 1 = the ReLU critic's factored records (mask words + scalar g); 2 = the ReLU actor's
 // records (mask words + the 4 values of g per sample; d2 rebuilt here)
@@ -74,16 +83,21 @@ struct Dw2 {
     // output column halves: a 256-wide second layer is split over two workgroups (blockIdx.y), each owning 128
     // output columns -- with all 256 in one workgroup every wave holds 16 tiles = 256 accumulators, the whole AGPR
     // file, and the register allocator spilled them to scratch inside the loop (~145 VGPRs)
-    static constexpr int CS = G2048_DW2_SPLIT && NT2 >= 8 ? 2 : 1;
+    static constexpr bool WIDE = G2048_DW2_WIDE && NT2 >= 8;
+    static constexpr int CS = !WIDE && G2048_DW2_SPLIT && NT2 >= 8 ? 2 : 1;
+    static constexpr int kW = WIDE ? 8 : 4;             // waves: a WR x WC grid over the output tiles
+    static constexpr int WR = 2, WC = kW / 2;
+    static constexpr int kThr = 64 * kW;
+    static_assert(kThr == dw2_threads(NT2), "launch bounds");
     static constexpr int NT2h = NT2 / CS, H2h = H2 / CS;
     static constexpr int kRows = FAC ? H1 : H1 + H2h;   // staged rows: a1 rows, then this half's d2 rows
     static constexpr int kRecFloats = FAC ? 256 : 0;    // FAC: the block's 1 KiB record (mask words, g)
     static constexpr int kStageFloats = kRows * kBK + kRecFloats;   // 64 B per staged row
     static constexpr int kRowGlds = kRows / 16;         // 1 KiB LDS-DMA instructions per stage (16 rows each)
     static constexpr int kGlds = kRowGlds + (FAC ? 1 : 0);          // + the record
-    static constexpr int kGldsPerWave = (kGlds + 3) / 4;
-    static constexpr int TR = NT1 >= 2 ? NT1 / 2 : 1;   // row tiles per wave (2 x 2 wave grid)
-    static constexpr int TC = NT2h >= 2 ? NT2h / 2 : 1;   // column tiles per wave
+    static constexpr int kGldsPerWave = (kGlds + kW - 1) / kW;
+    static constexpr int TR = NT1 >= WR ? NT1 / WR : 1;   // row tiles per wave
+    static constexpr int TC = NT2h >= WC ? NT2h / WC : 1;  // column tiles per wave
 };
 
 struct Dw2Args {
@@ -122,12 +136,12 @@ __device__ __forceinline__ void read_frag(const float* stage, int row, int h, fl
 // g per sample, so dW2 = W3[j] * sum (a1 g) m^T and db2 = W3[j] * sum g m: the A operand is a1 * g (one fp32 product,
 // split exactly into three planes), the B operand the mask (exact in bf16), three MFMAs per step instead of six.
 template <int NT1, int NT2, int MODE>
-__global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
+__global__ void __launch_bounds__(dw2_threads(NT2), 1) dw2_kernel(Dw2Args a) {
     using G = Dw2<NT1, NT2, MODE>;
     constexpr bool FAC = G::FAC;
     __shared__ float S[kStages * G::kStageFloats];   // the only LDS object (see the glds / second-object rule)
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5, r = lane & 31;
-    const int wr = w >> 1, wc = w & 1;
+    const int wr = w / G::WC, wc = w % G::WC;
     const uint32_t k_begin = a.col0 + blockIdx.x * a.kb;
     const uint32_t k_end = min(k_begin + a.kb, a.col0 + a.ncols);
     const int iters = k_end > k_begin ? (int)((k_end - k_begin) / kBK) : 0;
@@ -140,7 +154,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     // instruction that is depends only on the wave, so the per-stage source stride is a scalar)
     const int ws = __builtin_amdgcn_readfirstlane(w);
     const auto glds_index = [&](int i) {
-        const int g = ws + 4 * i;
+        const int g = ws + G::kW * i;
         return g < G::kGlds ? g : G::kGlds - 1;
     };
     const float* src[G::kGldsPerWave];
@@ -171,7 +185,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
     for (int i = 0; i < G::TR; i++)
 #pragma unroll
         for (int j = 0; j < G::TC; j++) acc[i][j] = floatx16{};
-    const bool rows_mine = NT1 >= 2 || wr == 0, cols_mine = G::NT2h >= 2 || wc == 0;
+    const bool rows_mine = NT1 >= G::WR || wr == 0, cols_mine = G::NT2h >= G::WC || wc == 0;
     // db2: thread t sums d2 row c0 + t (threads past H2h sum the half's last row and never store: no branch in the
     // loop body)
     const int drow = G::H1 + (t < G::H2h ? t : G::H2h - 1);
@@ -183,7 +197,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
         const float4* w3v = reinterpret_cast<const float4*>(a.w3);
         w3d = w3v[dunit];
 #pragma unroll
-        for (int j = 0; j < G::TC; j++) w3c[j] = w3v[c0 + 32 * ((G::NT2h >= 2 ? wc : 0) * G::TC + j) + r];
+        for (int j = 0; j < G::TC; j++) w3c[j] = w3v[c0 + 32 * ((G::NT2h >= G::WC ? wc : 0) * G::TC + j) + r];
     }
     // d2 = act'(a2) (W3 g) exactly as grad_kernel forms it: fl(g0 w0), three fmaf, times 1.0 or 0.0
     const auto d2_of = [](const float4 g, const float4 w, bool m) {
@@ -340,6 +354,25 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
         }
     };
 
+    if constexpr (G::WIDE) {
+        // two waves per SIMD, one register set of planes: each step waits for stage it, splits it and runs its
+        // MFMAs; the SIMD's other wave fills the gaps (the double-buffered set does not fit 256 registers)
+        Planes pa;
+        if (iters > 0) {
+#pragma unroll
+            for (int q = 0; q < kAhead; q++) issue_to(q, q < iters ? q : iters - 1);
+            for (int it = 0; it < iters; it++) {
+                const int q = it + kAhead;
+                issue_to(q % kStages, q < iters ? q : iters - 1);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kAhead * G::kGldsPerWave) : "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                load(S + (it % kStages) * G::kStageFloats, pa);
+                mfma(pa);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    } else {
     Planes pa, pb;
     if (iters > 0) {
 #pragma unroll
@@ -363,6 +396,7 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
         // by the compiler: drain them before the workgroup ends, so its LDS is never handed on with writes in flight
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    }
     // this workgroup's slab: dW2 rows from the accumulators (C/D layout: column = lane & 31, row = acc_row), db2
     // (FAC: each column scaled by W3[j] -- the one multiply of the factored form)
     float* out = a.part + (size_t)blockIdx.x * (G::H1 + 1) * G::H2;
@@ -384,10 +418,10 @@ __global__ void __launch_bounds__(kThreads, 1) dw2_kernel(Dw2Args a) {
 template <int NT1, int MODE>
 void launch_nt2(const Dw2Args& a, int nt2, int grid, hipStream_t s) {
     switch (nt2) {   // grid.y = the output column halves (Dw2::CS)
-        case 1: hipLaunchKernelGGL((dw2_kernel<NT1, 1, MODE>), dim3(grid, Dw2<NT1, 1, MODE>::CS), dim3(kThreads), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((dw2_kernel<NT1, 2, MODE>), dim3(grid, Dw2<NT1, 2, MODE>::CS), dim3(kThreads), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((dw2_kernel<NT1, 4, MODE>), dim3(grid, Dw2<NT1, 4, MODE>::CS), dim3(kThreads), 0, s, a); break;
-        default: hipLaunchKernelGGL((dw2_kernel<NT1, 8, MODE>), dim3(grid, Dw2<NT1, 8, MODE>::CS), dim3(kThreads), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((dw2_kernel<NT1, 1, MODE>), dim3(grid, Dw2<NT1, 1, MODE>::CS), dim3(Dw2<NT1, 1, MODE>::kThr), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((dw2_kernel<NT1, 2, MODE>), dim3(grid, Dw2<NT1, 2, MODE>::CS), dim3(Dw2<NT1, 2, MODE>::kThr), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((dw2_kernel<NT1, 4, MODE>), dim3(grid, Dw2<NT1, 4, MODE>::CS), dim3(Dw2<NT1, 4, MODE>::kThr), 0, s, a); break;
+        default: hipLaunchKernelGGL((dw2_kernel<NT1, 8, MODE>), dim3(grid, Dw2<NT1, 8, MODE>::CS), dim3(Dw2<NT1, 8, MODE>::kThr), 0, s, a); break;
     }
 }
 
