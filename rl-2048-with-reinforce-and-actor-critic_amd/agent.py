@@ -644,6 +644,102 @@ class ReinforceAgent:
         gW[nh] += acc[pw[nh]:pw[nh] + Hp[-1] * 4].view(Hp[-1], 4)[:hidden[-1], :out_dim]
         gb[nh] += acc[pb[nh]:pb[nh] + 4][:out_dim]
 
+    def _deep_critic_rows(self, params, dspec, steps: "_Steps", K: int, gW: list[torch.Tensor],
+                          gb: list[torch.Tensor], step_w: torch.Tensor, deltas: torch.Tensor) -> None:
+        """The critic branch through g2048_deep_grad without a separate V(s') forward (as _critic_grad_rows for the
+        two-layer kernels): the time rows of the time-major valid steps run LAST first, one launch each, and each
+        launch's V(s) (v_out) is the V(s') of the previous row's TD targets (src/reinforce_agent.py:423-443).  The
+        trailing short rows run first as one launch with their own V(s') forward (g2048_deep_policy), handing V(s)
+        of their first row to the chain.  One-hot first layers: each launch's layer-0 deltas collect in one buffer
+        (with their boards) that g2048_onehot_dw1 scatters whenever it is full."""
+        c = self.agent_config
+        obs_code, hidden, act, harr = dspec
+        onehot = obs_code == L.OBS_ONEHOT
+        loss = {"mse": 0, "huber": 1}[c.critic_loss_type]
+        packed = self._pack_deep(params, dspec, "critic", 1)
+        bpacked = self._pack_deep_grad(params, dspec, "critic")
+        nparts = int(self._lib.g2048_actor_grad_waves()) // 4
+        slab = int(self._lib.g2048_deep_grad_slab(obs_code, len(hidden), harr))
+        part = torch.empty(nparts, slab, dtype=torch.float32, device=self.device)
+        acc = torch.zeros(slab, dtype=torch.float64, device=self.device)
+        h0, H0p = hidden[0], _round32(hidden[0])
+        acc1 = torch.zeros(273 * h0, dtype=torch.float64, device=self.device) if onehot else None
+        scale = float(self.env_config.obs_log2_scale)
+        gamma = float(c.gamma)
+        n = steps.n
+        counts = torch.bincount(steps.t, minlength=steps.T).tolist()      # samples per time row (one host sync)
+        starts = [0] * len(counts)
+        for t in range(1, len(counts)):
+            starts[t] = starts[t - 1] + counts[t - 1]
+        t_tail, tail_m = len(counts), 0
+        while t_tail > 0 and counts[t_tail - 1] < self.critic_tail_row_max:
+            t_tail -= 1
+            tail_m += counts[t_tail]
+        vout = torch.empty(max(max(counts), tail_m, 1), dtype=torch.float32, device=self.device)
+        ldb = max(self.grad_chunk_steps, max(counts), tail_m)
+        d0buf = torch.empty(ldb, H0p, dtype=torch.float32, device=self.device) if onehot else None
+        bbuf = torch.empty(ldb, dtype=torch.int64, device=self.device) if onehot else None
+        used = 0
+
+        def flush_d0() -> None:
+            nonlocal used
+            if onehot and used:
+                self._onehot_dw1_into(bbuf[:used], d0buf[:used], acc1, h1=h0)
+            used = 0
+
+        def launch(s0: int, cnt: int, tgt: torch.Tensor, k: int) -> None:
+            nonlocal used
+            sel = torch.arange(s0, s0 + cnt, device=self.device)
+            b = steps.boards_at(sel, k)
+            if onehot and used + cnt > ldb:
+                flush_d0()
+            d0 = d0buf[used:used + cnt] if onehot else None
+            L.check(self._lib.g2048_deep_grad(L.ptr(packed), L.ptr(bpacked), len(hidden), harr, act, obs_code, scale,
+                                              0, L.ptr(b), None, L.ptr(step_w[s0:s0 + cnt]), 1, loss,
+                                              float(c.huber_delta), L.ptr(tgt), L.ptr(deltas[k, s0:s0 + cnt]),
+                                              L.ptr(vout), L.ptr(d0), cnt, L.ptr(part), nparts, self._stream))
+            self._fold(part, acc)
+            if onehot:
+                bbuf[used:used + cnt] = b
+                used += cnt
+
+        for k in range(K):
+            vb = [torch.zeros(n, dtype=torch.float32, device=self.device) for _ in range(2)]
+            if tail_m:
+                s0 = starts[t_tail]
+                sel = torch.arange(s0, s0 + tail_m, device=self.device)
+                hn = steps.has_next[sel]
+                vn = self._deep_forward(params, dspec, "critic", steps.boards_at(sel, k, nxt=True), 1)[:, 0]
+                launch(s0, tail_m, (steps.rewards[sel] + (gamma * vn) * hn.to(torch.float32)).contiguous(), k)
+                if t_tail > 0:
+                    vb[t_tail & 1].index_copy_(0, steps.lane[s0:s0 + counts[t_tail]], vout[:counts[t_tail]])
+            for t in range(t_tail - 1, -1, -1):
+                cnt = counts[t]
+                if cnt == 0:
+                    continue
+                s0 = starts[t]
+                lanes = steps.lane[s0:s0 + cnt]
+                hn = steps.has_next[s0:s0 + cnt]
+                vn = vb[(t + 1) & 1].index_select(0, lanes)
+                launch(s0, cnt, (steps.rewards[s0:s0 + cnt] + (gamma * vn) * hn.to(torch.float32)).contiguous(), k)
+                vb[t & 1].index_copy_(0, lanes, vout[:cnt])
+        flush_d0()
+        pw, pb = self._deep_slab_layout(hidden, onehot)
+        Hp = [_round32(h) for h in hidden]
+        acc = acc.to(torch.float32)
+        nh = len(hidden)
+        if onehot:
+            gW[0] += acc1[:272 * h0].view(272, h0).to(torch.float32)
+            gb[0] += acc[pb[0]:pb[0] + Hp[0]][:h0]
+        else:
+            gW[0] += acc[pw[0]:pw[0] + 16 * Hp[0]].view(16, Hp[0])[:, :h0]
+            gb[0] += acc[pb[0]:pb[0] + Hp[0]][:h0]
+        for l in range(1, nh):
+            gW[l] += acc[pw[l]:pw[l] + Hp[l - 1] * Hp[l]].view(Hp[l - 1], Hp[l])[:hidden[l - 1], :hidden[l]]
+            gb[l] += acc[pb[l]:pb[l] + Hp[l]][:hidden[l]]
+        gW[nh] += acc[pw[nh]:pw[nh] + Hp[-1] * 4].view(Hp[-1], 4)[:hidden[-1], :1]
+        gb[nh] += acc[pb[nh]:pb[nh] + 4][:1]
+
     def _packed_policy(self, spec) -> torch.Tensor:
         """The actor packed in MFMA fragment order (g2048_policy_pack), re-packed whenever a parameter tensor is
         replaced or modified in place (or after an update / load)."""
@@ -1459,8 +1555,13 @@ class ReinforceAgent:
                 self._paths["critic_grad"] = "g2048_deep_grad" + (" + g2048_onehot_dw1" if
                                                                  cdg[0] == L.OBS_ONEHOT else "")
                 with torch.no_grad():
-                    self._deep_grad_fused(self.critic_params, "critic", cdg, steps, K, critic_g[:ncW], critic_g[ncW:],
-                                          1, step_w=step_w, deltas=deltas)
+                    if self._critic_by_rows(steps):
+                        self._paths["critic_grad"] += " (time rows, last first)"
+                        self._deep_critic_rows(self.critic_params, cdg, steps, K, critic_g[:ncW], critic_g[ncW:],
+                                               step_w, deltas)
+                    else:
+                        self._deep_grad_fused(self.critic_params, "critic", cdg, steps, K, critic_g[:ncW],
+                                              critic_g[ncW:], 1, step_w=step_w, deltas=deltas)
                 cspec = cdg      # handled: skip the torch loop below
             cdspec = self._deep_spec(self.critic_params, 1) if cspec is None and steps.boards is not None else None
             oh1 = self._onehot_first_layer(steps) and cspec is None

@@ -1032,29 +1032,61 @@ __global__ void __launch_bounds__(256) onehot_l1_kernel(const float* __restrict_
 // samples [part * per, ...): acc[17 c + e_c(s)][lane] += d1[s][64 slice + lane] in sample order, then slab rows
 // 0..271 = dW1 and row 272 = db1 of its columns.  The 8 waves of a block share the [272][64] accumulator by cells
 // (wave k: cells 2k, 2k + 1, whose rows no other wave touches), each adding its rows in sample order in program
-// order: deterministic, and the same per-row order as one wave doing all 16 cells.  (One 64-lane wave per block
-// held the CU to two waves -- the accumulator is 68 KiB -- and its LDS read-modify-writes were latency-bound.)
+// order: deterministic, and the same per-row order as one wave doing all 16 cells.  The read-modify-writes are
+// latency-bound (each add waits for its row's read), so consecutive samples are taken in pairs (one read per row a
+// pair touches) and the two cells' rows live in separate LDS objects the compiler can overlap.
 constexpr int kDw1Rows = kOneHotRows + 1;
 
-constexpr int kDw1Waves = 8;   // wave k owns cells 2k, 2k + 1 = accumulator rows [34 k, 34 k + 34)
+constexpr int kDw1Waves = 8;   // wave k owns cells 2k (even array) and 2k + 1 (odd array)
 __global__ void __launch_bounds__(64 * kDw1Waves) onehot_dw1_kernel(const uint64_t* __restrict__ boards,
                                                                    const float* __restrict__ d1, int h1, int64_t m,
                                                                    int64_t ld, int64_t per, float* __restrict__ part) {
-    __shared__ float acc[kOneHotRows * 64];
+    // the even and odd cells' rows in two LDS objects, so the compiler may overlap their read-modify-writes
+    __shared__ float acc_e[kDw1Waves * 17 * 64];
+    __shared__ float acc_o[kDw1Waves * 17 * 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int slice = blockIdx.x, p = blockIdx.y;
     const int j = 64 * slice + lane;
-    const int r0 = 34 * w;                          // this wave's rows: cells 2w (17 rows) and 2w + 1 (17 rows)
-    for (int r = r0; r < r0 + 34; r++) acc[r * 64 + lane] = 0.0f;
+    float* Ae = acc_e + w * 17 * 64 + lane;         // rows 17 (2w) + e
+    float* Ao = acc_o + w * 17 * 64 + lane;         // rows 17 (2w + 1) + e
+    for (int r = 0; r < 17; r++) {
+        Ae[r * 64] = 0.0f;
+        Ao[r * 64] = 0.0f;
+    }
     float db = 0.0f;
     const int64_t s0 = (int64_t)p * per, s1 = s0 + per < m ? s0 + per : m;
     const bool live = j < h1;
     const uint32_t sh = 8u * (uint32_t)w;           // the two cells' nibbles
-    const auto add = [&](uint64_t b, float v) {
+    // one sample (tail)
+    const auto add1 = [&](uint64_t b, float v) {
         if (w == 0) db += v;
         const uint32_t e = (uint32_t)(b >> sh);
-        acc[(r0 + (int)(e & 15u)) * 64 + lane] += v;
-        acc[(r0 + 17 + (int)((e >> 4) & 15u)) * 64 + lane] += v;
+        Ae[(int)(e & 15u) * 64] += v;
+        Ao[(int)((e >> 4) & 15u) * 64] += v;
+    };
+    // two consecutive samples: a row both touch gets (x + v0) + v1 from one read (the sequential result, bit for
+    // bit); different rows are read together -- one LDS round trip per pair and cell instead of two.  The branches
+    // are wave-uniform (the boards are).
+    const auto pair = [](float* A, uint32_t e0, uint32_t e1, float v0, float v1) {
+        if (e0 == e1) {
+            float x = A[(int)e0 * 64];
+            x += v0;
+            x += v1;
+            A[(int)e0 * 64] = x;
+        } else {
+            const float x0 = A[(int)e0 * 64], x1 = A[(int)e1 * 64];
+            A[(int)e0 * 64] = x0 + v0;
+            A[(int)e1 * 64] = x1 + v1;
+        }
+    };
+    const auto add2 = [&](uint64_t b0, float v0, uint64_t b1, float v1) {
+        if (w == 0) {
+            db += v0;
+            db += v1;
+        }
+        const uint32_t e0 = (uint32_t)(b0 >> sh), e1 = (uint32_t)(b1 >> sh);
+        pair(Ae, e0 & 15u, e1 & 15u, v0, v1);
+        pair(Ao, (e0 >> 4) & 15u, (e1 >> 4) & 15u, v0, v1);
     };
     int64_t s = s0;
     for (; s + 4 <= s1; s += 4) {                   // the next 4 samples' loads in flight together
@@ -1065,13 +1097,16 @@ __global__ void __launch_bounds__(64 * kDw1Waves) onehot_dw1_kernel(const uint64
             bq[k] = boards[s + k];                      // wave-uniform
             vq[k] = live ? d1[(s + k) * ld + j] : 0.0f;
         }
-#pragma unroll
-        for (int k = 0; k < 4; k++) add(bq[k], vq[k]);
+        add2(bq[0], vq[0], bq[1], vq[1]);
+        add2(bq[2], vq[2], bq[3], vq[3]);
     }
-    for (; s < s1; s++) add(boards[s], live ? d1[s * ld + j] : 0.0f);
+    for (; s < s1; s++) add1(boards[s], live ? d1[s * ld + j] : 0.0f);
     float* slab = part + (int64_t)p * kDw1Rows * h1;
     if (live) {
-        for (int r = r0; r < r0 + 34; r++) slab[(int64_t)r * h1 + j] = acc[r * 64 + lane];
+        for (int r = 0; r < 17; r++) {
+            slab[(int64_t)(34 * w + r) * h1 + j] = Ae[r * 64];
+            slab[(int64_t)(34 * w + 17 + r) * h1 + j] = Ao[r * 64];
+        }
         if (w == 0) slab[(int64_t)kOneHotRows * h1 + j] = db;
     }
 }

@@ -288,24 +288,31 @@ def test_deep_rollout_suspend_resume_equals_stepwise(env, hidden):
         assert float(b1.total_reward[i]) == total
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused,rows", [(True, False), (False, False), (True, True)])
 @pytest.mark.parametrize("env,hidden,act,critic", [(REFCONF_ENV, [256, 128, 64], "ReLU", True),
                                                    (dict(REFCONF_ENV, max_steps=200), [40, 33, 20, 10], "Sigmoid", False),
                                                    (dict(obs_mode="log2", obs_log2_scale=0.0625, max_steps=None),
                                                     [64, 48, 32], "ReLU", True)])
-def test_deep_update_at_size_vs_fp64(env, hidden, act, critic, fused):
+def test_deep_update_at_size_vs_fp64(env, hidden, act, critic, fused, rows):
     """update_from_batch on nets the register-specialised kernels do not cover (the reference runner's documented
     config first: one-hot obs, 256-128-64, actor-critic) over 16,384 episodes of its own rollout: the pre-clip
     gradients within 1e-5 normwise of the exact fp64 value of update_batch's formula under the fp32 path's own
     ReLU pattern (tests/exact_grad.py exact_update_grads_deep), that pattern bounded against fp64's own (every
     disagreement within the fp32 accumulation bound, <= 1e-5 of the unit-samples), and the norms within 1e-5.
     fused: g2048_deep_grad (forward + backward in one kernel; the one-hot first layer by g2048_onehot_dw1's
-    scatter); else the gather + hipBLASLt path (g2048_onehot_layer1 / g2048_onehot_dw1 around torch GEMMs)."""
+    scatter); else the gather + hipBLASLt path (g2048_onehot_layer1 / g2048_onehot_dw1 around torch GEMMs).
+    rows: the critic by time rows, last first (each launch's V(s) the previous row's V(s'), no V(s') forward),
+    forced on this batch size (by default from 16,384 samples per row)."""
     import exact_grad as EG
 
+    if rows and not critic:
+        pytest.skip("the row pass is the critic's")
     a = _agent(env, hidden, act, baseline_mode="batch", gamma=0.99, use_critic=critic, optimizer="adam",
                learning_rate=0.01, critic_learning_rate=5e-4)
     a.use_fused_grad = fused
+    if rows:
+        a.critic_rows_min_avg = 0
+        a.critic_tail_row_max = 256
     n = 16384
     es = np.arange(7, 7 + n, dtype=np.int64)
     batch = a.rollout_batch(es, es + 3 * n)
@@ -316,6 +323,7 @@ def test_deep_update_at_size_vs_fp64(env, hidden, act, critic, fused):
         assert paths["actor_grad"].startswith("g2048_deep_grad"), paths
         if critic:
             assert paths["critic_grad"].startswith("g2048_deep_grad"), paths
+            assert ("time rows" in paths["critic_grad"]) == rows, paths
     elif env["obs_mode"] == "onehot":
         assert "g2048_onehot_layer1" in paths["actor_grad"], paths
     flips: dict = {}
