@@ -1088,17 +1088,32 @@ __global__ void __launch_bounds__(64 * kDw1Waves) onehot_dw1_kernel(const uint64
         pair(Ae, e0 & 15u, e1 & 15u, v0, v1);
         pair(Ao, (e0 >> 4) & 15u, (e1 >> 4) & 15u, v0, v1);
     };
+    // 8 samples per batch, the next batch's loads issued before this batch's adds (the adds wait on LDS only, so
+    // the loads' latency -- the deltas were just written, L2 / MALL -- hides under them)
+    constexpr int kB = 8;
     int64_t s = s0;
-    for (; s + 4 <= s1; s += 4) {                   // the next 4 samples' loads in flight together
-        uint64_t bq[4];
-        float vq[4];
+    uint64_t bq[kB], bn[kB];
+    float vq[kB], vn[kB];
+    const auto fetch = [&](int64_t at, uint64_t (&b)[kB], float (&v)[kB]) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            bq[k] = boards[s + k];                      // wave-uniform
-            vq[k] = live ? d1[(s + k) * ld + j] : 0.0f;
+        for (int k = 0; k < kB; k++) {
+            b[k] = boards[at + k];                      // wave-uniform
+            v[k] = live ? d1[(at + k) * ld + j] : 0.0f;
         }
-        add2(bq[0], vq[0], bq[1], vq[1]);
-        add2(bq[2], vq[2], bq[3], vq[3]);
+    };
+    if (s + kB <= s1) fetch(s, bq, vq);
+    for (; s + kB <= s1; s += kB) {
+        const bool more = s + 2 * kB <= s1;             // wave-uniform
+        if (more) fetch(s + kB, bn, vn);
+#pragma unroll
+        for (int k = 0; k < kB; k += 2) add2(bq[k], vq[k], bq[k + 1], vq[k + 1]);
+        if (more) {
+#pragma unroll
+            for (int k = 0; k < kB; k++) {
+                bq[k] = bn[k];
+                vq[k] = vn[k];
+            }
+        }
     }
     for (; s < s1; s++) add1(boards[s], live ? d1[s * ld + j] : 0.0f);
     float* slab = part + (int64_t)p * kDw1Rows * h1;
