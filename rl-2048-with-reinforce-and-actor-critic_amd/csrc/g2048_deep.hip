@@ -1029,99 +1029,68 @@ __global__ void __launch_bounds__(256) onehot_l1_kernel(const float* __restrict_
 }
 
 // dW1 / db1 partials of a one-hot first layer: block (slice, part) owns units [64 slice, 64 slice + 64) and
-// samples [part * per, ...): acc[17 c + e_c(s)][lane] += d1[s][64 slice + lane] in sample order, then slab rows
-// 0..271 = dW1 and row 272 = db1 of its columns.  The 8 waves of a block share the [272][64] accumulator by cells
-// (wave k: cells 2k, 2k + 1, whose rows no other wave touches), each adding its rows in sample order in program
-// order: deterministic, and the same per-row order as one wave doing all 16 cells.  The read-modify-writes are
-// latency-bound (each add waits for its row's read), so consecutive samples are taken in pairs (one read per row a
-// pair touches) and the two cells' rows live in separate LDS objects the compiler can overlap.
+// samples [part * per, ...): dW1[17 c + e_c(s)][j] += d1[s][j] in sample order, then slab rows 0..271 = dW1 and row
+// 272 = db1 of its columns.  Accumulated in registers: wave k of the 4 owns cells 4k .. 4k + 3, lane = unit, one
+// 16-float array per cell indexed by the cell's nibble -- the board is the same for the whole wave, so the index
+// is scalar and `acc[e] += v` is a register-relative move, an add and a move back (no memory round trip; row
+// 17 c + 16, exponent 16, never occurs on a bitboard and stays zero).  Each row's adds run in sample order:
+// deterministic.  (Round 4 before this: a [272][64] LDS accumulator, each add a read-modify-write that waited for
+// its read -- latency-bound at ~1.5 ms per 2^20 samples against ~0.3 ms for this form.)
 constexpr int kDw1Rows = kOneHotRows + 1;
-
-constexpr int kDw1Waves = 8;   // wave k owns cells 2k (even array) and 2k + 1 (odd array)
+constexpr int kDw1Waves = 4;
 __global__ void __launch_bounds__(64 * kDw1Waves) onehot_dw1_kernel(const uint64_t* __restrict__ boards,
                                                                    const float* __restrict__ d1, int h1, int64_t m,
                                                                    int64_t ld, int64_t per, float* __restrict__ part) {
-    // the even and odd cells' rows in two LDS objects, so the compiler may overlap their read-modify-writes
-    __shared__ float acc_e[kDw1Waves * 17 * 64];
-    __shared__ float acc_o[kDw1Waves * 17 * 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int slice = blockIdx.x, p = blockIdx.y;
     const int j = 64 * slice + lane;
-    float* Ae = acc_e + w * 17 * 64 + lane;         // rows 17 (2w) + e
-    float* Ao = acc_o + w * 17 * 64 + lane;         // rows 17 (2w + 1) + e
-    for (int r = 0; r < 17; r++) {
-        Ae[r * 64] = 0.0f;
-        Ao[r * 64] = 0.0f;
-    }
+    float a0[16], a1[16], a2[16], a3[16];           // cells 4w .. 4w + 3
+#pragma unroll
+    for (int r = 0; r < 16; r++) a0[r] = a1[r] = a2[r] = a3[r] = 0.0f;
     float db = 0.0f;
     const int64_t s0 = (int64_t)p * per, s1 = s0 + per < m ? s0 + per : m;
     const bool live = j < h1;
-    const uint32_t sh = 8u * (uint32_t)w;           // the two cells' nibbles
-    // one sample (tail)
-    const auto add1 = [&](uint64_t b, float v) {
+    const int jc = live ? j : 0;
+    const uint32_t sh = 16u * (uint32_t)__builtin_amdgcn_readfirstlane(w);   // the four cells' nibbles
+    const auto add = [&](uint64_t b, float v) {
         if (w == 0) db += v;
         const uint32_t e = (uint32_t)(b >> sh);
-        Ae[(int)(e & 15u) * 64] += v;
-        Ao[(int)((e >> 4) & 15u) * 64] += v;
+        a0[e & 15u] += v;
+        a1[(e >> 4) & 15u] += v;
+        a2[(e >> 8) & 15u] += v;
+        a3[(e >> 12) & 15u] += v;
     };
-    // two consecutive samples: a row both touch gets (x + v0) + v1 from one read (the sequential result, bit for
-    // bit); different rows are read together -- one LDS round trip per pair and cell instead of two.  The branches
-    // are wave-uniform (the boards are).
-    const auto pair = [](float* A, uint32_t e0, uint32_t e1, float v0, float v1) {
-        if (e0 == e1) {
-            float x = A[(int)e0 * 64];
-            x += v0;
-            x += v1;
-            A[(int)e0 * 64] = x;
-        } else {
-            const float x0 = A[(int)e0 * 64], x1 = A[(int)e1 * 64];
-            A[(int)e0 * 64] = x0 + v0;
-            A[(int)e1 * 64] = x1 + v1;
-        }
+    // the boards by one vector load per 64 samples (lane l: sample c0 + l), read out per sample with v_readlane
+    const auto board_of = [](uint64_t bl, int k) -> uint64_t {
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)bl, k), hi = __builtin_amdgcn_readlane((uint32_t)(bl >> 32), k);
+        return ((uint64_t)hi << 32) | lo;
     };
-    const auto add2 = [&](uint64_t b0, float v0, uint64_t b1, float v1) {
-        if (w == 0) {
-            db += v0;
-            db += v1;
-        }
-        const uint32_t e0 = (uint32_t)(b0 >> sh), e1 = (uint32_t)(b1 >> sh);
-        pair(Ae, e0 & 15u, e1 & 15u, v0, v1);
-        pair(Ao, (e0 >> 4) & 15u, (e1 >> 4) & 15u, v0, v1);
-    };
-    // 8 samples per batch, the next batch's loads issued before this batch's adds (the adds wait on LDS only, so
-    // the loads' latency -- the deltas were just written, L2 / MALL -- hides under them)
-    constexpr int kB = 8;
-    int64_t s = s0;
-    uint64_t bq[kB], bn[kB];
-    float vq[kB], vn[kB];
-    const auto fetch = [&](int64_t at, uint64_t (&b)[kB], float (&v)[kB]) {
+    for (int64_t c0 = s0; c0 < s1; c0 += 64) {
+        const int64_t cl = c0 + lane < s1 ? c0 + lane : s1 - 1;
+        const uint64_t bl = boards[cl];
+        const int cnt = s1 - c0 < 64 ? (int)(s1 - c0) : 64;
+        int k = 0;
+        for (; k + 8 <= cnt; k += 8) {
+            float v[8];
 #pragma unroll
-        for (int k = 0; k < kB; k++) {
-            b[k] = boards[at + k];                      // wave-uniform
-            v[k] = live ? d1[(at + k) * ld + j] : 0.0f;
-        }
-    };
-    if (s + kB <= s1) fetch(s, bq, vq);
-    for (; s + kB <= s1; s += kB) {
-        const bool more = s + 2 * kB <= s1;             // wave-uniform
-        if (more) fetch(s + kB, bn, vn);
+            for (int q = 0; q < 8; q++) v[q] = d1[(c0 + k + q) * ld + jc];
 #pragma unroll
-        for (int k = 0; k < kB; k += 2) add2(bq[k], vq[k], bq[k + 1], vq[k + 1]);
-        if (more) {
-#pragma unroll
-            for (int k = 0; k < kB; k++) {
-                bq[k] = bn[k];
-                vq[k] = vn[k];
-            }
+            for (int q = 0; q < 8; q++) add(board_of(bl, k + q), live ? v[q] : 0.0f);
         }
+        for (; k < cnt; k++) add(board_of(bl, k), live ? d1[(c0 + k) * ld + jc] : 0.0f);
     }
-    for (; s < s1; s++) add1(boards[s], live ? d1[s * ld + j] : 0.0f);
     float* slab = part + (int64_t)p * kDw1Rows * h1;
     if (live) {
-        for (int r = 0; r < 17; r++) {
-            slab[(int64_t)(34 * w + r) * h1 + j] = Ae[r * 64];
-            slab[(int64_t)(34 * w + 17 + r) * h1 + j] = Ao[r * 64];
+        const int64_t r0 = 17 * 4 * w;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            slab[(r0 + r) * h1 + j] = a0[r];
+            slab[(r0 + 17 + r) * h1 + j] = a1[r];
+            slab[(r0 + 34 + r) * h1 + j] = a2[r];
+            slab[(r0 + 51 + r) * h1 + j] = a3[r];
         }
+#pragma unroll
+        for (int q = 0; q < 4; q++) slab[(r0 + 17 * q + 16) * h1 + j] = 0.0f;
         if (w == 0) slab[(int64_t)kOneHotRows * h1 + j] = db;
     }
 }
