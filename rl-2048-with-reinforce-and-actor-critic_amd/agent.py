@@ -536,7 +536,7 @@ class ReinforceAgent:
         d1 = d1.contiguous()
         slices = -(-h1 // 64)
         cus = int(self._lib.g2048_actor_grad_waves()) // 4
-        per = max(1024, -(-m * slices // (2 * cus)))
+        per = max(1024, -(-m * slices // (8 * cus)))      # ~8 four-wave blocks per CU (the adds are latency-bound)
         nparts = -(-m // per)
         part = torch.empty(nparts, int(self._lib.g2048_onehot_dw1_slab(h1)), dtype=torch.float32, device=self.device)
         L.check(self._lib.g2048_onehot_dw1(L.ptr(boards), L.ptr(d1), h1, m, ld, per, L.ptr(part), nparts,
