@@ -2,7 +2,7 @@
 # Round 4: the whole GPU suite and smoke() on the shipped build.  Outputs under gpurun_out/r4suite/.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r4suite
+O=gpurun_out/r4suite2
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v -s -p no:cacheprovider --timeout 300 --timeout-method thread \
     > $O/gpu_tests_all.log 2>&1 || { tail -40 $O/gpu_tests_all.log; exit 1; }
