@@ -687,10 +687,14 @@ class ReinforceAgent:
                 self._onehot_dw1_into(bbuf[:used], d0buf[:used], acc1, h1=h0)
             used = 0
 
+        allb = steps.boards.reshape(-1)[steps.vidx].contiguous()     # the steps' boards, gathered once
+        hn_f = steps.has_next.to(torch.float32)
+
         def launch(s0: int, cnt: int, tgt: torch.Tensor, k: int) -> None:
             nonlocal used
-            sel = torch.arange(s0, s0 + cnt, device=self.device)
-            b = steps.boards_at(sel, k)
+            b = allb[s0:s0 + cnt]
+            if k:
+                b = self._symmetry_boards(b, k)
             if onehot and used + cnt > ldb:
                 flush_d0()
             d0 = d0buf[used:used + cnt] if onehot else None
@@ -719,9 +723,8 @@ class ReinforceAgent:
                     continue
                 s0 = starts[t]
                 lanes = steps.lane[s0:s0 + cnt]
-                hn = steps.has_next[s0:s0 + cnt]
-                vn = vb[(t + 1) & 1].index_select(0, lanes)
-                launch(s0, cnt, (steps.rewards[s0:s0 + cnt] + (gamma * vn) * hn.to(torch.float32)).contiguous(), k)
+                tgt = vb[(t + 1) & 1].index_select(0, lanes).mul_(gamma).mul_(hn_f[s0:s0 + cnt])
+                launch(s0, cnt, tgt.add_(steps.rewards[s0:s0 + cnt]), k)
                 vb[t & 1].index_copy_(0, lanes, vout[:cnt])
         flush_d0()
         pw, pb = self._deep_slab_layout(hidden, onehot)
@@ -965,9 +968,13 @@ class ReinforceAgent:
             else:
                 self._dw2(a1t, d2t, h1, h2, used, big)
 
+        # the steps' boards gathered once (k = 0) instead of per row launch
+        allb = flat[steps.vidx].contiguous()
+        hn_f = steps.has_next.to(torch.float32)
+
         def grad_launch(s0: int, cnt: int, tgt: torch.Tensor, k: int) -> None:
             nonlocal col, since_fold
-            b = flat[steps.vidx[s0:s0 + cnt]].contiguous()
+            b = allb[s0:s0 + cnt]
             if k:
                 b = self._symmetry_boards(b, k)
             ncols = -(-cnt // 32) * 32
@@ -1012,9 +1019,9 @@ class ReinforceAgent:
                     continue
                 s0 = starts[t]
                 lanes = steps.lane[s0:s0 + cnt]
-                hn = steps.has_next[s0:s0 + cnt]
-                vn = vb[(t + 1) & 1].index_select(0, lanes)
-                tgt = (steps.rewards[s0:s0 + cnt] + (gamma * vn) * hn.to(torch.float32)).contiguous()
+                # r + (gamma V(s')) m, the same roundings as the chunked path, in three in-place kernels
+                tgt = vb[(t + 1) & 1].index_select(0, lanes).mul_(gamma).mul_(hn_f[s0:s0 + cnt])
+                tgt.add_(steps.rewards[s0:s0 + cnt])
                 grad_launch(s0, cnt, tgt, k)
                 vb[t & 1].index_copy_(0, lanes, vout[:cnt])
         flush(col)
