@@ -620,8 +620,10 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
 #pragma unroll
     for (int k = 0; k < kGradTilesPerWave; k++) acc[k] = floatx16{};
     floatx16 acc0 = {};   // log2 / raw first layer: dW_0^T tile t = w
-    float dwo[4] = {0.f, 0.f, 0.f, 0.f}, dbo = 0.f;   // dW_out row tid; db_out (threads 0..3: output tid)
+    // dW_out / db_{L-1} partials of this thread's (unit, sample range); db_out (threads 0..3: output tid)
+    float dwo[4] = {0.f, 0.f, 0.f, 0.f}, dbl = 0.f, dbo = 0.f;
     const int HL = 32 * net.nt[L - 1];
+    const int oq = kDeepGradBlock / HL, oper = (32 + oq - 1) / oq;   // sample ranges of the output layer
     const float4* wout = reinterpret_cast<const float4*>(P + net.w[L]);
     const uint32_t groups = (a.n + 31u) >> 5;
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
@@ -785,12 +787,14 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
             for (int k = 0; k < 4; k++) gs[tid][k] = g[k];
         }
         __syncthreads();
-        // ---- output layer backward: dW_out row tid, db_out, delta_{L-1} in place (thread = unit)
-        if (tid < HL) {
-            float* arow = actl(L - 1) + tid * kActStride;
-            const float4 wv = wout[tid];
-            float d0 = dwo[0], d1 = dwo[1], d2 = dwo[2], d3 = dwo[3], db = dbs[(L - 1) * 256 + tid];
-            for (int n2 = 0; n2 < 32; n2++) {
+        // ---- output layer backward: dW_out, db_{L-1}, delta_{L-1} in place; thread (unit u, sample range q) of
+        //      oq ranges, so every thread works (one thread per unit ran 32 serial steps on one or two waves)
+        if (tid < oq * HL) {
+            const int u = tid % HL, q = tid / HL, n0 = q * oper, n1 = n0 + oper < 32 ? n0 + oper : 32;
+            float* arow = actl(L - 1) + u * kActStride;
+            const float4 wv = wout[u];
+            float d0 = dwo[0], d1 = dwo[1], d2 = dwo[2], d3 = dwo[3], db = dbl;
+            for (int n2 = n0; n2 < n1; n2++) {
                 const float x = arow[n2];
                 const float4 g4 = *reinterpret_cast<const float4*>(gs[n2]);
                 d0 = fmaf(x, g4.x, d0);
@@ -806,7 +810,7 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
                 arow[n2] = dl;
             }
             dwo[0] = d0; dwo[1] = d1; dwo[2] = d2; dwo[3] = d3;
-            dbs[(L - 1) * 256 + tid] = db;
+            dbl = db;
         }
         if (tid < 4) {
             float sgo = 0.f;
@@ -902,7 +906,27 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
         }
         __syncthreads();   // the next group rewrites the boards and layer 0
     }
-    // ---- this workgroup's partial slab
+    // ---- the output layer's (unit, range) partials summed per unit in range order (LDS: the activation area,
+    //      at least kOutRed floats), then this workgroup's partial slab
+    {
+        float* red = dyn;                                   // [oq][HL][5]
+        if (tid < oq * HL) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) red[tid * 5 + k] = dwo[k];
+            red[tid * 5 + 4] = dbl;
+        }
+        __syncthreads();
+        if (tid < HL) {
+            float sum[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+            for (int q = 0; q < oq; q++)
+#pragma unroll
+                for (int k = 0; k < 5; k++) sum[k] += red[(q * HL + tid) * 5 + k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) dwo[k] = sum[k];
+            dbs[(L - 1) * 256 + tid] = sum[4];
+        }
+        __syncthreads();
+    }
     float* out = a.part + (size_t)blockIdx.x * a.pslab;
 #pragma unroll
     for (int k = 0; k < kGradTilesPerWave; k++) {
@@ -998,10 +1022,15 @@ DeepGradLayout deep_grad_layout(const DeepNet& n) {
     return g;
 }
 
-int64_t deep_grad_lds_bytes(const DeepNet& n) {
+// floats of the output layer's final reduction (deep_grad_kernel: [oq][HL][5], oq HL <= the block size)
+constexpr int kOutRed = 5 * kDeepGradBlock;
+int64_t deep_grad_act_floats(const DeepNet& n) {
     int64_t units = 0;
     for (int l = 0; l < n.L; l++) units += 32 * n.nt[l];
-    return (units * kActStride + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256) * 4;
+    return units * kActStride > kOutRed ? units * kActStride : kOutRed;
+}
+int64_t deep_grad_lds_bytes(const DeepNet& n) {
+    return (deep_grad_act_floats(n) + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256) * 4;
 }
 
 // ------------------------------------------------------------------------------------ one-hot layer 1 (update)
@@ -1402,7 +1431,7 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
         a.aoff[l] = off;
         off += 32 * net.nt[l] * kActStride;
     }
-    a.lds_tail = off;
+    a.lds_tail = (int)deep_grad_act_floats(net);   // >= off: room for the output layer's reduction
     for (int l = 0; l <= net.L; l++) {
         a.pw[l] = g.pw[l];
         a.pb[l] = g.pb[l];
