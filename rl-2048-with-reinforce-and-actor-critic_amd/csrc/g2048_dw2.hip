@@ -71,7 +71,7 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
 #define G2048_DW2_SPLIT 1
 #endif
 #ifndef G2048_DW2_WIDEPIPE
-#define G2048_DW2_WIDEPIPE 1   // the wide kernel's tile-pipelined loop (0: stage by stage; tools/ A/B build)
+#define G2048_DW2_WIDEPIPE 0   // 1: the wide kernel's tile-pipelined loop (measured 3-5 % slower; tools/ A/B build)
 #endif
 
 __host__ __device__ constexpr int dw2_threads(int nt2) { return G2048_DW2_WIDE && nt2 >= 8 ? 512 : 256; }
@@ -463,10 +463,10 @@ __global__ void __launch_bounds__(dw2_threads(NT2), 1) dw2_kernel(Dw2Args a) {
     };
 
     if constexpr (G::WIDE && G2048_DW2_WIDEPIPE) {
-        // two waves per SIMD and one register set of planes (a second set does not fit 256 registers), pipelined
-        // by tile: in step it the MFMAs of stage it run row tile by row tile, and as each A tile's MFMAs are issued
-        // its registers are refilled with stage it + 1's split (then the B tiles) -- the VALU split overlaps the
-        // matrix cores inside each wave, not only across the SIMD's two waves, which every barrier re-aligns
+        // (A/B build G2048_DW2_WIDEPIPE=1) two waves per SIMD and one register set of planes, pipelined by tile: in
+        // step it the MFMAs of stage it run row tile by row tile, and as each A tile's MFMAs are issued its
+        // registers are refilled with stage it + 1's split (then the B tiles).  Measured 3-5 % slower than the
+        // stage-by-stage loop below (profiles/round4/r4c16/dw2_ab.log), configs[2] update equal.
         Planes pa;
         if (iters > 0) {
 #pragma unroll
@@ -495,7 +495,8 @@ __global__ void __launch_bounds__(dw2_threads(NT2), 1) dw2_kernel(Dw2Args a) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
     } else if constexpr (G::WIDE) {
-        // (A/B build G2048_DW2_WIDEPIPE=0) each step waits for stage it, splits it, then runs its MFMAs
+        // two waves per SIMD, one register set of planes (a second set does not fit 256 registers): each step waits
+        // for stage it, splits it and runs its MFMAs; the SIMD's other wave fills the gaps
         Planes pa;
         if (iters > 0) {
 #pragma unroll
