@@ -357,8 +357,9 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
                        const uint64_t* pol_inc, uint64_t* pol_buf, uint32_t* queue, const int32_t* order,
                        int64_t n_order, int resume, const g2048_suspend* sus, int64_t n, int64_t cap,
                        const g2048_traj* traj, void* stream);
-/* The activations of hidden layer `layer` as the deep kernels compute them: out[j * ld + u], u < its padded width
- * (tests and diagnostics: the kernels' own activation pattern). */
+/* The activations of hidden layer `layer` as g2048_deep_grad computes them (a layer with fewer than 8 output tiles
+ * and at least 2 k-tiles sums two half-k chains; g2048_deep_policy / g2048_deep_rollout keep one chain):
+ * out[j * ld + u], u < its padded width (tests and diagnostics: the gradient kernel's own activation pattern). */
 int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, int activation, int obs_mode,
                       float obs_scale, const uint64_t* boards, int64_t n, int layer, float* out, int64_t ld,
                       void* stream);

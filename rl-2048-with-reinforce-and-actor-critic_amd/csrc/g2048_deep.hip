@@ -151,10 +151,86 @@ struct DeepSmem {
     uint64_t board[32];               // the group's boards
 };
 
+// One dense hidden layer (in -> out, [unit][board] stride kActStride) whose k range is split in two halves when it
+// has fewer output tiles than 8 (the gradient kernel's waves) and at least 2 k-tiles: output tile o is
+// act(fl(c0 + c1) + b) with c0 / c1 the k-ordered MFMA chains over k-tiles [0, ntin/2) and [ntin/2, ntin) -- the
+// same values for any wave count NW, so deep_grad_kernel (8 waves) and its pattern probe deep_hidden_kernel (4 waves)
+// agree bit for bit; the halves' items keep the idle waves of a 2- or 4-tile layer busy.  The second half's chain
+// is parked in the output tile's own LDS cells until the first half adds it (one barrier inside).  The rollout /
+// policy kernels keep the single chain (their layers are already spread over their 4 waves).
+template <int ACT, int NW>
+__device__ __forceinline__ void dense_fwd_split(const float* in, float* out, const float4* __restrict__ frag,
+                                                const float* bias, int ntin, int ntout, int w) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    const auto chain = [&](int o, int t0, int t1) {
+        floatx16 c = {};
+        const float4* fo = frag + (int64_t)o * ntin * 256;
+        float4 fa[4], fb[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) fa[q] = fo[t0 * 256 + q * 64];
+        for (int t = t0; t < t1; t++) {
+            const float4* nx = fo + (t + 1 < t1 ? t + 1 : t) * 256;
+#pragma unroll
+            for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
+            const float* ib = in + (32 * t + h) * kActStride + col;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, ib[(8 * q + 0) * kActStride], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, ib[(8 * q + 2) * kActStride], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, ib[(8 * q + 4) * kActStride], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, ib[(8 * q + 6) * kActStride], c, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) fa[q] = fb[q];
+        }
+        return c;
+    };
+    const auto cell = [&](int o, int r) { return out + (32 * o + tile_row(r, h)) * kActStride + col; };
+    const auto finish = [&](int o, const floatx16& c) {
+        const float* bb = bias + 32 * o;
+#pragma unroll
+        for (int r = 0; r < 16; r++) *cell(o, r) = activate<ACT>(c[r] + bb[tile_row(r, h)]);
+    };
+    if (!(ntout < 8 && ntin >= 2)) {
+        for (int o = w; o < ntout; o += NW) finish(o, chain(o, 0, ntin));
+        return;
+    }
+    const int kh = ntin >> 1;
+    constexpr int kKeep = (7 + NW - 1) / NW;       // first-half items per wave (ntout <= 7)
+    constexpr int kSecond = (14 + NW - 1) / NW;    // item slots per wave that may hold a second half
+    floatx16 c0[kKeep];
+#pragma unroll
+    for (int r = 0; r < kKeep; r++) {
+        const int o = w + NW * r;
+        if (o < ntout) c0[r] = chain(o, 0, kh);
+    }
+#pragma unroll
+    for (int r = 0; r < kSecond; r++) {
+        const int i = w + NW * r;
+        if (i >= ntout && i < 2 * ntout) {
+            const floatx16 c1 = chain(i - ntout, kh, ntin);
+#pragma unroll
+            for (int q = 0; q < 16; q++) *cell(i - ntout, q) = c1[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kKeep; r++) {
+        const int o = w + NW * r;
+        if (o < ntout) {
+            floatx16 c = c0[r];
+#pragma unroll
+            for (int q = 0; q < 16; q++) c[q] = c[q] + *cell(o, q);
+            finish(o, c);
+        }
+    }
+}
+
 // The forward of the group's 32 boards (S.board) through every hidden layer, leaving the output layer's 8 partial
 // sums per board in S.part (the caller adds them in order p = 0..7 plus the output bias).  Every thread of the
 // workgroup calls it; it ends with a barrier.
-template <int OBS, int ACT>
+// KSPLIT: the dense layers by dense_fwd_split (the gradient kernel's forward, for the pattern probe).
+template <int OBS, int ACT, bool KSPLIT = false>
 __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, DeepSmem& S, float obs_scale) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
     // ---- first hidden layer -> S.act[0]
@@ -223,6 +299,11 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
         const int ntin = net.nt[l - 1], ntout = net.nt[l];
         const float4* __restrict__ frag = reinterpret_cast<const float4*>(P + net.w[l]) + lane;
         const float* bias = P + net.b[l];
+        if constexpr (KSPLIT) {
+            dense_fwd_split<ACT, kDeepBlock / 64>(in, out, frag, bias, ntin, ntout, w);
+            __syncthreads();
+            continue;
+        }
         for (int o = w; o < ntout; o += 4) {
             floatx16 acc = {};
             const float4* fo = frag + (int64_t)o * ntin * 256;
@@ -363,8 +444,8 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_policy_kernel(DeepPolArgs 
 }
 
 // The activations of hidden layer `layer` (the net truncated after it runs deep_forward; its output-layer partials
-// are unused): out[j * ld + u] for u < 32 nt[layer] -- bit for bit what deep_policy_kernel / deep_grad_kernel compute
-// (the same code path), for tests that impose the kernels' own activation pattern on an fp64 evaluation.
+// are unused): out[j * ld + u] for u < 32 nt[layer] -- bit for bit what deep_grad_kernel computes (dense layers by
+// dense_fwd_split), for tests that impose the gradient kernel's own activation pattern on an fp64 evaluation.
 template <int OBS, int ACT>
 __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net, const float* packed,
                                                                      const uint64_t* boards, uint32_t n, float obs_scale,
@@ -378,7 +459,7 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net,
             S.board[tid] = boards[j < n ? j : n - 1u];
         }
         __syncthreads();
-        deep_forward<OBS, ACT>(net, packed, S, obs_scale);
+        deep_forward<OBS, ACT, true>(net, packed, S, obs_scale);
         const float* act = S.act[layer & 1];
         for (int e = tid; e < 32 * H; e += kDeepBlock) {
             const int b = e / H, u = e % H;
@@ -696,35 +777,7 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
             float* out = actl(l);
             const int ntin = net.nt[l - 1], ntout = net.nt[l];
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(P + net.w[l]) + lane;
-            const float* bias = P + net.b[l];
-            for (int o = w; o < ntout; o += kDeepGradWaves) {
-                floatx16 c = {};
-                const float4* fo = frag + (int64_t)o * ntin * 256;
-                float4 fa[4], fb[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) fa[q] = fo[q * 64];
-                for (int t = 0; t < ntin; t++) {
-                    const float4* nx = fo + (t + 1 < ntin ? t + 1 : t) * 256;
-#pragma unroll
-                    for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
-                    const float* ib = in + (32 * t + h) * kActStride + col;
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, ib[(8 * q + 0) * kActStride], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, ib[(8 * q + 2) * kActStride], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, ib[(8 * q + 4) * kActStride], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, ib[(8 * q + 6) * kActStride], c, 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int q = 0; q < 4; q++) fa[q] = fb[q];
-                }
-                const float* bb = bias + 32 * o;
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int u = tile_row(r, h);
-                    out[(32 * o + u) * kActStride + col] = activate<ACT>(c[r] + bb[u]);
-                }
-            }
+            dense_fwd_split<ACT, kDeepGradWaves>(in, out, frag, P + net.b[l], ntin, ntout, w);
             __syncthreads();
         }
         // ---- output layer partials (as deep_forward; threads 0..255)
