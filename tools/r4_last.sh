@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4 end-of-session record on the shipped build: full GPU suite, smoke, the driver's bench command, rocprofv3
-# kernel stats of the step kernel (200 launches) and of the runner config, PMC passes of the configs[2] update.
+# kernel stats of the step kernel (200 launches), PMC passes of the configs[2] update, the runner config's kernel stats.
 # Outputs under gpurun_out/r4last/.
 set -o pipefail
 export TMPDIR=/tmp
@@ -16,4 +16,6 @@ grep '^{' $O/bench_driver_cmd.log | cut -c1-300
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_step -o step -- \
     python3 bench.py --no-cpu-baseline --no-policy --no-train --no-refconfig --traffic off --steps 200 --warmup 20 > $O/prof_step.log 2>&1 || exit 1
 EPISODES=1048576 PMC_OUT=r4last/pmc_configs2 bash tools/pmc_grad.sh || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_refconf -o rc -- python3 tools/bench_refconfig.py --label round4 > $O/refconf.log 2>&1 || { tail -30 $O/refconf.log; exit 1; }
+grep '^{' $O/refconf.log | cut -c1-330
 echo DONE > $O/done.log
