@@ -59,6 +59,11 @@ int fail(int code, const std::string& msg) {
 #ifndef G2048_LEAN
 #define G2048_LEAN 1
 #endif
+// 1: a lane whose episode ends stores its step outputs in the sweep before the deferred reset rewrites them (whole
+// lines); 0 (A/B builds only): it leaves them to the reset pass
+#ifndef G2048_RESET_FULL_STORES
+#define G2048_RESET_FULL_STORES 1
+#endif
 
 
 
@@ -398,14 +403,21 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     if (EXTRA && a.out.reward64) st(a.out.reward64, i, r);
     if (LIST && a.out.merged) st(a.out.merged, i, s.list);
     if (EXTRA && a.out.score_add) st(a.out.score_add, i, s.score);
-    if ((done || trunc) && a.auto_reset) {
-        reset = true;   // board / lane state / obs are written by reset_lane after the loop
+    reset = (done || trunc) && a.auto_reset;   // board / lane state / obs are rewritten by reset_lane after the loop
+#if !G2048_RESET_FULL_STORES
+    if (reset) {
         st(a.out.flags, i, (uint8_t)(fl | G2048_F_RESET));
         return m;
     }
+#endif
+    // A resetting lane stores this step's board / state / stream / mask / obs like any other lane (reset_lane
+    // overwrites them after the loop): the sweep's stores then cover whole lines.  A hole left for the reset pass
+    // is written back as a partial line, and filled later by another partial write; HBM3E has no byte mask, so
+    // each partial line is a read-modify-write in the memory controller (measured: the first steps after the
+    // synthetic start, 2-3 % of lanes resetting, ran 34 us against 29 us later; tools/step_launch_probe.py).
     uint32_t nst = sc | (mt << G2048_LS_MAXT_SHIFT) | ((done || trunc) ? 0u : G2048_LS_ACTIVE);
     if constexpr (RNG == G2048_RNG_PCG64) nst |= x.g.has_uint32 ? G2048_LS_HAS_U32 : 0u;
-    st(a.out.flags, i, (uint8_t)fl);
+    st(a.out.flags, i, (uint8_t)(fl | (reset ? G2048_F_RESET : 0u)));
     st(L.board, i, m);
     st(L.state, i, nst);
     if constexpr (RNG == G2048_RNG_PCG64) store_pcg(L, i, x.g, false);
