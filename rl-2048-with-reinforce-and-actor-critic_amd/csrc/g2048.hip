@@ -107,9 +107,16 @@ __device__ __forceinline__ void st(T* p, uint32_t idx, T v) {
 
 // observation stores are non-temporal (streaming): measured on MI355X, onehot obs (1,088 B/board) 260 -> 241 us at
 // 1M boards and 1050 -> 908 us at 4M; log2 obs unchanged (tools/ab_nt.sh, profiles/round1/ab_nt.log)
+#ifndef G2048_OBS_NT
+#define G2048_OBS_NT 1   // 0: plain stores (A/B builds only)
+#endif
 __device__ __forceinline__ void st_obs(float4* base, int q, float4 v) {
+#if G2048_OBS_NT
     typedef float f4v __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(base + q));
+#else
+    base[q] = v;
+#endif
 }
 
 struct LineFn {

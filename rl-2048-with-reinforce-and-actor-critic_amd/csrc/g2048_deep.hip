@@ -151,6 +151,44 @@ struct DeepSmem {
     uint64_t board[32];               // the group's boards
 };
 
+// The k-ordered MFMA chain of one output tile over k-tiles [t0, t1): A = the tile's weight fragments `fo` (4 float4
+// per lane per k-tile, streamed from L2), B = the activation rows `in` (LDS).  Two fragment register sets alternate
+// (no copy between them), and a scheduling barrier after each prefetch keeps the next k-tile's loads issued ahead of
+// this k-tile's 16 MFMAs -- without it hipcc sank every fragment load next to its MFMA and waited for it there (four
+// L2 round trips per k-tile).  Same MFMAs in the same order as a plain loop.
+__device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, const float* in, int t0, int t1, int h,
+                                               int col) {
+    floatx16 c = {};
+    if (t0 >= t1) return c;
+    float4 fa[4], fb[4];
+    const auto tile = [&](const float4 (&f)[4], int t) {
+        const float* ib = in + (32 * t + h) * kActStride + col;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].x, ib[(8 * q + 0) * kActStride], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].y, ib[(8 * q + 2) * kActStride], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].z, ib[(8 * q + 4) * kActStride], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].w, ib[(8 * q + 6) * kActStride], c, 0, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int q = 0; q < 4; q++) fa[q] = fo[t0 * 256 + q * 64];
+    int t = t0;
+    for (; t + 1 < t1; t += 2) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) fb[q] = fo[(t + 1) * 256 + q * 64];
+        __builtin_amdgcn_sched_barrier(0);
+        tile(fa, t);
+        const int tn = t + 2 < t1 ? t + 2 : t + 1;   // past the end: a harmless reload of the last k-tile
+#pragma unroll
+        for (int q = 0; q < 4; q++) fa[q] = fo[tn * 256 + q * 64];
+        __builtin_amdgcn_sched_barrier(0);
+        tile(fb, t + 1);
+    }
+    if (t < t1) tile(fa, t);
+    return c;
+}
+
 // One dense hidden layer (in -> out, [unit][board] stride kActStride) whose k range is split in two halves when it
 // has fewer output tiles than 8 (the gradient kernel's waves) and at least 2 k-tiles: output tile o is
 // act(fl(c0 + c1) + b) with c0 / c1 the k-ordered MFMA chains over k-tiles [0, ntin/2) and [ntin/2, ntin) -- the
@@ -163,33 +201,16 @@ __device__ __forceinline__ void dense_fwd_split(const float* in, float* out, con
                                                 const float* bias, int ntin, int ntout, int w) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
     const auto chain = [&](int o, int t0, int t1) {
-        floatx16 c = {};
-        const float4* fo = frag + (int64_t)o * ntin * 256;
-        float4 fa[4], fb[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) fa[q] = fo[t0 * 256 + q * 64];
-        for (int t = t0; t < t1; t++) {
-            const float4* nx = fo + (t + 1 < t1 ? t + 1 : t) * 256;
-#pragma unroll
-            for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
-            const float* ib = in + (32 * t + h) * kActStride + col;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, ib[(8 * q + 0) * kActStride], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, ib[(8 * q + 2) * kActStride], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, ib[(8 * q + 4) * kActStride], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, ib[(8 * q + 6) * kActStride], c, 0, 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++) fa[q] = fb[q];
-        }
-        return c;
+        return frag_chain(frag + (int64_t)o * ntin * 256, in, t0, t1, h, col);
     };
     const auto cell = [&](int o, int r) { return out + (32 * o + tile_row(r, h)) * kActStride + col; };
     const auto finish = [&](int o, const floatx16& c) {
         const float* bb = bias + 32 * o;
+        float bv[16];   // all 16 bias loads issued before the first use (one L2 round trip, not four)
 #pragma unroll
-        for (int r = 0; r < 16; r++) *cell(o, r) = activate<ACT>(c[r] + bb[tile_row(r, h)]);
+        for (int r = 0; r < 16; r++) bv[r] = bb[tile_row(r, h)];
+#pragma unroll
+        for (int r = 0; r < 16; r++) *cell(o, r) = activate<ACT>(c[r] + bv[r]);
     };
     if (!(ntout < 8 && ntin >= 2)) {
         for (int o = w; o < ntout; o += NW) finish(o, chain(o, 0, ntin));
@@ -229,6 +250,46 @@ __device__ __forceinline__ void dense_fwd_split(const float* in, float* out, con
 // The forward of the group's 32 boards (S.board) through every hidden layer, leaving the output layer's 8 partial
 // sums per board in S.part (the caller adds them in order p = 0..7 plus the output bias).  Every thread of the
 // workgroup calls it; it ends with a barrier.
+// cells of the one-hot gather unrolled per batch of loads (16 / this L2 round trips per group when every tile is
+// present; x 4 tiles for the gradient kernel, x 8 / 2 for deep_forward)
+#ifndef G2048_DEEP_GATHER_UNROLL
+#define G2048_DEEP_GATHER_UNROLL 4
+#endif
+
+// One-hot layer-0 gather of one board: acc[m] += W1 row (17 c + e_c), units 32 (m0 + m) + 4 k .. + 3 (`tab` points
+// at unit 32 m0 + 4 k of row 0), summed over the 16 cells in cell order, for the tiles m < mcount (wave-uniform).
+// With all NM tiles present the loads carry no guard, so a batch of cells issues back to back: a per-load guard
+// made the compiler wait for every load before the next (one L2 round trip per load).  Same adds, same order
+// either way, so every kernel that gathers (rollout, policy, probe, gradient) computes the same bits.
+template <int NM>
+__device__ __forceinline__ void onehot_gather(const float* tab, uint64_t b, int H, int mcount, float4 (&acc)[NM]) {
+    const auto add = [](float4& s, const float4 v) {
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+    };
+    if (mcount >= NM) {
+#pragma unroll(NM == 4 ? G2048_DEEP_GATHER_UNROLL : (G2048_DEEP_GATHER_UNROLL + 1) / 2)
+        for (int c = 0; c < 16; c++) {
+            const float* row = tab + (int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * H;
+            float4 v[NM];
+#pragma unroll
+            for (int m = 0; m < NM; m++) v[m] = *reinterpret_cast<const float4*>(row + 32 * m);
+#pragma unroll
+            for (int m = 0; m < NM; m++) add(acc[m], v[m]);
+        }
+    } else {
+#pragma unroll 4
+        for (int c = 0; c < 16; c++) {
+            const float* row = tab + (int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * H;
+#pragma unroll
+            for (int m = 0; m < NM; m++)
+                if (m < mcount) add(acc[m], *reinterpret_cast<const float4*>(row + 32 * m));
+        }
+    }
+}
+
 // KSPLIT: the dense layers by dense_fwd_split (the gradient kernel's forward, for the pattern probe).
 template <int OBS, int ACT, bool KSPLIT = false>
 __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, DeepSmem& S, float obs_scale) {
@@ -246,20 +307,7 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
             float4 acc[8];
 #pragma unroll
             for (int m = 0; m < 8; m++) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 4
-            for (int c = 0; c < 16; c++) {
-                const float* row = tab + (int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * H;
-#pragma unroll
-                for (int m = 0; m < 8; m++) {
-                    if (m < nt0) {
-                        const float4 v = *reinterpret_cast<const float4*>(row + 32 * m);
-                        acc[m].x += v.x;
-                        acc[m].y += v.y;
-                        acc[m].z += v.z;
-                        acc[m].w += v.w;
-                    }
-                }
-            }
+            onehot_gather<8>(tab, b, H, nt0, acc);
 #pragma unroll
             for (int m = 0; m < 8; m++) {
                 if (m < nt0) {
@@ -305,26 +353,7 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
             continue;
         }
         for (int o = w; o < ntout; o += 4) {
-            floatx16 acc = {};
-            const float4* fo = frag + (int64_t)o * ntin * 256;
-            float4 fa[4], fb[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) fa[q] = fo[q * 64];
-            for (int t = 0; t < ntin; t++) {
-                const float4* nx = fo + (t + 1 < ntin ? t + 1 : t) * 256;
-#pragma unroll
-                for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
-                const float* ib = in + (32 * t + h) * kActStride + col;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, ib[(8 * q + 0) * kActStride], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, ib[(8 * q + 2) * kActStride], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, ib[(8 * q + 4) * kActStride], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, ib[(8 * q + 6) * kActStride], acc, 0, 0, 0);
-                }
-#pragma unroll
-                for (int q = 0; q < 4; q++) fa[q] = fb[q];
-            }
+            const floatx16 acc = frag_chain(frag + (int64_t)o * ntin * 256, in, 0, ntin, h, col);
             const float* bb = bias + 32 * o;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
@@ -725,20 +754,7 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
                 float4 ac[4];
 #pragma unroll
                 for (int m = 0; m < 4; m++) ac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 4
-                for (int c = 0; c < 16; c++) {
-                    const float* row = tab + (int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * H;
-#pragma unroll
-                    for (int m = 0; m < 4; m++) {
-                        if (m0 + m < nt0) {
-                            const float4 v = *reinterpret_cast<const float4*>(row + 32 * m);
-                            ac[m].x += v.x;
-                            ac[m].y += v.y;
-                            ac[m].z += v.z;
-                            ac[m].w += v.w;
-                        }
-                    }
-                }
+                onehot_gather<4>(tab, b, H, nt0 - m0, ac);
 #pragma unroll
                 for (int m = 0; m < 4; m++) {
                     if (m0 + m < nt0) {
@@ -896,26 +912,7 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(a.bpacked + a.boff[l]) + lane;
             float* Aw = actl(l - 1);
             for (int o = w; o < ntin; o += kDeepGradWaves) {
-                floatx16 c = {};
-                const float4* fo = frag + (int64_t)o * ntout * 256;
-                float4 fa[4], fb[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) fa[q] = fo[q * 64];
-                for (int t = 0; t < ntout; t++) {
-                    const float4* nx = fo + (t + 1 < ntout ? t + 1 : t) * 256;
-#pragma unroll
-                    for (int q = 0; q < 4; q++) fb[q] = nx[q * 64];
-                    const float* ib = D + (32 * t + h) * kActStride + col;
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, ib[(8 * q + 0) * kActStride], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, ib[(8 * q + 2) * kActStride], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, ib[(8 * q + 4) * kActStride], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, ib[(8 * q + 6) * kActStride], c, 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int q = 0; q < 4; q++) fa[q] = fb[q];
-                }
+                const floatx16 c = frag_chain(frag + (int64_t)o * ntout * 256, D, 0, ntout, h, col);
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
                     float* pa = Aw + (32 * o + tile_row(r, h)) * kActStride + col;
