@@ -308,15 +308,18 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
 #pragma unroll
             for (int m = 0; m < 8; m++) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
             onehot_gather<8>(tab, b, H, nt0, acc);
+            float4 bv[8];   // bias loads issued together (clamped index: always a valid address)
+#pragma unroll
+            for (int m = 0; m < 8; m++)
+                bv[m] = *reinterpret_cast<const float4*>(P + net.b[0] + 32 * (m < nt0 ? m : nt0 - 1) + 4 * k);
 #pragma unroll
             for (int m = 0; m < 8; m++) {
                 if (m < nt0) {
                     const int u = 32 * m + 4 * k;
-                    const float4 bv = *reinterpret_cast<const float4*>(P + net.b[0] + u);
-                    out[(u + 0) * kActStride + bb] = activate<ACT>(acc[m].x + bv.x);
-                    out[(u + 1) * kActStride + bb] = activate<ACT>(acc[m].y + bv.y);
-                    out[(u + 2) * kActStride + bb] = activate<ACT>(acc[m].z + bv.z);
-                    out[(u + 3) * kActStride + bb] = activate<ACT>(acc[m].w + bv.w);
+                    out[(u + 0) * kActStride + bb] = activate<ACT>(acc[m].x + bv[m].x);
+                    out[(u + 1) * kActStride + bb] = activate<ACT>(acc[m].y + bv[m].y);
+                    out[(u + 2) * kActStride + bb] = activate<ACT>(acc[m].z + bv[m].z);
+                    out[(u + 3) * kActStride + bb] = activate<ACT>(acc[m].w + bv[m].w);
                 }
             }
         } else {
@@ -355,11 +358,11 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
         for (int o = w; o < ntout; o += 4) {
             const floatx16 acc = frag_chain(frag + (int64_t)o * ntin * 256, in, 0, ntin, h, col);
             const float* bb = bias + 32 * o;
+            float bv[16];   // the 16 bias loads issued before the first use
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int u = tile_row(r, h);
-                out[(32 * o + u) * kActStride + col] = activate<ACT>(acc[r] + bb[u]);
-            }
+            for (int r = 0; r < 16; r++) bv[r] = bb[tile_row(r, h)];
+#pragma unroll
+            for (int r = 0; r < 16; r++) out[(32 * o + tile_row(r, h)) * kActStride + col] = activate<ACT>(acc[r] + bv[r]);
         }
         __syncthreads();
     }
