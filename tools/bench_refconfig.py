@@ -3,7 +3,7 @@
 the given episode counts, against the package found under --repo (so a checkout of an earlier round can be timed
 by the same script).  One warm-up iteration at the first size; prints one JSON object per size.
 
-    python tools/bench_refconfig.py [--repo DIR] [--episodes 65536 1048576]
+    python tools/bench_refconfig.py [--repo DIR] [--episodes 65536 1048576]     (G2048_LIB=<path>: an A/B build)
 """
 import argparse
 import json
@@ -17,6 +17,10 @@ ap.add_argument("--episodes", type=int, nargs="+", default=[65536, 1 << 20])
 ap.add_argument("--label", default="")
 args = ap.parse_args()
 sys.path.insert(0, os.path.abspath(args.repo))
+if os.environ.get("G2048_LIB"):   # an A/B build of the library
+    from rl2048_amd import _lib as _L0
+
+    _L0.use_library_for_tools(os.environ["G2048_LIB"])
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
