@@ -1,0 +1,113 @@
+#!/bin/bash
+# One parameterised GPU-box script (replaces round 3/4's one-off r3_*.sh / r4_*.sh checks): runs the named steps in
+# order, each under its own time limit, and stops at the first failure.  Outputs under gpurun_out/$RUN/.
+#
+#   RUN=r5a tools/gpu.sh tests:tests/test_gpu_deep.py refconf pmc_refconf:262144 bench smoke prof_step
+#
+# steps:
+#   tests[:ARGS]        pytest -m gpu over ARGS (space-separated after the colon; default: the whole suite)
+#   smoke               __graft_entry__.smoke()
+#   bench               the driver's bench command (bench.py --gpus 1 --steps 20 --warmup 5)
+#   prof_step           rocprofv3 kernel stats of 200 step-kernel launches (bench.py step leg only)
+#   refconf[:EPISODES]  tools/bench_refconfig.py under rocprofv3 --kernel-trace --stats; the top kernels printed
+#   pmc_refconf[:E]     PMC passes over the runner config at E episodes (default 262144): SQ busy / LDS, SQ waits,
+#                       FETCH_SIZE, WRITE_SIZE, TCC hit / miss -- one counter group per run; tools/pmc_grad_summary.py
+#   pmc_configs2        the same passes over one configs[2] update (tools/bench_update.py, 1,048,576 episodes)
+#   abref:LIB[:N]       N (default 2) interleaved runner-config iterations: the shipped library, then LIB
+#   cmd:'...'           any other command (its own timeout inside)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+O=gpurun_out/${RUN:-gpu}
+mkdir -p "$O"
+
+top_kernels() {   # $1 = kernel_stats.csv
+    python3 - "$1" <<'PY'
+import csv, sys
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: -float(r["TotalDurationNs"]))
+for r in rows[:12]:
+    print(f"{float(r['TotalDurationNs'])/1e6:9.1f} ms {int(r['Calls']):6d} calls {float(r['AverageNs'])/1e3:9.1f} us  {r['Name'][:96]}")
+PY
+}
+
+pmc_passes() {   # $1 = dir, rest = command
+    local d=$1
+    shift
+    local P="--kernel-trace --output-format csv"
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$d/trace" -o run -- "$@" > "$d/trace.log" 2>&1 &&
+    timeout -s KILL 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU GRBM_GUI_ACTIVE $P -d "$d/sq" -o run -- "$@" > "$d/sq.log" 2>&1 &&
+    timeout -s KILL 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS \
+        SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_COEXEC_CYCLES $P -d "$d/sqw" -o run -- "$@" > "$d/sqw.log" 2>&1 &&
+    timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE $P -d "$d/fetch" -o run -- "$@" > "$d/fetch.log" 2>&1 &&
+    timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE $P -d "$d/write" -o run -- "$@" > "$d/write.log" 2>&1 &&
+    timeout -s KILL 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum $P -d "$d/tcc" -o run -- "$@" > "$d/tcc.log" 2>&1 &&
+    python3 tools/pmc_grad_summary.py "$d" > "$d/summary.jsonl" && cat "$d/summary.jsonl"
+}
+
+for step in "$@"; do
+    name=${step%%:*}
+    arg=""
+    [[ "$step" == *:* ]] && arg=${step#*:}
+    echo "=== $step" | cut -c1-200
+    case $name in
+    tests)
+        # shellcheck disable=SC2086
+        timeout -k 10 900 python3 -u -m pytest ${arg:-tests} -m gpu -v -s -p no:cacheprovider --timeout 300 \
+            --timeout-method thread > "$O/tests_${RUN:-gpu}_$SECONDS.log" 2>&1
+        rc=$?
+        tail -3 "$(ls -t "$O"/tests_*.log | head -1)" || true
+        [ $rc -eq 0 ] || { grep -E "FAILED|Error|error" "$(ls -t "$O"/tests_*.log | head -1)" | head -40; exit 1; }
+        ;;
+    smoke)
+        timeout -k 10 200 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > "$O/smoke.log" 2>&1 ||
+            { tail -20 "$O/smoke.log"; exit 1; }
+        tail -1 "$O/smoke.log"
+        ;;
+    bench)
+        timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver_cmd.log" 2>&1 ||
+            { tail -20 "$O/bench_driver_cmd.log"; exit 1; }
+        grep '^{' "$O/bench_driver_cmd.log" | cut -c1-400
+        ;;
+    prof_step)
+        timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_step" -o step -- \
+            python3 bench.py --no-cpu-baseline --no-policy --no-train --no-refconfig --traffic off --steps 200 --warmup 20 \
+            > "$O/prof_step.log" 2>&1 || { tail -20 "$O/prof_step.log"; exit 1; }
+        grep '^{' "$O/prof_step.log" | cut -c1-300
+        top_kernels "$O/prof_step/step_kernel_stats.csv"
+        ;;
+    refconf)
+        # shellcheck disable=SC2086
+        timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_refconf" -o rc -- \
+            python3 tools/bench_refconfig.py --label "${RUN:-gpu}" ${arg:+--episodes $arg} > "$O/refconf.log" 2>&1 ||
+            { tail -30 "$O/refconf.log"; exit 1; }
+        grep '^{' "$O/refconf.log" | cut -c1-330
+        top_kernels "$O/prof_refconf/rc_kernel_stats.csv"
+        ;;
+    pmc_refconf)
+        mkdir -p "$O/pmc_refconf"
+        pmc_passes "$O/pmc_refconf" python3 tools/bench_refconfig.py --episodes "${arg:-262144}" || exit 1
+        ;;
+    pmc_configs2)
+        mkdir -p "$O/pmc_configs2"
+        pmc_passes "$O/pmc_configs2" python3 tools/bench_update.py --episodes 1048576 --repeats 1 --critic || exit 1
+        ;;
+    abref)
+        lib=${arg%%:*}
+        n=2
+        [[ "$arg" == *:* ]] && n=${arg#*:}
+        for r in $(seq "$n"); do
+            timeout -k 10 300 python3 tools/bench_refconfig.py --label shipped > "$O/ab_shipped_$r.log" 2>&1 || exit 1
+            G2048_LIB=$lib timeout -k 10 300 python3 tools/bench_refconfig.py --label "$(basename "$lib")" > "$O/ab_var_$r.log" 2>&1 || exit 1
+        done
+        grep -h '^{' "$O"/ab_*.log | cut -c1-220
+        ;;
+    cmd)
+        bash -o pipefail -c "$arg" || exit 1
+        ;;
+    *)
+        echo "unknown step $step"
+        exit 2
+        ;;
+    esac
+done
+echo DONE > "$O/done.log"
