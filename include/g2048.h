@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 13
+#define G2048_ABI_VERSION 14
 
 /* status codes */
 #define G2048_OK 0
@@ -357,15 +357,18 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
                        const uint64_t* pol_inc, uint64_t* pol_buf, uint32_t* queue, const int32_t* order,
                        int64_t n_order, int resume, const g2048_suspend* sus, int64_t n, int64_t cap,
                        const g2048_traj* traj, void* stream);
-/* The activations of hidden layer `layer` as g2048_deep_grad computes them (a layer with fewer than 8 output tiles
- * and at least 2 k-tiles sums two half-k chains; g2048_deep_policy / g2048_deep_rollout keep one chain):
+/* The activations of hidden layer `layer` as g2048_deep_grad computes them (in its 8-wave instantiations -- nets of
+ * 41..64 dense tiles -- a layer with fewer than 8 output tiles and at least 2 k-tiles sums two half-k chains; the
+ * 4-wave one and g2048_deep_policy / g2048_deep_rollout keep one chain):
  * out[j * ld + u], u < its padded width (tests and diagnostics: the gradient kernel's own activation pattern). */
 int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, int activation, int obs_mode,
                       float obs_scale, const uint64_t* boards, int64_t n, int layer, float* out, int64_t ld,
                       void* stream);
 /* update_batch's actor or critic gradient (src/reinforce_agent.py:403-555, _backpropagation :639-678) fused for a
  * packed deep net (forward + loss gradient + backward in one kernel, 32 samples per workgroup step), covered when
- * g2048_deep_grad_slab() >= 0 (at most 48 dense 32x32 weight-gradient tiles: [256, 128, 64] and smaller).
+ * g2048_deep_grad_slab() >= 0 (at most 64 dense 32x32 weight-gradient tiles: [256, 256], [256, 128, 64] and
+ * smaller).  ABI 14: nets of at most 40 tiles run two 4-wave workgroups per CU -- pass nparts =
+ * g2048_deep_grad_parts() (any nparts >= 1 is correct; that one fills the chip).
  * grad_packed: g2048_deep_grad_pack (the dense layers' weights in backward-fragment order; re-pack after every
  * update).  Actor: coef = advantage x step weight, actions; critic (critic = 1): coef = step weight, target =
  * r + gamma V(s') m, loss 0 MSE / 1 Huber, delta_out = target - V, value_out = V (NULL ok).  partials [nparts][slab]
@@ -375,6 +378,8 @@ int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, 
  * first layer's deltas for g2048_onehot_dw1 (ld = H0p). */
 int64_t g2048_deep_grad_pack_size(int obs_mode, int n_hidden, const int32_t* hidden);
 int64_t g2048_deep_grad_slab(int obs_mode, int n_hidden, const int32_t* hidden);
+/* the workgroup count that fills the current device for this net (ABI 14; -1 when g2048_deep_grad_slab() < 0) */
+int g2048_deep_grad_parts(int obs_mode, int n_hidden, const int32_t* hidden);
 int g2048_deep_grad_pack(const float* const* W, int obs_mode, int n_hidden, const int32_t* hidden, float* packed,
                          int64_t packed_len, void* stream);
 int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden, const int32_t* hidden,
@@ -390,8 +395,10 @@ int g2048_onehot_layer1(const float* W1, const float* b1, int h1, int activation
 /* floats of one g2048_onehot_dw1 partial slab: 272 h1 (dW1) + h1 (db1) */
 int64_t g2048_onehot_dw1_slab(int h1);
 /* dW1 = X^T D1 and db1 = sum D1 of a one-hot first layer (X one-hot, D1 = d1[s * ld + j] the layer-1 deltas): slab
- * p of partials (nparts = ceil(m / per)) holds the sums over samples [p per, (p + 1) per) -- a 16-row scatter-add
- * per sample in sample order; fold them with g2048_fold_partials. */
+ * p of partials (nparts = ceil(m / per)) holds the sums over samples [p per, (p + 1) per) -- ABI 14: an fp32
+ * accumulation on the bf16 MFMA of the exact products of the one-hot with each delta's three bf16 planes
+ * (deterministic, one 8-wave workgroup per slab: pick per so that nparts ~ the CU count); fold them with
+ * g2048_fold_partials. */
 int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m, int64_t ld, int64_t per,
                      float* partials, int64_t nparts, void* stream);
 

@@ -534,9 +534,8 @@ class ReinforceAgent:
         if m == 0:
             return
         d1 = d1.contiguous()
-        slices = -(-h1 // 64)
         cus = int(self._lib.g2048_actor_grad_waves()) // 4
-        per = max(1024, -(-m * slices // (8 * cus)))      # ~8 four-wave blocks per CU (the adds are latency-bound)
+        per = max(512, -(-m // (16 * cus)) * 16)         # one 8-wave MFMA workgroup per CU, whole 16-sample steps
         nparts = -(-m // per)
         part = torch.empty(nparts, int(self._lib.g2048_onehot_dw1_slab(h1)), dtype=torch.float32, device=self.device)
         L.check(self._lib.g2048_onehot_dw1(L.ptr(boards), L.ptr(d1), h1, m, ld, per, L.ptr(part), nparts,
@@ -544,7 +543,7 @@ class ReinforceAgent:
         self._fold(part, acc)
 
     def _deep_grad_spec(self, params, out_dim: int):
-        """_deep_spec when g2048_deep_grad covers the net (at most 48 dense 32x32 weight-gradient tiles), else None."""
+        """_deep_spec when g2048_deep_grad covers the net (at most 64 dense 32x32 weight-gradient tiles), else None."""
         if not self.use_fused_grad:
             return None
         d = self._deep_spec(params, out_dim)
@@ -597,7 +596,7 @@ class ReinforceAgent:
         critic = deltas is not None
         packed = self._pack_deep(params, dspec, slot, out_dim)
         bpacked = self._pack_deep_grad(params, dspec, slot)
-        nparts = int(self._lib.g2048_actor_grad_waves()) // 4          # one workgroup per CU
+        nparts = int(self._lib.g2048_deep_grad_parts(obs_code, len(hidden), harr))   # fills the chip
         slab = int(self._lib.g2048_deep_grad_slab(obs_code, len(hidden), harr))
         part = torch.empty(nparts, slab, dtype=torch.float32, device=self.device)
         acc = torch.zeros(slab, dtype=torch.float64, device=self.device)
@@ -658,7 +657,7 @@ class ReinforceAgent:
         loss = {"mse": 0, "huber": 1}[c.critic_loss_type]
         packed = self._pack_deep(params, dspec, "critic", 1)
         bpacked = self._pack_deep_grad(params, dspec, "critic")
-        nparts = int(self._lib.g2048_actor_grad_waves()) // 4
+        nparts = int(self._lib.g2048_deep_grad_parts(obs_code, len(hidden), harr))
         slab = int(self._lib.g2048_deep_grad_slab(obs_code, len(hidden), harr))
         part = torch.empty(nparts, slab, dtype=torch.float32, device=self.device)
         acc = torch.zeros(slab, dtype=torch.float64, device=self.device)

@@ -23,6 +23,8 @@
 // sample and slice).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "g2048.h"
 #include "g2048_core.h"
 
@@ -261,7 +263,7 @@ __device__ __forceinline__ void dense_fwd_split(const float* in, float* out, con
 // With all NM tiles present the loads carry no guard, so a batch of cells issues back to back: a per-load guard
 // made the compiler wait for every load before the next (one L2 round trip per load).  Same adds, same order
 // either way, so every kernel that gathers (rollout, policy, probe, gradient) computes the same bits.
-template <int NM>
+template <int NM, int UNROLL = (NM == 4 ? G2048_DEEP_GATHER_UNROLL : (G2048_DEEP_GATHER_UNROLL + 1) / 2)>
 __device__ __forceinline__ void onehot_gather(const float* tab, uint64_t b, int H, int mcount, float4 (&acc)[NM]) {
     const auto add = [](float4& s, const float4 v) {
         s.x += v.x;
@@ -270,7 +272,7 @@ __device__ __forceinline__ void onehot_gather(const float* tab, uint64_t b, int 
         s.w += v.w;
     };
     if (mcount >= NM) {
-#pragma unroll(NM == 4 ? G2048_DEEP_GATHER_UNROLL : (G2048_DEEP_GATHER_UNROLL + 1) / 2)
+#pragma unroll UNROLL
         for (int c = 0; c < 16; c++) {
             const float* row = tab + (int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * H;
             float4 v[NM];
@@ -477,8 +479,9 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_policy_kernel(DeepPolArgs 
 
 // The activations of hidden layer `layer` (the net truncated after it runs deep_forward; its output-layer partials
 // are unused): out[j * ld + u] for u < 32 nt[layer] -- bit for bit what deep_grad_kernel computes (dense layers by
-// dense_fwd_split), for tests that impose the gradient kernel's own activation pattern on an fp64 evaluation.
-template <int OBS, int ACT>
+// dense_fwd_split when the net's gradient instantiation splits k, else deep_forward's chain), for tests that impose
+// the gradient kernel's own activation pattern on an fp64 evaluation.
+template <int OBS, int ACT, bool KSPLIT>
 __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net, const float* packed,
                                                                      const uint64_t* boards, uint32_t n, float obs_scale,
                                                                      float* out, uint32_t ld) {
@@ -491,7 +494,7 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net,
             S.board[tid] = boards[j < n ? j : n - 1u];
         }
         __syncthreads();
-        deep_forward<OBS, ACT, true>(net, packed, S, obs_scale);
+        deep_forward<OBS, ACT, KSPLIT>(net, packed, S, obs_scale);
         const float* act = S.act[layer & 1];
         for (int e = tid; e < 32 * H; e += kDeepBlock) {
             const int b = e / H, u = e % H;
@@ -674,11 +677,21 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArg
 //     written out ([n][H0p], row-major) for g2048_onehot_dw1's scatter;
 //   * biases: per-thread sums (unit = thread).
 // Every workgroup writes one fp32 partial slab (g2048_fold_partials sums them in fp64).
-// 8 waves x 6 dense dW tiles held in accumulator registers (x 16 floats): two waves per SIMD, so one wave's MFMA
-// chains run while the other's gathers, epilogues and barriers do (a 4-wave workgroup with 12 tiles per wave took
-// the whole register file, one wave per SIMD)
-constexpr int kDeepGradWaves = 8, kDeepGradBlock = 64 * kDeepGradWaves;
-constexpr int kGradTilesPerWave = 6;
+// Three instantiations by the net's dense dW tile count (deep_grad_variant), every one at two waves per SIMD so that
+// one wave's MFMA chains run while the other's gathers, epilogues and barriers do:
+//   * NW = 4, TPW = 10 (<= 40 tiles, LDS <= 80 KiB): TWO 4-wave workgroups per CU, each on its own 32-sample
+//     groups -- the two overlap each other's barriers, gathers and VALU phases (round 5; the runner config's
+//     [256, 128, 64] has exactly 40 tiles).  Its dense layers run the plain k-ordered chain (every output tile on one
+//     wave, as deep_forward), so its activations are bit for bit the rollout / policy kernels'.
+//   * NW = 8, TPW = 6 (<= 48 tiles): one 8-wave workgroup per CU (round 4); dense layers with fewer than 8 output
+//     tiles split k in two halves (dense_fwd_split) to keep the idle waves busy.
+//   * NW = 8, TPW = 8 (<= 64 tiles: one-hot / log2 [256, 256] and [256, 256, x] nets, round 5): as above with 128
+//     accumulator registers per wave.
+// (A 4-wave workgroup alone per CU with 12 tiles per wave took the whole register file, one wave per SIMD.)
+constexpr int kDeepGradMaxBlock = 512;
+struct DeepGradVariant {
+    int nw, tpw, ksplit, per_cu;
+};
 
 struct DeepGradArgs {
     DeepNet net;
@@ -712,8 +725,9 @@ __device__ __forceinline__ float act_deriv(float a) {   // from the activation (
     else return a * (1.0f - a);
 }
 
-template <int OBS, int ACT>
-__global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradArgs a) {
+template <int OBS, int ACT, int NW, int TPW, bool KSPLIT>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs a) {
+    constexpr int kBlock = 64 * NW;
     extern __shared__ float dyn[];
     const DeepNet& net = a.net;
     const int L = net.L;
@@ -729,14 +743,17 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
     if (tid < 256)
         for (int l = 0; l < kMaxHidden; l++) dbs[l * 256 + tid] = 0.0f;
     const float* P = a.packed;
-    floatx16 acc[kGradTilesPerWave];
+    floatx16 acc[TPW];
 #pragma unroll
-    for (int k = 0; k < kGradTilesPerWave; k++) acc[k] = floatx16{};
-    floatx16 acc0 = {};   // log2 / raw first layer: dW_0^T tile t = w
+    for (int k = 0; k < TPW; k++) acc[k] = floatx16{};
+    constexpr int kA0 = 8 / NW;   // log2 / raw first layer: dW_0^T tiles t = w + NW i
+    floatx16 acc0[kA0];
+#pragma unroll
+    for (int i = 0; i < kA0; i++) acc0[i] = floatx16{};
     // dW_out / db_{L-1} partials of this thread's (unit, sample range); db_out (threads 0..3: output tid)
     float dwo[4] = {0.f, 0.f, 0.f, 0.f}, dbl = 0.f, dbo = 0.f;
     const int HL = 32 * net.nt[L - 1];
-    const int oq = kDeepGradBlock / HL, oper = (32 + oq - 1) / oq;   // sample ranges of the output layer
+    const int oq = kBlock / HL, oper = (32 + oq - 1) / oq;   // sample ranges of the output layer
     const float4* wout = reinterpret_cast<const float4*>(P + net.w[L]);
     const uint32_t groups = (a.n + 31u) >> 5;
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
@@ -749,25 +766,36 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
             float* out = actl(0);
             const int nt0 = net.nt[0];
             if constexpr (OBS == G2048_OBS_ONEHOT) {
-                // waves w and w + 4: boards 8 (w & 3) .. + 7, 8 lanes per board; tiles 4 (w >> 2) .. + 3
-                const int bb = 8 * (w & 3) + (lane >> 3), k = lane & 7, m0 = 4 * (w >> 2);
+                // wave w: boards 8 (w & 3) .. + 7, 8 lanes per board; tiles 4 (w >> 2) .. + 3 (NW = 8), or all 8
+                // tiles in two passes of 4 (NW = 4, two cells' loads in flight: its registers hold 10 dW tiles) --
+                // each unit's sum is the same 16 adds in cell order either way
+                const int bb = 8 * (w & 3) + (lane >> 3), k = lane & 7;
                 const uint64_t b = bds[bb];
                 const int H = 32 * nt0;
-                const float* tab = P + net.w[0] + 4 * k + 32 * m0;
-                float4 ac[4];
+                const auto pass = [&](int m0) {
+                    const float* tab = P + net.w[0] + 4 * k + 32 * m0;
+                    float4 ac[4];
 #pragma unroll
-                for (int m = 0; m < 4; m++) ac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
-                onehot_gather<4>(tab, b, H, nt0 - m0, ac);
+                    for (int m = 0; m < 4; m++) ac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if constexpr (NW == 4) onehot_gather<4, 2>(tab, b, H, nt0 - m0, ac);
+                    else onehot_gather<4>(tab, b, H, nt0 - m0, ac);
 #pragma unroll
-                for (int m = 0; m < 4; m++) {
-                    if (m0 + m < nt0) {
-                        const int u = 32 * (m0 + m) + 4 * k;
-                        const float4 bv = *reinterpret_cast<const float4*>(P + net.b[0] + u);
-                        out[(u + 0) * kActStride + bb] = activate<ACT>(ac[m].x + bv.x);
-                        out[(u + 1) * kActStride + bb] = activate<ACT>(ac[m].y + bv.y);
-                        out[(u + 2) * kActStride + bb] = activate<ACT>(ac[m].z + bv.z);
-                        out[(u + 3) * kActStride + bb] = activate<ACT>(ac[m].w + bv.w);
+                    for (int m = 0; m < 4; m++) {
+                        if (m0 + m < nt0) {
+                            const int u = 32 * (m0 + m) + 4 * k;
+                            const float4 bv = *reinterpret_cast<const float4*>(P + net.b[0] + u);
+                            out[(u + 0) * kActStride + bb] = activate<ACT>(ac[m].x + bv.x);
+                            out[(u + 1) * kActStride + bb] = activate<ACT>(ac[m].y + bv.y);
+                            out[(u + 2) * kActStride + bb] = activate<ACT>(ac[m].z + bv.z);
+                            out[(u + 3) * kActStride + bb] = activate<ACT>(ac[m].w + bv.w);
+                        }
                     }
+                };
+                if constexpr (NW == 8) {
+                    pass(4 * (w >> 2));
+                } else {
+                    pass(0);
+                    if (nt0 > 4) pass(4);
                 }
             } else {
                 const uint64_t b = bds[col];
@@ -775,7 +803,7 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
 #pragma unroll
                 for (int s2 = 0; s2 < 8; s2++) x[s2] = obs_value<OBS>(b, 2 * s2 + h, a.obs_scale);
                 const float* w1f = P + net.w[0];
-                for (int t = w; t < nt0; t += kDeepGradWaves) {
+                for (int t = w; t < nt0; t += NW) {
                     floatx16 c = {};
 #pragma unroll
                     for (int s2 = 0; s2 < 8; s2++)
@@ -796,7 +824,19 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
             float* out = actl(l);
             const int ntin = net.nt[l - 1], ntout = net.nt[l];
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(P + net.w[l]) + lane;
-            dense_fwd_split<ACT, kDeepGradWaves>(in, out, frag, P + net.b[l], ntin, ntout, w);
+            if constexpr (KSPLIT) {
+                dense_fwd_split<ACT, NW>(in, out, frag, P + net.b[l], ntin, ntout, w);
+            } else {   // deep_forward's chain: the rollout / policy kernels' bits
+                for (int o = w; o < ntout; o += NW) {
+                    const floatx16 c = frag_chain(frag + (int64_t)o * ntin * 256, in, 0, ntin, h, col);
+                    const float* bb = P + net.b[l] + 32 * o;
+                    float bv[16];
+#pragma unroll
+                    for (int r = 0; r < 16; r++) bv[r] = bb[tile_row(r, h)];
+#pragma unroll
+                    for (int r = 0; r < 16; r++) out[(32 * o + tile_row(r, h)) * kActStride + col] = activate<ACT>(c[r] + bv[r]);
+                }
+            }
             __syncthreads();
         }
         // ---- output layer partials (as deep_forward; threads 0..255)
@@ -897,8 +937,8 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
             const int ntin = net.nt[l - 1], ntout = net.nt[l];
             const int f0 = a.tile_begin[l], f1 = f0 + ntin * ntout;
 #pragma unroll
-            for (int k = 0; k < kGradTilesPerWave; k++) {
-                const int f = w + kDeepGradWaves * k;
+            for (int k = 0; k < TPW; k++) {
+                const int f = w + NW * k;
                 if (f >= f0 && f < f1) {                     // wave-uniform
                     const int ti = (f - f0) / ntout, tj = (f - f0) % ntout;
                     const float* ap = A + (32 * ti + col) * kActStride + h;
@@ -914,7 +954,7 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
             // delta_{l-1} = (W_l delta_l) act'(a_{l-1}): output tiles = layer l-1's units, k = layer l's units
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(a.bpacked + a.boff[l]) + lane;
             float* Aw = actl(l - 1);
-            for (int o = w; o < ntin; o += kDeepGradWaves) {
+            for (int o = w; o < ntin; o += NW) {
                 const floatx16 c = frag_chain(frag + (int64_t)o * ntout * 256, D, 0, ntout, h, col);
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
@@ -937,24 +977,31 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
             const int H0 = 32 * net.nt[0];
             if (tid < H0) {
                 const float* drow = actl(0) + tid * kActStride;
-                for (int n2 = 0; n2 < 32; n2++) {
-                    const uint32_t jj = gi * 32u + (uint32_t)n2;
-                    if (jj < a.n) a.d0_out[(size_t)jj * H0 + tid] = drow[n2];
+                float* dst = a.d0_out + (size_t)gi * 32u * H0 + tid;
+                const uint32_t left = a.n - gi * 32u;
+                if (left >= 32u) {   // a whole group: 32 stores without a per-store branch
+#pragma unroll
+                    for (int n2 = 0; n2 < 32; n2++) dst[(size_t)n2 * H0] = drow[n2];
+                } else {
+                    for (uint32_t n2 = 0; n2 < left; n2++) dst[(size_t)n2 * H0] = drow[n2];
                 }
             }
         } else {
             // dW_0^T tile t (32 units x 32 features, features >= 16 zero): A = delta_0 [unit][sample], B = x [sample][feature]
             const float* D0 = actl(0);
-            const int t = w;
-            if (t < net.nt[0]) {
-                floatx16 c = acc0;
-                const float* dp = D0 + (32 * t + col) * kActStride + h;
 #pragma unroll
-                for (int s2 = 0; s2 < 16; s2++) {
-                    const float xv = col < 16 ? obs_value<OBS>(bds[2 * s2 + h], col, a.obs_scale) : 0.0f;
-                    c = __builtin_amdgcn_mfma_f32_32x32x2f32(dp[2 * s2], xv, c, 0, 0, 0);
+            for (int i = 0; i < kA0; i++) {
+                const int t = w + NW * i;
+                if (t < net.nt[0]) {
+                    floatx16 c = acc0[i];
+                    const float* dp = D0 + (32 * t + col) * kActStride + h;
+#pragma unroll
+                    for (int s2 = 0; s2 < 16; s2++) {
+                        const float xv = col < 16 ? obs_value<OBS>(bds[2 * s2 + h], col, a.obs_scale) : 0.0f;
+                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(dp[2 * s2], xv, c, 0, 0, 0);
+                    }
+                    acc0[i] = c;
                 }
-                acc0 = c;
             }
         }
         __syncthreads();   // the next group rewrites the boards and layer 0
@@ -982,8 +1029,8 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
     }
     float* out = a.part + (size_t)blockIdx.x * a.pslab;
 #pragma unroll
-    for (int k = 0; k < kGradTilesPerWave; k++) {
-        const int f = w + kDeepGradWaves * k;
+    for (int k = 0; k < TPW; k++) {
+        const int f = w + NW * k;
         if (f < a.ntiles) {
             int l = 1;
             while (l + 1 < L && f >= a.tile_begin[l + 1]) l++;
@@ -997,10 +1044,13 @@ __global__ void __launch_bounds__(kDeepGradBlock, 1) deep_grad_kernel(DeepGradAr
     }
     if constexpr (OBS != G2048_OBS_ONEHOT) {
         const int H0 = 32 * net.nt[0];
-        const int t = w;
-        if (t < net.nt[0] && col < 16) {                   // C[unit][feature]: dW_0[feature][unit]
 #pragma unroll
-            for (int r = 0; r < 16; r++) out[a.pw[0] + (int64_t)col * H0 + 32 * t + tile_row(r, h)] = acc0[r];
+        for (int i = 0; i < kA0; i++) {
+            const int t = w + NW * i;
+            if (t < net.nt[0] && col < 16) {               // C[unit][feature]: dW_0[feature][unit]
+#pragma unroll
+                for (int r = 0; r < 16; r++) out[a.pw[0] + (int64_t)col * H0 + 32 * t + tile_row(r, h)] = acc0[i][r];
+            }
         }
     }
     for (int l = 0; l < L; l++)
@@ -1076,14 +1126,25 @@ DeepGradLayout deep_grad_layout(const DeepNet& n) {
 }
 
 // floats of the output layer's final reduction (deep_grad_kernel: [oq][HL][5], oq HL <= the block size)
-constexpr int kOutRed = 5 * kDeepGradBlock;
-int64_t deep_grad_act_floats(const DeepNet& n) {
+int64_t deep_grad_act_floats(const DeepNet& n, int nw) {
     int64_t units = 0;
     for (int l = 0; l < n.L; l++) units += 32 * n.nt[l];
-    return units * kActStride > kOutRed ? units * kActStride : kOutRed;
+    const int64_t red = 5 * 64 * nw;
+    return units * kActStride > red ? units * kActStride : red;
 }
-int64_t deep_grad_lds_bytes(const DeepNet& n) {
-    return (deep_grad_act_floats(n) + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256) * 4;
+int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {
+    return (deep_grad_act_floats(n, nw) + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256) * 4;
+}
+
+// the instantiation that covers the net (nw = 0: none; see deep_grad_kernel).  The 4-wave and the 64-tile ones are
+// one-hot only: with the log2 / raw first layer's MFMA tiles (dW_0 accumulators, the obs rebuilt per k-step) on top
+// of 10 or 8 dense tiles per wave, hipcc spills whole accumulator tiles (~300-650 VGPRs).
+DeepGradVariant deep_grad_variant(const DeepNet& n) {
+    const int tiles = deep_grad_layout(n).ntiles;
+    if (n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024) return {4, 10, 0, 2};
+    if (tiles <= 48 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 6, 1, 1};
+    if (n.onehot && tiles <= 64 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 8, 1, 1};
+    return {0, 0, 0, 0};
 }
 
 // ------------------------------------------------------------------------------------ one-hot layer 1 (update)
@@ -1174,6 +1235,134 @@ __global__ void __launch_bounds__(64 * kDw1Waves) onehot_dw1_kernel(const uint64
 #pragma unroll
         for (int q = 0; q < 4; q++) slab[(r0 + 17 * q + 16) * h1 + j] = 0.0f;
         if (w == 0) slab[(int64_t)kOneHotRows * h1 + j] = db;
+    }
+}
+
+// dW1 / db1 of a one-hot first layer on the bf16 MFMA (round 5; replaces onehot_dw1_kernel's register scatter on
+// the update path).  dW1 = X^T D1 with X the [samples][272] one-hot of the boards is a GEMM whose A operand is exact
+// in bf16 (0 / 1): v_mfma_f32_32x32x16_bf16 with A = X^T of two cells (row 16 q + e: cell 2 p + q, exponent e; k = 16
+// samples) and B = the samples' deltas split exactly into three bf16 planes (d = d0 + d1 + d2, 8 significant bits
+// each), so every product is exact and only the fp32 accumulation rounds, as the sequential sum does.  Wave w owns
+// the 32 units 32 w .. 32 w + 31 (one column tile) x all 16 cells (8 cell pairs): 8 accumulator tiles = 128
+// registers, two waves per SIMD (16 tiles = 256 AGPRs per wave made hipcc spill ~250 VGPRs), one 8-wave workgroup
+// per CU and sample range (always 8 waves: the units past h1 compute zeros and store nothing).  Per 16 samples: 24 MFMAs per wave (8 pairs x 3 planes), 1,536 cycles per SIMD for 256 units,
+// against 16 KiB of deltas read per workgroup.  The one-hot A fragments (the same for every wave) are built once per
+// workgroup: wave w builds pair w (from byte w of each board) into a double-buffered LDS image that every wave
+// reads back (one ds_read_b128 per pair, one pair ahead of its MFMAs).  db1 is each lane's sum of its B values (samples 8 h .. 8 h + 7 of each step, in order), the
+// two lane halves added at the end.  Deltas and boards are loaded two steps ahead (a three-slot register ring).
+// Rows 17 c + 16 (exponent 16, never on a bitboard) are written as zeros.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kDw1Step = 16;        // samples per MFMA k-step
+constexpr int kDw1MaxWaves = 8;     // 32 units per wave
+
+__device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {   // round to nearest even at each step: x = p0 + p1 + p2 exactly
+        const __bf16 hh = (__bf16)v[j];
+        const float rr = v[j] - (float)hh;
+        const __bf16 mm = (__bf16)rr;
+        p0[j] = hh;
+        p1[j] = mm;
+        p2[j] = (__bf16)(rr - (float)mm);
+    }
+}
+
+struct Dw1Slot {
+    float v[8];       // deltas of this lane's unit, samples 8 h .. 8 h + 7 of the step
+    uint32_t bw[8];   // byte w of the same samples' boards: cells 2 w, 2 w + 1 (this wave's cell pair)
+};
+
+__global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_mfma_kernel(
+    const uint64_t* __restrict__ boards, const float* __restrict__ d1, int h1, int64_t m, int64_t ld, int64_t per,
+    float* __restrict__ part) {
+    __shared__ uint4 abuf[2][8][64];   // [buffer][cell pair][lane]: the A fragment (8 bf16) of `lane`
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t s0 = (int64_t)blockIdx.x * per, s1 = s0 + per < m ? s0 + per : m;
+    const int u = 32 * w + r;
+    const uint8_t* bbytes = reinterpret_cast<const uint8_t*>(boards) + w;
+    const bool live = u < h1;
+    const int64_t uc = live ? u : h1 - 1;
+    const uint32_t q = (uint32_t)r >> 4, e = (uint32_t)r & 15u;
+    floatx16 acc[8];
+#pragma unroll
+    for (int p = 0; p < 8; p++) acc[p] = floatx16{};
+    float db = 0.0f;
+    const auto load = [&](int64_t c0, Dw1Slot& sl) {   // unconditional loads (clamped rows), zeros past s1
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int64_t s = c0 + 8 * h + k, sc = s < s1 ? s : s1 - 1;
+            sl.v[k] = d1[sc * ld + uc];
+            sl.bw[k] = bbytes[8 * sc];
+        }
+    };
+    const auto build_a = [&](const Dw1Slot& sl, int buf) {   // this wave's cell pair of the step's one-hot
+        uint32_t d[4];
+#pragma unroll
+        for (int k2 = 0; k2 < 4; k2++) {
+            const uint32_t x0 = (sl.bw[2 * k2] >> (4u * q)) & 15u, x1 = (sl.bw[2 * k2 + 1] >> (4u * q)) & 15u;
+            d[k2] = (x0 == e ? 0x3F80u : 0u) | (x1 == e ? 0x3F800000u : 0u);   // bf16 1.0 / 0 per sample
+        }
+        abuf[buf][w][lane] = make_uint4(d[0], d[1], d[2], d[3]);
+    };
+    // one step: the MFMAs of `cur` (its A image in `buf`) while the loads of two steps ahead are in flight and the
+    // next step's A image is built
+    const auto step = [&](Dw1Slot& cur, Dw1Slot& nxt, Dw1Slot& ahead, int64_t c0, int buf) {
+        const int64_t c1 = c0 + kDw1Step, c2 = c0 + 2 * kDw1Step;
+        if (c2 < s1) load(c2, ahead);
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            v[k] = (live && c0 + 8 * h + k < s1) ? cur.v[k] : 0.0f;
+            db += v[k];
+        }
+        bf16x8 pl[3];
+        split3_bf16(v, pl[0], pl[1], pl[2]);
+        if (c1 < s1) build_a(nxt, buf ^ 1);
+        uint4 a = abuf[buf][0][lane];
+#pragma unroll
+        for (int p = 0; p < 8; p++) {
+            const bf16x8 av = __builtin_bit_cast(bf16x8, a);
+            if (p < 7) a = abuf[buf][p + 1][lane];
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, pl[0], acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, pl[1], acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, pl[2], acc[p], 0, 0, 0);
+        }
+        __syncthreads();   // the next step's A image is complete; this one is free to be rewritten
+    };
+    Dw1Slot sl0, sl1, sl2;
+    if (s0 < s1) {
+        load(s0, sl0);
+        if (s0 + kDw1Step < s1) load(s0 + kDw1Step, sl1);
+        build_a(sl0, 0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int64_t c0 = s0; c0 < s1; c0 += 3 * kDw1Step) {   // block-uniform trip count; the slots rotate by 3
+        step(sl0, sl1, sl2, c0, buf);
+        buf ^= 1;
+        if (c0 + kDw1Step >= s1) break;
+        step(sl1, sl2, sl0, c0 + kDw1Step, buf);
+        buf ^= 1;
+        if (c0 + 2 * kDw1Step >= s1) break;
+        step(sl2, sl0, sl1, c0 + 2 * kDw1Step, buf);
+        buf ^= 1;
+    }
+    db += __shfl_xor(db, 32);   // lane half 0 + half 1 (addition commutes: both halves hold the same bits)
+    if (!live) return;
+    float* slab = part + (int64_t)blockIdx.x * kDw1Rows * h1;
+#pragma unroll
+    for (int p = 0; p < 8; p++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int row = tile_row(i, h);                       // 16 q' + e' of the pair
+            slab[(int64_t)(17 * (2 * p + (row >> 4)) + (row & 15)) * h1 + u] = acc[p][i];
+        }
+    }
+    if (h == 0) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) slab[(int64_t)(17 * c + 16) * h1 + u] = 0.0f;   // exponent 16: never on a bitboard
+        slab[(int64_t)kOneHotRows * h1 + u] = db;
     }
 }
 
@@ -1376,12 +1565,20 @@ int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, 
         return dfail(G2048_EINVAL, "Unsupported activation");
     if (!packed || (n > 0 && (!boards || !out))) return dfail(G2048_EINVAL, "deep hidden: NULL buffer");
     if (n == 0) return G2048_OK;
+    const bool ksplit = deep_grad_variant(net).ksplit != 0;   // the full net's gradient instantiation
     net.L = layer + 1;   // truncated: deep_forward stops after `layer` (offsets of the kept layers unchanged)
     const int64_t groups = (n + 31) / 32, cap = 2 * (int64_t)device_cus();
     const int grid = (int)(groups < cap ? groups : cap);
     hipStream_t s = (hipStream_t)stream;
-#define G2048_HIDDEN(O, A) hipLaunchKernelGGL((deep_hidden_kernel<O, A>), dim3(grid), dim3(kDeepBlock), 0, s, net, packed, \
-                                             boards, (uint32_t)n, obs_scale, out, (uint32_t)ld)
+#define G2048_HIDDEN(O, A)                                                                                          \
+    do {                                                                                                            \
+        if (ksplit)                                                                                                 \
+            hipLaunchKernelGGL((deep_hidden_kernel<O, A, true>), dim3(grid), dim3(kDeepBlock), 0, s, net, packed,   \
+                               boards, (uint32_t)n, obs_scale, out, (uint32_t)ld);                                  \
+        else                                                                                                        \
+            hipLaunchKernelGGL((deep_hidden_kernel<O, A, false>), dim3(grid), dim3(kDeepBlock), 0, s, net, packed,  \
+                               boards, (uint32_t)n, obs_scale, out, (uint32_t)ld);                                  \
+    } while (0)
     if (obs_mode == G2048_OBS_ONEHOT) {
         if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_ONEHOT, 0); else G2048_HIDDEN(G2048_OBS_ONEHOT, 1);
     } else if (obs_mode == G2048_OBS_LOG2) {
@@ -1404,9 +1601,15 @@ int64_t g2048_deep_grad_slab(int obs_mode, int n_hidden, const int32_t* hidden) 
     DeepNet n;
     if (obs_mode != G2048_OBS_LOG2 && obs_mode != G2048_OBS_RAW && obs_mode != G2048_OBS_ONEHOT) return -1;
     if (!deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, n)) return -1;
-    const DeepGradLayout g = deep_grad_layout(n);
-    if (g.ntiles > kDeepGradWaves * kGradTilesPerWave || deep_grad_lds_bytes(n) > 160 * 1024) return -1;   // not covered
-    return g.pslab;
+    if (deep_grad_variant(n).nw == 0) return -1;   // not covered
+    return deep_grad_layout(n).pslab;
+}
+
+int g2048_deep_grad_parts(int obs_mode, int n_hidden, const int32_t* hidden) {
+    DeepNet n;
+    if (g2048_deep_grad_slab(obs_mode, n_hidden, hidden) < 0) return -1;
+    deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, n);
+    return deep_grad_variant(n).per_cu * device_cus();
 }
 
 int g2048_deep_grad_pack(const float* const* W, int obs_mode, int n_hidden, const int32_t* hidden, float* packed,
@@ -1437,17 +1640,31 @@ int g2048_deep_grad_pack(const float* const* W, int obs_mode, int n_hidden, cons
 }  // extern "C"
 
 namespace {
-template <int OBS, int ACT>
-int launch_deep_grad(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t s) {
-    static bool attr_set = false;   // per instantiation (the attribute is per kernel; setting it twice is harmless)
-    if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&deep_grad_kernel<OBS, ACT>),
+template <int OBS, int ACT, int NW, int TPW, bool KSPLIT>
+int launch_deep_grad_v(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t s) {
+    // the dynamic-LDS attribute is per kernel and device: one bit per device id, set on the first launch there
+    // (two threads racing both set it, which is harmless)
+    static std::atomic<uint64_t> attr_set{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return dfail(G2048_EHIP, "deep gradient: hipGetDevice failed");
+    const uint64_t bit = 1ull << (dev & 63);
+    if (!(attr_set.load(std::memory_order_acquire) & bit)) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&deep_grad_kernel<OBS, ACT, NW, TPW, KSPLIT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return dfail(G2048_EHIP, "deep gradient: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-        attr_set = true;
+        attr_set.fetch_or(bit, std::memory_order_acq_rel);
     }
-    hipLaunchKernelGGL((deep_grad_kernel<OBS, ACT>), dim3(grid), dim3(kDeepGradBlock), (unsigned)lds, s, a);
+    hipLaunchKernelGGL((deep_grad_kernel<OBS, ACT, NW, TPW, KSPLIT>), dim3(grid), dim3(64 * NW), (unsigned)lds, s, a);
     return check_hip();
+}
+
+template <int OBS, int ACT>
+int launch_deep_grad(const DeepGradArgs& a, const DeepGradVariant& v, int grid, int64_t lds, hipStream_t s) {
+    if constexpr (OBS == G2048_OBS_ONEHOT) {
+        if (v.nw == 4) return launch_deep_grad_v<OBS, ACT, 4, 10, false>(a, grid, lds, s);
+        if (v.tpw == 8) return launch_deep_grad_v<OBS, ACT, 8, 8, true>(a, grid, lds, s);
+    }
+    return launch_deep_grad_v<OBS, ACT, 8, 6, true>(a, grid, lds, s);
 }
 }  // namespace
 
@@ -1463,7 +1680,7 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
         return dfail(G2048_EINVAL, "Unsupported activation");
     if (g2048_deep_grad_slab(obs_mode, n_hidden, hidden) < 0)
         return dfail(G2048_EINVAL, "deep gradient: net not covered (obs mode, 1..4 layers of 1..256 units, at most "
-                                   "48 dense 32x32 weight-gradient tiles)");
+                                   "64 dense 32x32 weight-gradient tiles)");
     if (critic && loss != 0 && loss != 1) return dfail(G2048_EINVAL, "Unknown critic loss type");
     if (!packed || !partials || (n > 0 && (!boards || !coef)) || (n > 0 && !critic && !actions) ||
         (n > 0 && critic && !target) || (n > 0 && obs_mode == G2048_OBS_ONEHOT && !d0_out))
@@ -1484,7 +1701,8 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
         a.aoff[l] = off;
         off += 32 * net.nt[l] * kActStride;
     }
-    a.lds_tail = (int)deep_grad_act_floats(net);   // >= off: room for the output layer's reduction
+    const DeepGradVariant v = deep_grad_variant(net);
+    a.lds_tail = (int)deep_grad_act_floats(net, v.nw);   // >= off: room for the output layer's reduction
     for (int l = 0; l <= net.L; l++) {
         a.pw[l] = g.pw[l];
         a.pb[l] = g.pb[l];
@@ -1505,17 +1723,17 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
     a.obs_scale = obs_scale;
     a.n = (uint32_t)n;
     a.use_mask = use_mask;
-    const int64_t lds = deep_grad_lds_bytes(net);
+    const int64_t lds = deep_grad_lds_bytes(net, v.nw);
     hipStream_t s = (hipStream_t)stream;
     const int grid = (int)nparts;   // every workgroup writes its slab (zeros when it gets no group)
     if (obs_mode == G2048_OBS_ONEHOT)
-        return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_ONEHOT, 0>(a, grid, lds, s)
-                                            : launch_deep_grad<G2048_OBS_ONEHOT, 1>(a, grid, lds, s);
+        return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_ONEHOT, 0>(a, v, grid, lds, s)
+                                            : launch_deep_grad<G2048_OBS_ONEHOT, 1>(a, v, grid, lds, s);
     if (obs_mode == G2048_OBS_LOG2)
-        return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_LOG2, 0>(a, grid, lds, s)
-                                            : launch_deep_grad<G2048_OBS_LOG2, 1>(a, grid, lds, s);
-    return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_RAW, 0>(a, grid, lds, s)
-                                        : launch_deep_grad<G2048_OBS_RAW, 1>(a, grid, lds, s);
+        return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_LOG2, 0>(a, v, grid, lds, s)
+                                            : launch_deep_grad<G2048_OBS_LOG2, 1>(a, v, grid, lds, s);
+    return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_RAW, 0>(a, v, grid, lds, s)
+                                        : launch_deep_grad<G2048_OBS_RAW, 1>(a, v, grid, lds, s);
 }
 
 int g2048_onehot_layer1(const float* W1, const float* b1, int h1, int activation, const uint64_t* boards, int64_t m,
@@ -1543,8 +1761,13 @@ int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m,
     if (nparts != (m + per - 1) / per || nparts > 65535) return dfail(G2048_EINVAL, "one-hot dW1: nparts != ceil(m / per)");
     if (m > 0 && (!boards || !d1 || !partials)) return dfail(G2048_EINVAL, "one-hot dW1: NULL buffer");
     if (m == 0) return G2048_OK;
+#if G2048_DW1_SCATTER   // A/B build only: round 4's register scatter
     hipLaunchKernelGGL(onehot_dw1_kernel, dim3((h1 + 63) / 64, (unsigned)nparts), dim3(64 * kDw1Waves), 0, (hipStream_t)stream,
                        boards, d1, h1, m, ld, per, partials);
+#else
+    hipLaunchKernelGGL(onehot_dw1_mfma_kernel, dim3((unsigned)nparts), dim3(64 * kDw1MaxWaves), 0, (hipStream_t)stream,
+                       boards, d1, h1, m, ld, per, partials);
+#endif
     return check_hip();
 }
 

@@ -32,7 +32,7 @@ def test_header_declares_expected_api():
         "g2048_policy_pack", "g2048_policy", "g2048_rollout", "g2048_grad_packed_size", "g2048_grad_partial_size",
         "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2",
         "g2048_fold_partials", "g2048_dw2_factored", "g2048_dw2_actor", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
-        "g2048_deep_rollout", "g2048_deep_hidden", "g2048_deep_grad_pack_size", "g2048_deep_grad_slab",
+        "g2048_deep_rollout", "g2048_deep_hidden", "g2048_deep_grad_pack_size", "g2048_deep_grad_slab", "g2048_deep_grad_parts",
         "g2048_deep_grad_pack", "g2048_deep_grad", "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1"])
 
 
@@ -142,7 +142,7 @@ def test_argument_validation_without_gpu(L):
 def test_deep_sizes_and_validation_without_gpu(L):
     """The any-depth / one-hot entry points (g2048_deep.hip): packed sizes and slab layouts agree with the host's
     own layout (agent._deep_slab_layout), the coverage limits (<= 4 hidden layers of <= 256 units; the fused
-    gradient: <= 48 dense 32x32 weight-gradient tiles) and the argument checks, all before any launch."""
+    gradient: <= 64 dense 32x32 weight-gradient tiles on one-hot obs, <= 48 on log2 / raw) and the argument checks, all before any launch."""
     import ctypes
 
     from rl2048_amd.agent import ReinforceAgent, _round32
@@ -164,14 +164,23 @@ def test_deep_sizes_and_validation_without_gpu(L):
         assert lib.g2048_deep_packed_size(obs, len(hs), arr(hs)) == -1, (obs, hs)
     # the fused gradient's partial slab == the layout the host folds it with; nets past its tile budget -> -1
     for obs, hs in ((L.OBS_ONEHOT, [256, 128, 64]), (L.OBS_LOG2, [64, 48, 32]), (L.OBS_RAW, [40, 33, 20, 10]),
-                    (L.OBS_LOG2, [128, 128, 128])):
+                    (L.OBS_LOG2, [128, 128, 128]), (L.OBS_ONEHOT, [256, 256]), (L.OBS_ONEHOT, [200, 250])):
         pw, pb = ReinforceAgent._deep_slab_layout(hs, obs == L.OBS_ONEHOT)
         assert lib.g2048_deep_grad_slab(obs, len(hs), arr(hs)) == pb[-1] + 4, (obs, hs)
         t = [_round32(h) // 32 for h in hs]
         nb = sum(t[l] * t[l - 1] * 1024 for l in range(1, len(hs)))
         assert lib.g2048_deep_grad_pack_size(obs, len(hs), arr(hs)) == max(nb, 1)
-    for obs, hs in ((L.OBS_ONEHOT, [256, 256, 256]), (L.OBS_LOG2, [256, 256]), (L.OBS_LOG2, [32] * 5)):
+    # past 64 tiles; log2 / raw nets past 48 tiles (their 64-tile instantiation would spill, see g2048_deep.hip --
+    # log2 [256, 256] is the two-layer fused kernels' net anyway)
+    for obs, hs in ((L.OBS_ONEHOT, [256, 256, 256]), (L.OBS_ONEHOT, [256, 256, 32]), (L.OBS_LOG2, [256, 256]),
+                    (L.OBS_LOG2, [32] * 5)):
         assert lib.g2048_deep_grad_slab(obs, len(hs), arr(hs)) == -1, (obs, hs)
+        assert lib.g2048_deep_grad_parts(obs, len(hs), arr(hs)) == -1, (obs, hs)
+    # workgroups that fill the chip: two 4-wave workgroups per CU for one-hot nets of <= 40 tiles, else one
+    cus = lib.g2048_deep_grad_parts(L.OBS_LOG2, 3, arr([64, 48, 32]))
+    assert cus > 0
+    assert lib.g2048_deep_grad_parts(L.OBS_ONEHOT, 3, arr([256, 128, 64])) == 2 * cus
+    assert lib.g2048_deep_grad_parts(L.OBS_ONEHOT, 2, arr([256, 256])) == cus
     assert lib.g2048_onehot_dw1_slab(256) == 273 * 256 and lib.g2048_onehot_dw1_slab(0) == -1
     assert lib.g2048_onehot_dw1_slab(257) == -1
     p = ctypes.c_void_p(8)
