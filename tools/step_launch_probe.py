@@ -10,6 +10,10 @@ Interleaved, on one env of the bench's shape (1,048,576 boards, PCG64, log2 obs,
   resetS / sparseS -- as freshS from env.reset's two-tile boards / from synthetic boards with cells 1-3 of
               each row cleared
 G2048_LIB=<path> loads an A/B build.    zfreshS / mfreshS -- as freshS with obs_log2_scale 0 (zero obs values) / max_tile_seen starting at 2^12
+  reloadS  -- (round 5: buffer age vs board state) the long-running env (hundreds of launches on its buffers) given
+              the synthetic random-state boards and lane state again, S untimed steps, then the timed K
+  evolvedS -- a new env (freshly initialised buffers) given the long-running env's evolved boards and lane state,
+              S untimed steps, then the timed K
 Also the host cost of one step_into call.  Prints one JSON line per repetition.
 """
 import argparse
@@ -68,7 +72,20 @@ def main():
     torch.cuda.synchronize()
 
     def timed(mode):
-        if mode[0] in "frsmz":
+        if mode.startswith("reload") or mode.startswith("evolved"):
+            skip = int(mode.lstrip("reloadevolved") or 5)
+            if mode.startswith("reload"):
+                fenv = env
+                fenv.board.copy_(bench.synthetic_boards(torch, B, 0, dev))
+                fenv.set_lane_state(step_count=0, max_tile_exp=2, active=True)
+            else:
+                fenv = bench.make_env(torch, args, B, 0, dev)
+                fenv.board.copy_(env.board)
+                fenv.state.copy_(env.state)
+            for k in range(skip):
+                fenv.step_into(actions[k % K])
+            torch.cuda.synchronize()
+        elif mode[0] in "frsmz":
             skip = int(mode.lstrip("freshsparetmz") or 5)
             fenv = bench.make_env(torch, args, B, 0, dev)
             if mode.startswith("zfresh"):      # obs values all 0.0 (same stores)
@@ -92,7 +109,7 @@ def main():
         e0.record()
         if mode == "graph":
             gr.replay()
-        elif mode[0] in "frsmz":
+        elif mode[0] in "frsmze":
             for k in range(K):
                 fenv.step_into(actions[k])
         else:
