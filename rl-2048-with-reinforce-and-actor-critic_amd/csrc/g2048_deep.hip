@@ -33,6 +33,36 @@ using namespace g2048;
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// two floats rounded to nearest even into one dword of bf16 (a in the low half): one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+// exact split of 8 floats into three bf16 planes (x = p0 + p1 + p2; each residual is exact in fp32), packed two
+// values per dword: 11 VALU per pair
+__device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 h, m, l;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const float x0 = v[2 * j], x1 = v[2 * j + 1];
+        const uint32_t hh = pk_bf16(x0, x1);
+        const float r0 = x0 - __uint_as_float(hh << 16), r1 = x1 - __uint_as_float(hh & 0xFFFF0000u);
+        const uint32_t mm = pk_bf16(r0, r1);
+        const float t0 = r0 - __uint_as_float(mm << 16), t1 = r1 - __uint_as_float(mm & 0xFFFF0000u);
+        h[j] = hh;
+        m[j] = mm;
+        l[j] = pk_bf16(t0, t1);
+    }
+    p0 = __builtin_bit_cast(bf16x8, h);
+    p1 = __builtin_bit_cast(bf16x8, m);
+    p2 = __builtin_bit_cast(bf16x8, l);
+}
+
 
 constexpr int kMaxHidden = G2048_DEEP_MAX_HIDDEN;   // hidden layers
 constexpr int kDeepBlock = 256;                      // 4 waves; two workgroups per CU
@@ -154,15 +184,50 @@ struct DeepSmem {
 };
 
 // The k-ordered MFMA chain of one output tile over k-tiles [t0, t1): A = the tile's weight fragments `fo` (4 float4
-// per lane per k-tile, streamed from L2), B = the activation rows `in` (LDS).  Two fragment register sets alternate
-// (no copy between them), and a scheduling barrier after each prefetch keeps the next k-tile's loads issued ahead of
-// this k-tile's 16 MFMAs -- without it hipcc sank every fragment load next to its MFMA and waited for it there (four
-// L2 round trips per k-tile).  Same MFMAs in the same order as a plain loop.
+// per lane per k-tile, streamed from L2), B = the activation rows `in` (LDS).  Two fragment register sets, fa for
+// the even and fb for the odd k-tiles, refilled as a sliding window: as soon as fragment q of k-tile t has fed its 4
+// MFMAs, its register is reloaded with fragment q of k-tile t + 2 (a scheduling barrier keeps the load there), so
+// every fragment load is issued two k-tiles (~2,000 cycles) before its use -- L2 latency under the gradient kernel's
+// load exceeded the one k-tile of round 4's double buffer.  Past the end the window reloads the last k-tile
+// (harmless, an L1 hit).  (Without a barrier hipcc sank every fragment load next to its MFMA and waited for it there:
+// four L2 round trips per k-tile.)  Same MFMAs in the same order as a plain loop.
+#ifndef G2048_DEEP_CHAIN_WINDOW
+#define G2048_DEEP_CHAIN_WINDOW 1
+#endif
 __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, const float* in, int t0, int t1, int h,
                                                int col) {
     floatx16 c = {};
     if (t0 >= t1) return c;
     float4 fa[4], fb[4];
+#if G2048_DEEP_CHAIN_WINDOW
+    const auto seg = [&](float4& f, int t, int q, int tn) {
+        const float* ib = in + (32 * t + h) * kActStride + col + 8 * q * kActStride;
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, ib[0 * kActStride], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, ib[2 * kActStride], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, ib[4 * kActStride], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, ib[6 * kActStride], c, 0, 0, 0);
+        f = fo[tn * 256 + q * 64];
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    const int last = t1 - 1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) fa[q] = fo[t0 * 256 + q * 64];
+#pragma unroll
+    for (int q = 0; q < 4; q++) fb[q] = fo[(t0 + 1 < t1 ? t0 + 1 : last) * 256 + q * 64];
+    __builtin_amdgcn_sched_barrier(0);
+    int t = t0;
+    for (; t + 1 < t1; t += 2) {
+        const int ta = t + 2 < t1 ? t + 2 : last, tb = t + 3 < t1 ? t + 3 : last;
+#pragma unroll
+        for (int q = 0; q < 4; q++) seg(fa[q], t, q, ta);
+#pragma unroll
+        for (int q = 0; q < 4; q++) seg(fb[q], t + 1, q, tb);
+    }
+    if (t < t1) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) seg(fa[q], t, q, last);
+    }
+#else   // round 4's double buffer (A/B builds)
     const auto tile = [&](const float4 (&f)[4], int t) {
         const float* ib = in + (32 * t + h) * kActStride + col;
 #pragma unroll
@@ -188,6 +253,7 @@ __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, co
         tile(fb, t + 1);
     }
     if (t < t1) tile(fa, t);
+#endif
     return c;
 }
 
@@ -292,15 +358,108 @@ __device__ __forceinline__ void onehot_gather(const float* tab, uint64_t b, int 
     }
 }
 
-// KSPLIT: the dense layers by dense_fwd_split (the gradient kernel's forward, for the pattern probe).
-template <int OBS, int ACT, bool KSPLIT = false>
-__device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, DeepSmem& S, float obs_scale) {
+// One-hot first layer on the bf16 MFMA for the update (round 5): a0[u][s] = act(sum_c W1[17 c + e_c(s)][u] + b1[u])
+// per 32-sample group, written as a group block [unit][left] (left = the group's valid samples, 32 but for the last
+// group) -- the layout g2048_deep_grad reads back into its LDS activations (in the d0_out buffer, whose rows the
+// same workgroup later overwrites with the group's layer-0 deltas).  x W1 of a one-hot x is a GEMM whose B operand
+// (one-hot: cell c's 16 exponents as one k-step of v_mfma_f32_32x32x16_bf16, k = 8 h .. 8 h + 7 per lane half) is
+// exact in bf16; W1 is split exactly into three bf16 planes (w = hi + mid + lo), so every product is exact: each
+// MFMA adds exactly one nonzero term per output (the cell's exponent), hi terms into one accumulator and mid + lo
+// into another (their sum as accurate as the gather's 16-term fp32 sum).  Wave w owns unit tile w and keeps its
+// 16 cells x 3 planes of W1 fragments in registers for the whole launch (192 VGPRs), so the weights are read once
+// per launch instead of 16 KiB of W1 rows per board from L2 (the gather the gradient kernel ran: latency-bound,
+// 24 % of its time).  48 MFMAs per wave per group; the 1 KiB per sample it writes is the bound.
+constexpr int kL0Waves = 8;
+template <int ACT>
+__global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNet net, const float* __restrict__ P,
+                                                                          const uint64_t* __restrict__ boards,
+                                                                          uint32_t n, float* __restrict__ out) {
+    __shared__ float bias[256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, col = lane & 31;
+    const int nt0 = net.nt[0], H = 32 * nt0;
+    for (int u = threadIdx.x; u < H; u += blockDim.x) bias[u] = P[net.b[0] + u];
+    __syncthreads();
+    if (w >= nt0) return;   // wave-uniform; no barrier below
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    bf16x8 wp[16][3];
+    {
+        const float* tab = P + net.w[0] + 32 * w + col;
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = tab[(int64_t)(17 * c + 8 * h + j) * H];
+            split3_bf16(v, wp[c][0], wp[c][1], wp[c][2]);
+        }
+    }
+    const uint32_t groups = (n + 31u) >> 5;
+    for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
+        const uint32_t j = gi * 32u + (uint32_t)col;
+        const uint64_t b = boards[j < n ? j : n - 1u];
+        floatx16 hi = {}, lo = {};
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+            const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
+            u32x4 d;
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++)
+                d[jj] = (nib == (uint32_t)(8 * h + 2 * jj) ? 0x3F80u : 0u) | (nib == (uint32_t)(8 * h + 2 * jj + 1) ? 0x3F800000u : 0u);
+            const bf16x8 bv = __builtin_bit_cast(bf16x8, d);
+            hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][0], bv, hi, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][1], bv, lo, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][2], bv, lo, 0, 0, 0);
+        }
+        const uint32_t left = n - gi * 32u < 32u ? n - gi * 32u : 32u;
+        float* blk = out + (size_t)gi * 32u * (uint32_t)H;
+        if ((uint32_t)col < left) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int u = 32 * w + tile_row(i, h);
+                blk[(uint32_t)u * left + (uint32_t)col] = activate<ACT>((hi[i] + lo[i]) + bias[u]);
+            }
+        }
+    }
+}
+
+// layer 0 of a one-hot net from its onehot_l0_mfma_kernel block (group gi, [unit][left]) into LDS [unit][sample]
+// (stride kActStride); samples past the batch read as 0.  Every thread of the block (NT threads) calls it.
+template <int NT>
+__device__ __forceinline__ void load_l0_block(const float* __restrict__ a0, uint32_t n, uint32_t gi, int H, float* out) {
+    const float* blk = a0 + (size_t)gi * 32u * (uint32_t)H;
+    const uint32_t left = n - gi * 32u < 32u ? n - gi * 32u : 32u;
+    const int tid = threadIdx.x;
+    if (left == 32u) {
+        const float4* b4 = reinterpret_cast<const float4*>(blk);
+#pragma unroll 8
+        for (int e4 = tid; e4 < 8 * H; e4 += NT) {   // all of a thread's loads issued before the LDS writes
+            const float4 v = b4[e4];
+            float* o = out + (e4 >> 3) * kActStride + ((e4 & 7) << 2);
+            o[0] = v.x;
+            o[1] = v.y;
+            o[2] = v.z;
+            o[3] = v.w;
+        }
+    } else {
+        for (int e = tid; e < 32 * H; e += NT) {
+            const uint32_t u = (uint32_t)e >> 5, sm = (uint32_t)e & 31u;
+            out[u * kActStride + sm] = sm < left ? blk[u * left + sm] : 0.0f;
+        }
+    }
+}
+
+// KSPLIT: the dense layers by dense_fwd_split (the gradient kernel's forward, for the pattern probe).  A0IN (one-hot,
+// the probe): layer 0 from onehot_l0_mfma_kernel's block of group gi (a0) -- the update's layer-0 bits.
+template <int OBS, int ACT, bool KSPLIT = false, bool A0IN = false>
+__device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, DeepSmem& S, float obs_scale,
+                             const float* a0 = nullptr, uint32_t n = 0, uint32_t gi = 0) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
     // ---- first hidden layer -> S.act[0]
     {
         float* out = S.act[0];
         const int nt0 = net.nt[0];
-        if constexpr (OBS == G2048_OBS_ONEHOT) {
+        if constexpr (A0IN) {
+            load_l0_block<kDeepBlock>(a0, n, gi, 32 * nt0, out);
+        } else if constexpr (OBS == G2048_OBS_ONEHOT) {
             // wave w: boards 8 w .. 8 w + 7, 8 lanes per board; lane k of a board: units 4 k + 32 m (m < nt0)
             const int bb = 8 * w + (lane >> 3), k = lane & 7;
             const uint64_t b = S.board[bb];
@@ -481,10 +640,10 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_policy_kernel(DeepPolArgs 
 // are unused): out[j * ld + u] for u < 32 nt[layer] -- bit for bit what deep_grad_kernel computes (dense layers by
 // dense_fwd_split when the net's gradient instantiation splits k, else deep_forward's chain), for tests that impose
 // the gradient kernel's own activation pattern on an fp64 evaluation.
-template <int OBS, int ACT, bool KSPLIT>
+template <int OBS, int ACT, bool KSPLIT, bool A0IN>
 __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net, const float* packed,
                                                                      const uint64_t* boards, uint32_t n, float obs_scale,
-                                                                     float* out, uint32_t ld) {
+                                                                     float* out, uint32_t ld, const float* a0) {
     __shared__ DeepSmem S;
     const uint32_t groups = (n + 31u) >> 5;
     const int tid = threadIdx.x, layer = net.L - 1, H = 32 * net.nt[layer];
@@ -494,7 +653,7 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net,
             S.board[tid] = boards[j < n ? j : n - 1u];
         }
         __syncthreads();
-        deep_forward<OBS, ACT, KSPLIT>(net, packed, S, obs_scale);
+        deep_forward<OBS, ACT, KSPLIT, A0IN>(net, packed, S, obs_scale, a0, n, gi);
         const float* act = S.act[layer & 1];
         for (int e = tid; e < 32 * H; e += kDeepBlock) {
             const int b = e / H, u = e % H;
@@ -717,7 +876,25 @@ struct DeepGradArgs {
     int tile_begin[kMaxHidden];   // flattened tile index of layer l's first tile (l >= 1)
     int aoff[kMaxHidden];         // LDS float offset of layer l's activations / deltas
     int lds_tail;                 // LDS float offset of the output partials, g, boards and bias sums
+    uint64_t* diag;               // -DG2048_DEEP_DIAG=1 builds only (tools/diag_deep.py): per-wave phase cycles
 };
+
+// Phase-time attribution (tools-only build, -DG2048_DEEP_DIAG=1): each wave adds the s_memtime cycles of every
+// phase (ending at the barrier that closes it, so a phase includes waiting for the slowest wave) to its own slot
+// diag[(block * NW + wave) * kDiagSlots + phase]; slot kDiagSlots - 1 counts the groups.  No stamp in the product.
+constexpr int kDiagSlots = 10;
+#if G2048_DEEP_DIAG
+#define DEEP_STAMP(i)                                             \
+    do {                                                          \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();         \
+        dph[i] += t_ - dlast;                                     \
+        dlast = t_;                                               \
+    } while (0)
+#else
+#define DEEP_STAMP(i) \
+    do {              \
+    } while (0)
+#endif
 
 template <int ACT>
 __device__ __forceinline__ float act_deriv(float a) {   // from the activation (src/reinforce_agent.py:624-636)
@@ -756,47 +933,24 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     const int oq = kBlock / HL, oper = (32 + oq - 1) / oq;   // sample ranges of the output layer
     const float4* wout = reinterpret_cast<const float4*>(P + net.w[L]);
     const uint32_t groups = (a.n + 31u) >> 5;
+#if G2048_DEEP_DIAG
+    uint64_t dph[kDiagSlots] = {};
+    uint64_t dlast = __builtin_amdgcn_s_memtime();
+#endif
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
         const uint32_t j = gi * 32u + (uint32_t)(tid & 31);
         const bool valid = j < a.n;
         if (tid < 32) bds[tid] = valid ? a.boards[j] : 0ull;
         __syncthreads();
+        DEEP_STAMP(0);
         // ---- forward: layer 0
         {
             float* out = actl(0);
             const int nt0 = net.nt[0];
             if constexpr (OBS == G2048_OBS_ONEHOT) {
-                // wave w: boards 8 (w & 3) .. + 7, 8 lanes per board; tiles 4 (w >> 2) .. + 3 (NW = 8), or all 8
-                // tiles in two passes of 4 (NW = 4, two cells' loads in flight: its registers hold 10 dW tiles) --
-                // each unit's sum is the same 16 adds in cell order either way
-                const int bb = 8 * (w & 3) + (lane >> 3), k = lane & 7;
-                const uint64_t b = bds[bb];
-                const int H = 32 * nt0;
-                const auto pass = [&](int m0) {
-                    const float* tab = P + net.w[0] + 4 * k + 32 * m0;
-                    float4 ac[4];
-#pragma unroll
-                    for (int m = 0; m < 4; m++) ac[m] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if constexpr (NW == 4) onehot_gather<4, 2>(tab, b, H, nt0 - m0, ac);
-                    else onehot_gather<4>(tab, b, H, nt0 - m0, ac);
-#pragma unroll
-                    for (int m = 0; m < 4; m++) {
-                        if (m0 + m < nt0) {
-                            const int u = 32 * (m0 + m) + 4 * k;
-                            const float4 bv = *reinterpret_cast<const float4*>(P + net.b[0] + u);
-                            out[(u + 0) * kActStride + bb] = activate<ACT>(ac[m].x + bv.x);
-                            out[(u + 1) * kActStride + bb] = activate<ACT>(ac[m].y + bv.y);
-                            out[(u + 2) * kActStride + bb] = activate<ACT>(ac[m].z + bv.z);
-                            out[(u + 3) * kActStride + bb] = activate<ACT>(ac[m].w + bv.w);
-                        }
-                    }
-                };
-                if constexpr (NW == 8) {
-                    pass(4 * (w >> 2));
-                } else {
-                    pass(0);
-                    if (nt0 > 4) pass(4);
-                }
+                // the group's block from onehot_l0_mfma_kernel (in d0_out: this workgroup overwrites the same rows
+                // with the group's layer-0 deltas at its end)
+                load_l0_block<kBlock>(a.d0_out, a.n, gi, 32 * nt0, out);
             } else {
                 const uint64_t b = bds[col];
                 float x[8];
@@ -818,6 +972,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             }
         }
         __syncthreads();
+        DEEP_STAMP(1);
         // ---- forward: dense layers (each into its own region)
         for (int l = 1; l < L; l++) {
             const float* in = actl(l - 1);
@@ -839,6 +994,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             }
             __syncthreads();
         }
+        DEEP_STAMP(2);
         // ---- output layer partials (as deep_forward; threads 0..255)
         if (tid < 256) {
             const float* in = actl(L - 1);
@@ -858,6 +1014,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             part[pp][bb][3] = s3;
         }
         __syncthreads();
+        DEEP_STAMP(3);
         // ---- logits -> g (threads 0..31, one sample each)
         if (tid < 32) {
             const float* bo = P + net.b[L];
@@ -899,6 +1056,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             for (int k = 0; k < 4; k++) gs[tid][k] = g[k];
         }
         __syncthreads();
+        DEEP_STAMP(4);
         // ---- output layer backward: dW_out, db_{L-1}, delta_{L-1} in place; thread (unit u, sample range q) of
         //      oq ranges, so every thread works (one thread per unit ran 32 serial steps on one or two waves)
         if (tid < oq * HL) {
@@ -930,6 +1088,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             dbo += sgo;
         }
         __syncthreads();
+        DEEP_STAMP(5);
         // ---- dense layers top down: dW_l (MFMA over the 32 samples), then delta_{l-1} (MFMA chain) in place
         for (int l = L - 1; l >= 1; l--) {
             const float* A = actl(l - 1);
@@ -951,6 +1110,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 }
             }
             __syncthreads();                               // every read of a_{l-1} by the dW tiles is done
+            DEEP_STAMP(6);
             // delta_{l-1} = (W_l delta_l) act'(a_{l-1}): output tiles = layer l-1's units, k = layer l's units
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(a.bpacked + a.boff[l]) + lane;
             float* Aw = actl(l - 1);
@@ -970,6 +1130,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 for (int n2 = 0; n2 < 32; n2++) db += drow[n2];
                 dbs[(l - 1) * 256 + tid] = db;
             }
+            DEEP_STAMP(7);
         }
         // ---- first layer's weight gradient
         if constexpr (OBS == G2048_OBS_ONEHOT) {
@@ -1005,7 +1166,18 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             }
         }
         __syncthreads();   // the next group rewrites the boards and layer 0
+        DEEP_STAMP(8);
+#if G2048_DEEP_DIAG
+        dph[kDiagSlots - 1] += 1;
+#endif
     }
+#if G2048_DEEP_DIAG
+    if (a.diag && lane == 0) {
+        uint64_t* slot = a.diag + ((size_t)blockIdx.x * NW + w) * kDiagSlots;
+#pragma unroll
+        for (int i = 0; i < kDiagSlots; i++) slot[i] += dph[i];
+    }
+#endif
     // ---- the output layer's (unit, range) partials summed per unit in range order (LDS: the activation area,
     //      at least kOutRed floats), then this workgroup's partial slab
     {
@@ -1249,29 +1421,20 @@ __global__ void __launch_bounds__(64 * kDw1Waves) onehot_dw1_kernel(const uint64
 // against 16 KiB of deltas read per workgroup.  The one-hot A fragments (the same for every wave) are built once per
 // workgroup: wave w builds pair w (from byte w of each board) into a double-buffered LDS image that every wave
 // reads back (one ds_read_b128 per pair, one pair ahead of its MFMAs).  db1 is each lane's sum of its B values (samples 8 h .. 8 h + 7 of each step, in order), the
-// two lane halves added at the end.  Deltas and boards are loaded two steps ahead (a three-slot register ring).
+// two lane halves added at the end.  Deltas and boards are loaded three steps ahead (a four-slot register ring)
+// through buffer resources.
 // Rows 17 c + 16 (exponent 16, never on a bitboard) are written as zeros.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int kDw1Step = 16;        // samples per MFMA k-step
 constexpr int kDw1MaxWaves = 8;     // 32 units per wave
 
-__device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) {   // round to nearest even at each step: x = p0 + p1 + p2 exactly
-        const __bf16 hh = (__bf16)v[j];
-        const float rr = v[j] - (float)hh;
-        const __bf16 mm = (__bf16)rr;
-        p0[j] = hh;
-        p1[j] = mm;
-        p2[j] = (__bf16)(rr - (float)mm);
-    }
-}
-
 struct Dw1Slot {
-    float v[8];       // deltas of this lane's unit, samples 8 h .. 8 h + 7 of the step
+    float v[8];       // deltas of this lane's unit, samples 8 h .. 8 h + 7 of the step (0 past the range)
     uint32_t bw[8];   // byte w of the same samples' boards: cells 2 w, 2 w + 1 (this wave's cell pair)
 };
 
+// Loads through two buffer resources over this workgroup's sample range [s0, s1): a lane's voffset plus a scalar
+// per-sample offset, so a step's 16 loads need no address arithmetic (64-bit per-load addresses cost ~80 VALU per
+// step), and a load past s1 returns 0 (num_records), which is the tail's zero delta.
 __global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_mfma_kernel(
     const uint64_t* __restrict__ boards, const float* __restrict__ d1, int h1, int64_t m, int64_t ld, int64_t per,
     float* __restrict__ part) {
@@ -1280,20 +1443,27 @@ __global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_mfma_kernel(
     const int r = lane & 31, h = lane >> 5;
     const int64_t s0 = (int64_t)blockIdx.x * per, s1 = s0 + per < m ? s0 + per : m;
     const int u = 32 * w + r;
-    const uint8_t* bbytes = reinterpret_cast<const uint8_t*>(boards) + w;
     const bool live = u < h1;
-    const int64_t uc = live ? u : h1 - 1;
     const uint32_t q = (uint32_t)r >> 4, e = (uint32_t)r & 15u;
+    const int nsteps = s1 > s0 ? (int)((s1 - s0 + kDw1Step - 1) / kDw1Step) : 0;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(d1 + s0 * ld), 0, (int)((s1 - s0) * ld * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint64_t*>(boards + s0), 0, (int)((s1 - s0) * 8), 0x00020000);
+    const uint32_t ld4 = (uint32_t)ld * 4u;
+    // this lane's first delta; a unit past h1 reads past num_records (0) instead of being masked per load
+    const uint32_t dvo = live ? (uint32_t)(8 * h) * ld4 + (uint32_t)u * 4u : 0x80000000u;
+    const uint32_t bvo = (uint32_t)(8 * h) * 8u + (uint32_t)w;                      // its first board byte
     floatx16 acc[8];
 #pragma unroll
     for (int p = 0; p < 8; p++) acc[p] = floatx16{};
     float db = 0.0f;
-    const auto load = [&](int64_t c0, Dw1Slot& sl) {   // unconditional loads (clamped rows), zeros past s1
+    const auto load = [&](int st, Dw1Slot& sl) {
+        const uint32_t so = (uint32_t)(st * kDw1Step);   // the step's first sample, relative to s0
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-            const int64_t s = c0 + 8 * h + k, sc = s < s1 ? s : s1 - 1;
-            sl.v[k] = d1[sc * ld + uc];
-            sl.bw[k] = bbytes[8 * sc];
+            sl.v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, (int)dvo, (int)((so + k) * ld4), 0));
+            sl.bw[k] = __builtin_amdgcn_raw_buffer_load_b8(rb, (int)bvo, (int)((so + k) * 8u), 0);
         }
     };
     const auto build_a = [&](const Dw1Slot& sl, int buf) {   // this wave's cell pair of the step's one-hot
@@ -1305,20 +1475,15 @@ __global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_mfma_kernel(
         }
         abuf[buf][w][lane] = make_uint4(d[0], d[1], d[2], d[3]);
     };
-    // one step: the MFMAs of `cur` (its A image in `buf`) while the loads of two steps ahead are in flight and the
+    // step st: the MFMAs of `cur` (its A image in `buf`) while the loads of three steps ahead are in flight and the
     // next step's A image is built
-    const auto step = [&](Dw1Slot& cur, Dw1Slot& nxt, Dw1Slot& ahead, int64_t c0, int buf) {
-        const int64_t c1 = c0 + kDw1Step, c2 = c0 + 2 * kDw1Step;
-        if (c2 < s1) load(c2, ahead);
-        float v[8];
+    const auto step = [&](Dw1Slot& cur, Dw1Slot& nxt, Dw1Slot& ahead, int st, int buf) {
+        if (st + 3 < nsteps) load(st + 3, ahead);
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            v[k] = (live && c0 + 8 * h + k < s1) ? cur.v[k] : 0.0f;
-            db += v[k];
-        }
+        for (int k = 0; k < 8; k++) db += cur.v[k];
         bf16x8 pl[3];
-        split3_bf16(v, pl[0], pl[1], pl[2]);
-        if (c1 < s1) build_a(nxt, buf ^ 1);
+        split3_bf16(cur.v, pl[0], pl[1], pl[2]);
+        if (st + 1 < nsteps) build_a(nxt, buf ^ 1);
         uint4 a = abuf[buf][0][lane];
 #pragma unroll
         for (int p = 0; p < 8; p++) {
@@ -1330,23 +1495,20 @@ __global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_mfma_kernel(
         }
         __syncthreads();   // the next step's A image is complete; this one is free to be rewritten
     };
-    Dw1Slot sl0, sl1, sl2;
-    if (s0 < s1) {
-        load(s0, sl0);
-        if (s0 + kDw1Step < s1) load(s0 + kDw1Step, sl1);
-        build_a(sl0, 0);
-    }
+    Dw1Slot sl0, sl1, sl2, sl3;
+    if (nsteps > 0) load(0, sl0);
+    if (nsteps > 1) load(1, sl1);
+    if (nsteps > 2) load(2, sl2);
+    if (nsteps > 0) build_a(sl0, 0);
     __syncthreads();
-    int buf = 0;
-    for (int64_t c0 = s0; c0 < s1; c0 += 3 * kDw1Step) {   // block-uniform trip count; the slots rotate by 3
-        step(sl0, sl1, sl2, c0, buf);
-        buf ^= 1;
-        if (c0 + kDw1Step >= s1) break;
-        step(sl1, sl2, sl0, c0 + kDw1Step, buf);
-        buf ^= 1;
-        if (c0 + 2 * kDw1Step >= s1) break;
-        step(sl2, sl0, sl1, c0 + 2 * kDw1Step, buf);
-        buf ^= 1;
+    for (int st = 0; st < nsteps; st += 4) {   // block-uniform trip count; the four slots rotate
+        step(sl0, sl1, sl3, st, 0);
+        if (st + 1 >= nsteps) break;
+        step(sl1, sl2, sl0, st + 1, 1);
+        if (st + 2 >= nsteps) break;
+        step(sl2, sl3, sl1, st + 2, 0);
+        if (st + 3 >= nsteps) break;
+        step(sl3, sl0, sl2, st + 3, 1);
     }
     db += __shfl_xor(db, 32);   // lane half 0 + half 1 (addition commutes: both halves hold the same bits)
     if (!live) return;
@@ -1403,6 +1565,16 @@ int dfail(int code, const char* msg) { return g2048_internal::set_error(code, ms
 int check_hip() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : dfail(G2048_EHIP, hipGetErrorString(e));
+}
+int launch_onehot_l0(const DeepNet& net, const float* packed, const uint64_t* boards, uint32_t n, int activation,
+                     float* out, hipStream_t s) {
+    const int64_t groups = ((int64_t)n + 31) / 32, cap = device_cus();
+    const int grid = (int)(groups < cap ? groups : cap);   // one 8-wave workgroup per CU, W1 resident in registers
+    if (activation == G2048_ACT_RELU)
+        hipLaunchKernelGGL(onehot_l0_mfma_kernel<0>, dim3(grid), dim3(64 * kL0Waves), 0, s, net, packed, boards, n, out);
+    else
+        hipLaunchKernelGGL(onehot_l0_mfma_kernel<1>, dim3(grid), dim3(64 * kL0Waves), 0, s, net, packed, boards, n, out);
+    return check_hip();
 }
 }  // namespace
 
@@ -1566,27 +1738,35 @@ int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, 
     if (!packed || (n > 0 && (!boards || !out))) return dfail(G2048_EINVAL, "deep hidden: NULL buffer");
     if (n == 0) return G2048_OK;
     const bool ksplit = deep_grad_variant(net).ksplit != 0;   // the full net's gradient instantiation
+    hipStream_t s = (hipStream_t)stream;
+    float* a0 = nullptr;   // one-hot: the update's layer 0 (onehot_l0_mfma_kernel) in a scratch buffer
+    if (obs_mode == G2048_OBS_ONEHOT) {
+        if (hipMallocAsync(reinterpret_cast<void**>(&a0), (size_t)n * 32 * net.nt[0] * sizeof(float), s) != hipSuccess)
+            return dfail(G2048_EHIP, "deep hidden: scratch allocation failed");
+        const int rc = launch_onehot_l0(net, packed, boards, (uint32_t)n, activation, a0, s);
+        if (rc) return rc;
+    }
     net.L = layer + 1;   // truncated: deep_forward stops after `layer` (offsets of the kept layers unchanged)
     const int64_t groups = (n + 31) / 32, cap = 2 * (int64_t)device_cus();
     const int grid = (int)(groups < cap ? groups : cap);
-    hipStream_t s = (hipStream_t)stream;
-#define G2048_HIDDEN(O, A)                                                                                          \
+#define G2048_HIDDEN(O, A, A0)                                                                                      \
     do {                                                                                                            \
         if (ksplit)                                                                                                 \
-            hipLaunchKernelGGL((deep_hidden_kernel<O, A, true>), dim3(grid), dim3(kDeepBlock), 0, s, net, packed,   \
-                               boards, (uint32_t)n, obs_scale, out, (uint32_t)ld);                                  \
+            hipLaunchKernelGGL((deep_hidden_kernel<O, A, true, A0>), dim3(grid), dim3(kDeepBlock), 0, s, net,       \
+                               packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld, a0);                      \
         else                                                                                                        \
-            hipLaunchKernelGGL((deep_hidden_kernel<O, A, false>), dim3(grid), dim3(kDeepBlock), 0, s, net, packed,  \
-                               boards, (uint32_t)n, obs_scale, out, (uint32_t)ld);                                  \
+            hipLaunchKernelGGL((deep_hidden_kernel<O, A, false, A0>), dim3(grid), dim3(kDeepBlock), 0, s, net,      \
+                               packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld, a0);                      \
     } while (0)
     if (obs_mode == G2048_OBS_ONEHOT) {
-        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_ONEHOT, 0); else G2048_HIDDEN(G2048_OBS_ONEHOT, 1);
+        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_ONEHOT, 0, true); else G2048_HIDDEN(G2048_OBS_ONEHOT, 1, true);
     } else if (obs_mode == G2048_OBS_LOG2) {
-        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_LOG2, 0); else G2048_HIDDEN(G2048_OBS_LOG2, 1);
+        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_LOG2, 0, false); else G2048_HIDDEN(G2048_OBS_LOG2, 1, false);
     } else {
-        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_RAW, 0); else G2048_HIDDEN(G2048_OBS_RAW, 1);
+        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_RAW, 0, false); else G2048_HIDDEN(G2048_OBS_RAW, 1, false);
     }
 #undef G2048_HIDDEN
+    if (a0 && hipFreeAsync(a0, s) != hipSuccess) return dfail(G2048_EHIP, "deep hidden: scratch free failed");
     return check_hip();
 }
 
@@ -1668,6 +1848,13 @@ int launch_deep_grad(const DeepGradArgs& a, const DeepGradVariant& v, int grid, 
 }
 }  // namespace
 
+#if G2048_DEEP_DIAG
+namespace {
+uint64_t* g_deep_diag = nullptr;
+}
+extern "C" void g2048_diag_deep_stamps(uint64_t* p) { g_deep_diag = p; }   // tools-only build (no header entry)
+#endif
+
 extern "C" {
 
 int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden, const int32_t* hidden,
@@ -1723,9 +1910,16 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
     a.obs_scale = obs_scale;
     a.n = (uint32_t)n;
     a.use_mask = use_mask;
+#if G2048_DEEP_DIAG
+    a.diag = g_deep_diag;
+#endif
     const int64_t lds = deep_grad_lds_bytes(net, v.nw);
     hipStream_t s = (hipStream_t)stream;
     const int grid = (int)nparts;   // every workgroup writes its slab (zeros when it gets no group)
+    if (obs_mode == G2048_OBS_ONEHOT && n > 0) {   // layer 0 on the bf16 MFMA, into d0_out (group blocks)
+        const int rc = launch_onehot_l0(net, packed, boards, (uint32_t)n, activation, d0_out, s);
+        if (rc) return rc;
+    }
     if (obs_mode == G2048_OBS_ONEHOT)
         return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_ONEHOT, 0>(a, v, grid, lds, s)
                                             : launch_deep_grad<G2048_OBS_ONEHOT, 1>(a, v, grid, lds, s);
@@ -1759,6 +1953,7 @@ int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m,
                      float* partials, int64_t nparts, void* stream) {
     if (h1 < 1 || h1 > 256 || m < 0 || ld < h1 || per < 1) return dfail(G2048_EINVAL, "one-hot dW1: bad sizes");
     if (nparts != (m + per - 1) / per || nparts > 65535) return dfail(G2048_EINVAL, "one-hot dW1: nparts != ceil(m / per)");
+    if (per * ld * 4 >= ((int64_t)1 << 31)) return dfail(G2048_EINVAL, "one-hot dW1: per x ld too large (2 GiB per slab range)");
     if (m > 0 && (!boards || !d1 || !partials)) return dfail(G2048_EINVAL, "one-hot dW1: NULL buffer");
     if (m == 0) return G2048_OK;
 #if G2048_DW1_SCATTER   // A/B build only: round 4's register scatter

@@ -1,0 +1,69 @@
+"""TOOL: where deep_grad_kernel's time goes, phase by phase, on the reference runner config (runner.py:10-47:
+one-hot obs, [256, 128, 64] ReLU, actor-critic MSE, Adam).  Needs the stamp build:
+
+    python tools/build_variants.py --tu g2048_deep.hip deepdiag=G2048_DEEP_DIAG=1
+    python tools/diag_deep.py [--episodes 262144] [--lib tools/libg2048_deepdiag.so]
+
+Each wave adds the s_memtime cycles of every phase of every 32-sample group it runs (a phase ends at the barrier
+that closes it, so it includes the wait for the slowest wave); printed: cycles per group per phase (mean over waves)
+for one update (actor + critic launches), and the same as a share of the group.  The MFMA floor per group for this
+net (the busiest wave's MFMA cycles, its SIMD shared with the other workgroup's wave) is printed beside it."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ap = argparse.ArgumentParser()
+ap.add_argument("--episodes", type=int, default=262144)
+ap.add_argument("--lib", default="tools/libg2048_deepdiag.so")
+ap.add_argument("--label", default="")
+args = ap.parse_args()
+from rl2048_amd import _lib as L  # noqa: E402
+
+L.use_library_for_tools(args.lib)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rl2048_amd import Game2048EnvConfig  # noqa: E402
+from rl2048_amd.agent import ReinforceAgent, ReinforceAgentConfig  # noqa: E402
+from rl2048_amd.mlp import MLPConfig  # noqa: E402
+
+ENV = dict(obs_mode="onehot", obs_log2_scale=1.0, reward_mode="log2", base_reward_scale=1.0, bonus_mode="off",
+           bonus_scale=1.0, step_reward=0.0, endgame_penalty=0.0, use_action_mask=True, invalid_action_penalty=-1.0,
+           max_steps=None, empty_tile_reward=0.05, merge_reward=0.0)
+MLP = dict(hidden_sizes=[256, 128, 64], activation="ReLU", init_distribution="HeNormal", last_init_normal=True)
+AGENT = dict(gamma=0.99, learning_rate=0.01, baseline_mode="batch", model_seed=0, reward_rank_weights=None,
+             optimizer="adam", adam_beta1=0.9, adam_beta2=0.999, augmentation=False, use_critic=True,
+             critic_learning_rate=0.0005, critic_loss_type="mse", huber_delta=1.0)
+PHASES = ["boards", "layer0", "dense_fwd", "out_partials", "logits_g", "out_bwd", "dW", "delta+db", "first_layer_out"]
+dev = torch.device("cuda", 0)
+agent = ReinforceAgent(Game2048EnvConfig(**ENV), MLPConfig(**MLP), ReinforceAgentConfig(**AGENT), device=dev)
+lib = L.lib()
+lib.g2048_diag_deep_stamps.argtypes = [ctypes.c_void_p]
+slots = 4096 * 10
+buf = torch.zeros(slots, dtype=torch.int64, device=dev)
+E = args.episodes
+for rep in range(2):
+    es = np.arange(3 + rep * E, 3 + (rep + 1) * E, dtype=np.int64)
+    batch = agent.rollout_batch(es, es + 7 * E)
+    torch.cuda.synchronize()
+    buf.zero_()
+    lib.g2048_diag_deep_stamps(ctypes.c_void_p(buf.data_ptr()))
+    agent.update_from_batch(batch)
+    torch.cuda.synchronize()
+    lib.g2048_diag_deep_stamps(None)
+    d = buf.view(-1, 10).cpu().numpy().astype(np.float64)
+    d = d[d[:, 9] > 0]
+    per = d[:, :9] / d[:, 9:10]                      # cycles per group, per wave
+    mean = per.mean(axis=0)
+    tot = mean.sum()
+    print(json.dumps({"label": args.label, "rep": rep, "episodes": E, "samples": int(batch.lengths.sum()),
+                      "waves": int(d.shape[0]), "groups_per_wave": float(d[:, 9].mean()),
+                      "cycles_per_group": round(tot),
+                      # the busiest wave's MFMAs (4-wave variant: 512 x 64 cycles), its SIMD shared with the other
+                      # workgroup's wave: 2 x that per group at 100 % MFMA
+                      "mfma_floor_cycles_per_group": 2 * 512 * 64,
+                      "phases_cycles": {p: round(v) for p, v in zip(PHASES, mean)},
+                      "phases_share": {p: round(v / tot, 3) for p, v in zip(PHASES, mean)}}), flush=True)

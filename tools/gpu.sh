@@ -5,7 +5,7 @@
 #   RUN=r5a tools/gpu.sh tests:tests/test_gpu_deep.py refconf pmc_refconf:262144 bench smoke prof_step
 #
 # steps:
-#   tests[:ARGS]        pytest -m gpu over ARGS (space-separated after the colon; default: the whole suite)
+#   tests[:ARGS]        pytest -m gpu over ARGS (shell-parsed after the colon; default: the whole suite)
 #   smoke               __graft_entry__.smoke()
 #   bench               the driver's bench command (bench.py --gpus 1 --steps 20 --warmup 5)
 #   prof_step           rocprofv3 kernel stats of 200 step-kernel launches (bench.py step leg only)
@@ -51,9 +51,9 @@ for step in "$@"; do
     echo "=== $step" | cut -c1-200
     case $name in
     tests)
-        # shellcheck disable=SC2086
-        timeout -k 10 900 python3 -u -m pytest ${arg:-tests} -m gpu -v -s -p no:cacheprovider --timeout 300 \
-            --timeout-method thread > "$O/tests_${RUN:-gpu}_$SECONDS.log" 2>&1
+        # ARGS is shell-parsed (quote a -k expression inside it: "tests:tests/x.py -k 'a or b'")
+        eval "timeout -k 10 900 python3 -u -m pytest ${arg:-tests} -m gpu -v -s -p no:cacheprovider --timeout 300 \
+            --timeout-method thread" > "$O/tests_${RUN:-gpu}_$SECONDS.log" 2>&1
         rc=$?
         tail -3 "$(ls -t "$O"/tests_*.log | head -1)" || true
         [ $rc -eq 0 ] || { grep -E "FAILED|Error|error" "$(ls -t "$O"/tests_*.log | head -1)" | head -40; exit 1; }
