@@ -461,10 +461,15 @@ def main():
     device = torch.device("cuda", local_rank % max(ndev, 1))
     torch.cuda.set_device(device)
     if world > 1:
+        # rank 0 ran the PMC passes and the CPU baseline before getting here (each bounded by its own timeout, a
+        # few minutes at most): the rendezvous timeout is set well above that
+        import datetime
+
+        tmo = datetime.timedelta(minutes=30)
         if ndev >= world:
-            dist.init_process_group("nccl", device_id=device)   # RCCL: one rank per GPU (the production layout)
+            dist.init_process_group("nccl", device_id=device, timeout=tmo)   # RCCL: one rank per GPU (production)
         else:
-            dist.init_process_group("gloo")   # rehearsal of the N-rank path with ranks sharing a GPU (timing only)
+            dist.init_process_group("gloo", timeout=tmo)   # rehearsal of the N-rank path with ranks sharing a GPU
     B = args.boards
     # The extra legs (training iterations, policy rollouts) run first, so that the headline env-step leg below is
     # timed on a chip at its working clock: on a cold chip the first ~20 launches of the step kernel run 10-30 %
@@ -485,9 +490,10 @@ def main():
             policy["train_iteration_configs2"] = train_iteration_rate(torch, device, episodes=1 << 20, repeats=1,
                                                                       critic=True)
             if not args.no_refconfig:
+                # each size: one warm-up iteration, then the timed one (tools/bench_refconfig.py reports the same)
                 policy["train_iteration_reference_runner_config"] = {
                     "65536": train_iteration_refconfig(torch, device, 1 << 16),
-                    "1048576": train_iteration_refconfig(torch, device, 1 << 20, repeats=0)}
+                    "1048576": train_iteration_refconfig(torch, device, 1 << 20)}
         except Exception as e:  # noqa: BLE001 -- an extra, never the headline
             policy = {"error": repr(e)}
     torch.cuda.empty_cache()

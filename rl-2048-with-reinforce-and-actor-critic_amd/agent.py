@@ -129,10 +129,22 @@ def _unrecord_actor(rec: torch.Tensor, w3: torch.Tensor, c0: int, m: int) -> tor
     cols = torch.arange(c0, c0 + m, device=rec.device)
     bits = (words[cols >> 4] >> (cols & 15)[:, None]) & 1                                 # [m, H2p]
     gc = g[cols]
-    # the kernel's operation order, one rounding per step (fmaf = one rounding: evaluated in fp64, then rounded)
+    # the kernel's operation order, one rounding per step.  fmaf = fl32(g w + dh): the product is exact in fp64, the
+    # fp64 sum s may round (a 48-bit product plus dh), and rounding s to fp32 could then round twice; the exact
+    # error e of the fp64 sum (TwoSum) settles the one case that matters -- s exactly halfway between two floats,
+    # where fp32's tie-to-even picked the neighbour on the wrong side of the true value s + e.
     dh = (gc[:, 0:1] * w3[None, :, 0])
     for k in (1, 2, 3):
-        dh = (gc[:, k:k + 1].double() * w3[None, :, k].double() + dh.double()).to(torch.float32)
+        p = gc[:, k:k + 1].double() * w3[None, :, k].double()
+        d = dh.double()
+        s = p + d
+        bb = s - p
+        e = (p - (s - bb)) + (d - bb)
+        r = s.to(torch.float32)
+        diff = s - r.double()
+        nxt = torch.nextafter(r, torch.where(diff > 0, torch.full_like(r, float("inf")), torch.full_like(r, float("-inf"))))
+        tie = (diff != 0) & (2.0 * diff.abs() == (nxt.double() - r.double()).abs())
+        dh = torch.where(tie & (e * diff > 0), nxt, r)
     return (dh * bits.to(torch.float32)).t()
 
 
@@ -1266,8 +1278,10 @@ class ReinforceAgent:
                                max_tile=torch.ones(n, dtype=torch.int64, device=dev) << max_e.to(torch.int64),
                                final_boards=final, probs=probs[:T] if probs is not None else None)
 
-    # first trajectory capacity of g2048_deep_rollout when max_steps is None (doubled while episodes run past it)
+    # first trajectory capacity of g2048_deep_rollout when max_steps is None (doubled while episodes run past it), and
+    # the most rows it may grow to (an episode that never ends raises instead of exhausting device memory)
     deep_rollout_cap0 = 512
+    deep_rollout_max_rows = 1 << 24
 
     def _rollout_deep(self, env_seeds, policy_seeds, dspec, use_greedy: bool, record_probs: bool) -> TrajectoryBatch:
         """rollout_batch through g2048_deep_rollout (any depth, one-hot obs, max_steps None): every episode runs
@@ -1322,6 +1336,18 @@ class ReinforceAgent:
             queue.zero_()
             sus_count.zero_()
             grow = cap
+            # The batch is time-major [T, n] for all n episodes (the update's layout), so a few long episodes grow
+            # every lane's rows.  An episode that never ends (max_steps None with invalid actions allowed, where the
+            # reference itself would loop forever) must not run the device out of memory: refuse past the rows the
+            # free memory holds, or past deep_rollout_max_rows.
+            row_bytes = n * (8 + 1 + 8 + 1 + (16 if probs is not None else 0))
+            free_b = torch.cuda.mem_get_info(dev)[0] if dev.type == "cuda" else 1 << 62
+            if cap + grow > self.deep_rollout_max_rows or (cap + grow) * row_bytes > free_b + cap * row_bytes // 2:
+                raise RuntimeError(
+                    f"rollout_batch (max_steps=None): {k} episode(s) still running after {cap} steps; growing the "
+                    f"[T, n] trajectory buffer to {cap + grow} rows needs {(cap + grow) * row_bytes / 2**30:.1f} GiB "
+                    f"(free: {free_b / 2**30:.1f} GiB, row limit {self.deep_rollout_max_rows}) -- set max_steps or "
+                    f"use_action_mask=True")
             boards = torch.cat([boards, torch.empty(grow, n, dtype=torch.int64, device=dev)])
             actions = torch.cat([actions, torch.zeros(grow, n, dtype=torch.uint8, device=dev)])
             rewards = torch.cat([rewards, torch.zeros(grow, n, dtype=torch.float64, device=dev)])

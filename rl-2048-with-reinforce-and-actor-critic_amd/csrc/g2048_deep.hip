@@ -917,9 +917,14 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     float (*gs)[4] = reinterpret_cast<float (*)[4]>(lds_end + 8 * 32 * 4);       // [32][4]
     uint64_t* bds = reinterpret_cast<uint64_t*>(lds_end + 8 * 32 * 4 + 32 * 4);  // [32]
     float* dbs = lds_end + 8 * 32 * 4 + 32 * 4 + 64;                             // [kMaxHidden][256]: db_l of unit tid
+    float* wol = dbs + kMaxHidden * 256;                                         // [HL][4] output weights, then [4] bias
     if (tid < 256)
         for (int l = 0; l < kMaxHidden; l++) dbs[l * 256 + tid] = 0.0f;
     const float* P = a.packed;
+    {   // the output layer's weights and bias in LDS for the whole launch (its phases read them every group)
+        const int HLw = 32 * net.nt[L - 1] * 4;
+        for (int i = tid; i < HLw + 4; i += kBlock) wol[i] = i < HLw ? P[net.w[L] + i] : P[net.b[L] + (i - HLw)];
+    }
     floatx16 acc[TPW];
 #pragma unroll
     for (int k = 0; k < TPW; k++) acc[k] = floatx16{};
@@ -927,11 +932,13 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     floatx16 acc0[kA0];
 #pragma unroll
     for (int i = 0; i < kA0; i++) acc0[i] = floatx16{};
-    // dW_out / db_{L-1} partials of this thread's (unit, sample range); db_out (threads 0..3: output tid)
-    float dwo[4] = {0.f, 0.f, 0.f, 0.f}, dbl = 0.f, dbo = 0.f;
+    // dW_out / db_{L-1} partials of this thread's (unit, sample range); db_out: threads 0..31 sum their sample slot's
+    // g over the groups (the slots are added in order at the end)
+    float dwo[4] = {0.f, 0.f, 0.f, 0.f}, dbl = 0.f, dbo4[4] = {0.f, 0.f, 0.f, 0.f};
     const int HL = 32 * net.nt[L - 1];
     const int oq = kBlock / HL, oper = (32 + oq - 1) / oq;   // sample ranges of the output layer
-    const float4* wout = reinterpret_cast<const float4*>(P + net.w[L]);
+    const float4* wout = reinterpret_cast<const float4*>(wol);
+    const float* bo = wol + 4 * HL;
     const uint32_t groups = (a.n + 31u) >> 5;
 #if G2048_DEEP_DIAG
     uint64_t dph[kDiagSlots] = {};
@@ -940,7 +947,12 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
         const uint32_t j = gi * 32u + (uint32_t)(tid & 31);
         const bool valid = j < a.n;
+        const uint32_t jc = valid ? j : a.n - 1u;
         if (tid < 32) bds[tid] = valid ? a.boards[j] : 0ull;
+        // the sample's coefficient / action / target, loaded now so that the forward covers their latency
+        const float cf = (tid < 32 && valid) ? a.coef[jc] : 0.0f;
+        const uint32_t act_j = (tid < 32 && !a.critic) ? a.actions[jc] : 0u;
+        const float tg = (tid < 32 && a.critic) ? a.target[jc] : 0.0f;
         __syncthreads();
         DEEP_STAMP(0);
         // ---- forward: layer 0
@@ -1017,7 +1029,6 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         DEEP_STAMP(3);
         // ---- logits -> g (threads 0..31, one sample each)
         if (tid < 32) {
-            const float* bo = P + net.b[L];
             float lg[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -1026,12 +1037,11 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 for (int q = 1; q < 8; q++) v += part[q][tid][k];
                 lg[k] = v + bo[k];
             }
-            const float cf = valid ? a.coef[j] : 0.0f;
             float g[4];
             if (!a.critic) {
                 // logits_to_probs (src/MLP.py:139-156) and the policy-gradient logits delta (:328-354)
                 const uint32_t mw = a.use_mask ? mask_word_of(bds[tid]) : 0x01010101u;
-                const uint32_t act = valid ? a.actions[j] : 0u;
+                const uint32_t act = valid ? act_j : 0u;
                 float l4[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) l4[k] = ((mw >> (8 * k)) & 0xFFu) ? lg[k] : -1e9f;
@@ -1044,7 +1054,6 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf;
             } else {
                 // the critic's value-loss gradient (update_batch :403-498, _get_grad_logits_critic :884-910)
-                const float tg = valid ? a.target[j] : 0.0f;
                 const float diff = lg[0] - tg;
                 const float gd = (a.huber && fabsf(diff) > a.huber_delta) ? copysignf(a.huber_delta, diff) : diff;
                 g[0] = gd * cf;
@@ -1053,7 +1062,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 if (valid && a.v_out) a.v_out[j] = lg[0];
             }
 #pragma unroll
-            for (int k = 0; k < 4; k++) gs[tid][k] = g[k];
+            for (int k = 0; k < 4; k++) {
+                gs[tid][k] = g[k];
+                dbo4[k] += g[k];
+            }
         }
         __syncthreads();
         DEEP_STAMP(4);
@@ -1081,11 +1093,6 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             }
             dwo[0] = d0; dwo[1] = d1; dwo[2] = d2; dwo[3] = d3;
             dbl = db;
-        }
-        if (tid < 4) {
-            float sgo = 0.f;
-            for (int n2 = 0; n2 < 32; n2++) sgo += gs[n2][tid];
-            dbo += sgo;
         }
         __syncthreads();
         DEEP_STAMP(5);
@@ -1179,9 +1186,14 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     }
 #endif
     // ---- the output layer's (unit, range) partials summed per unit in range order (LDS: the activation area,
-    //      at least kOutRed floats), then this workgroup's partial slab
+    //      at least kOutRed floats), db_out's 32 sample slots in slot order, then this workgroup's partial slab
+    float dbo = 0.0f;
     {
         float* red = dyn;                                   // [oq][HL][5]
+        if (tid < 32) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) gs[tid][k] = dbo4[k];
+        }
         if (tid < oq * HL) {
 #pragma unroll
             for (int k = 0; k < 4; k++) red[tid * 5 + k] = dwo[k];
@@ -1197,6 +1209,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             for (int k = 0; k < 4; k++) dwo[k] = sum[k];
             dbs[(L - 1) * 256 + tid] = sum[4];
         }
+        if (tid < 4)
+            for (int q = 0; q < 32; q++) dbo += gs[q][tid];
         __syncthreads();
     }
     float* out = a.part + (size_t)blockIdx.x * a.pslab;
@@ -1304,8 +1318,8 @@ int64_t deep_grad_act_floats(const DeepNet& n, int nw) {
     const int64_t red = 5 * 64 * nw;
     return units * kActStride > red ? units * kActStride : red;
 }
-int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {
-    return (deep_grad_act_floats(n, nw) + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256) * 4;
+int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, bias sums, output weights / bias
+    return (deep_grad_act_floats(n, nw) + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256 + 256 * 4 + 4) * 4;
 }
 
 // the instantiation that covers the net (nw = 0: none; see deep_grad_kernel).  The 4-wave and the 64-tile ones are

@@ -16,6 +16,7 @@
 // exact: a padded unit's outgoing weights are zero.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 
 #include "g2048.h"
@@ -1490,10 +1491,19 @@ bool grad_coop_enabled() {
 template <int ACT, int OBS, int FAC>
 void launch_coop(const GradArgs& a, int grid, hipStream_t s) {
     constexpr int kBytes = CoopLds<8, 8>::kBytes;
-    static bool attr_set = false;   // a failure shows as the launch's error (hipGetLastError in the caller)
-    if (!attr_set && hipFuncSetAttribute(reinterpret_cast<const void*>(&grad_coop_kernel<8, 8, ACT, OBS, FAC>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, kBytes) == hipSuccess)
-        attr_set = true;
+    // the dynamic-LDS attribute is per kernel and device: one bit per device id, set on the first launch there (two
+    // threads racing both set it, harmlessly).  A failure skips the launch and stays the last HIP error, which the
+    // caller's hipGetLastError check reports.
+    static std::atomic<uint64_t> attr_set{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (!(attr_set.load(std::memory_order_acquire) & bit)) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&grad_coop_kernel<8, 8, ACT, OBS, FAC>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kBytes) != hipSuccess)
+            return;
+        attr_set.fetch_or(bit, std::memory_order_acq_rel);
+    }
     hipLaunchKernelGGL((grad_coop_kernel<8, 8, ACT, OBS, FAC>), dim3(grid), dim3(kPolBlock), (unsigned)kBytes, s, a);
 }
 

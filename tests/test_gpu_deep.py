@@ -244,6 +244,20 @@ def _agent(env: dict, hidden, act="ReLU", **acfg):
                           ReinforceAgentConfig(**acfg), device=DEV)
 
 
+def test_deep_rollout_refuses_unbounded_growth():
+    """max_steps=None: episodes still running when the trajectory buffer would grow past deep_rollout_max_rows raise
+    a clear RuntimeError instead of doubling the [T, n] buffers until the device runs out of memory (an episode the
+    reference would play forever -- invalid actions allowed -- must not take the process down)."""
+    a = _agent(REFCONF_ENV, [64, 32])
+    a.deep_rollout_cap0, a.deep_rollout_max_rows = 8, 12
+    es = np.arange(7_000, 7_000 + 257, dtype=np.int64)
+    with pytest.raises(RuntimeError, match="still running after 8 steps"):
+        a.rollout_batch(es, es + 10 ** 9)
+    a.deep_rollout_max_rows = 1 << 24                     # and the same agent then rolls out normally
+    b = a.rollout_batch(es, es + 10 ** 9)
+    assert b.T > 8 and int(b.lengths.min()) > 0
+
+
 @pytest.mark.parametrize("env,hidden", [(REFCONF_ENV, [256, 128, 64]),
                                         (dict(obs_mode="log2", obs_log2_scale=0.0625, max_steps=None), [256, 256]),
                                         (dict(REFCONF_ENV, max_steps=70), [40, 33, 20, 10])])

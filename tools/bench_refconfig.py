@@ -1,7 +1,8 @@
 """Time one training iteration (rollout_batch + update_from_batch) of the reference runner's documented config
 (runner.py:10-47: one-hot obs, MLP [256, 128, 64] ReLU, actor-critic MSE, Adam, batch baseline, max_steps None) at
 the given episode counts, against the package found under --repo (so a checkout of an earlier round can be timed
-by the same script).  One warm-up iteration at the first size; prints one JSON object per size.
+by the same script).  One warm-up iteration at every size (rep 0), then the timed one (rep 1) -- the
+definition bench.py's train_iteration_reference_runner_config uses; prints one JSON object per iteration.
 
     python tools/bench_refconfig.py [--repo DIR] [--episodes 65536 1048576]     (G2048_LIB=<path>: an A/B build)
 """
@@ -39,7 +40,7 @@ AGENT = dict(gamma=0.99, learning_rate=0.01, baseline_mode="batch", model_seed=0
 dev = torch.device("cuda", 0)
 agent = ReinforceAgent(Game2048EnvConfig(**ENV), MLPConfig(**MLP), ReinforceAgentConfig(**AGENT), device=dev)
 for si, E in enumerate(args.episodes):
-    for rep in range(2 if si == 0 else 1):
+    for rep in range(2):   # one warm-up iteration at every size, then the timed one (bench.py's definition)
         es = np.arange(3 + (rep + 10 * si) * E, 3 + (rep + 10 * si + 1) * E, dtype=np.int64)
         ps = es + 7 * E
         torch.cuda.synchronize()
