@@ -241,10 +241,26 @@ int g2048_actor_grad(const float* packed, const float* grad_packed, int h1, int 
                      float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions, const float* coef,
                      int64_t n, int64_t ld, float* a1t, float* d2t, float* partials, int64_t waves, int d2_form,
                      void* stream);
+/* ABI 14: the per-row critic pass's TD targets inside the gradient kernels (g2048_critic_grad, g2048_deep_grad).
+ * With td != NULL the kernels ignore `target` / `value_out` and compute target_j =
+ * ((v_next[lane[j]] * gamma) * has_next[j]) + reward[j] in fp32 (the host's operation order), writing the launch's
+ * V(s_j) to v_out[lane[j]]: the time rows of the critic branch (src/reinforce_agent.py:423-443, V(s') = the next
+ * step's value) run one launch each, last row first, with two lane-indexed value buffers alternating and no
+ * host-side gather or scatter between launches.  v_next must be finite for every lane read (rows with
+ * has_next = 0 multiply it by 0). */
+typedef struct g2048_td_rows {
+    const int64_t* lane;     /* sample j -> its episode (batch column) */
+    const float* reward;     /* r_j (fp32, the critic's rewards) */
+    const float* has_next;   /* 1.0 when step j has a successor in its episode, else 0.0 */
+    const float* v_next;     /* by lane: V of the next time row */
+    float* v_out;            /* by lane: this launch's V(s) */
+    float gamma;
+    int32_t reserved;
+} g2048_td_rows;
 /* The critic branch of update_batch (src/reinforce_agent.py:403-498, _get_grad_logits_critic :884-910) on the same
  * kernel: the critic packed like the actor with its value head [h2 x 1] / [1] as output 0 of a 4-wide layer (outputs
  * 1..3 zero); per sample the value V(s), the TD error delta_out = target - V (target = r + gamma V(s') m from the
- * host), and dL/dV = (V - target) (loss 0, MSE) or its Huber clip at huber_delta (loss 1), times weight[i];
+ * host, or from td: g2048_td_rows), and dL/dV = (V - target) (loss 0, MSE) or its Huber clip at huber_delta (loss 1), times weight[i];
  * the outputs as for g2048_actor_grad (only column / entry 0 of dW3 / db3 is the value head's), plus V(s) per
  * sample in value_out (NULL ok).  Column window: sample i's a1^T / d2^T column is col_off + i, and the columns
  * col_off .. col_off + ncols - 1 are written (those past n as zero-coefficient padding; col_off, ncols multiples
@@ -260,7 +276,7 @@ int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int
                       float obs_scale, int loss, float huber_delta, const uint64_t* boards, const float* target,
                       const float* weight, float* delta_out, float* value_out, int64_t n, int64_t ld, int64_t col_off,
                       int64_t ncols, float* a1t, float* d2t, float* partials, int accumulate, int64_t waves,
-                      int d2_form, void* stream);
+                      int d2_form, const g2048_td_rows* td, void* stream);
 
 /* The layer-2 weight / bias gradient of the fused update (the a1 d2^T outer products of _backpropagation,
  * src/reinforce_agent.py:639-678, summed over samples): over the columns [col0, col0 + ncols) of the column
@@ -386,7 +402,7 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
                     int activation, int obs_mode, float obs_scale, int use_mask, const uint64_t* boards,
                     const uint8_t* actions, const float* coef, int critic, int loss, float huber_delta,
                     const float* target, float* delta_out, float* value_out, float* d0_out, int64_t n,
-                    float* partials, int64_t nparts, void* stream);
+                    float* partials, int64_t nparts, const g2048_td_rows* td, void* stream);
 /* The update's one-hot first layer: out[s * ld + j] = act(b1[j] + sum_c W1[17 c + e_c(s), j]) for s < m, j < h1
  * (W1 the [272, h1] parameter) -- the kept layer-1 activations of _backpropagation (src/reinforce_agent.py:639-678)
  * without the [m, 272] one-hot obs. */

@@ -132,6 +132,13 @@ class Traj(ctypes.Structure):
                                                      "totals", "max_tile", "final_board")]
 
 
+class TdRows(ctypes.Structure):
+    """g2048_td_rows: the per-row critic pass's TD target inputs (lane-indexed V(s') in, V(s) out)."""
+    _fields_ = [("lane", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("has_next", ctypes.c_void_p),
+                ("v_next", ctypes.c_void_p), ("v_out", ctypes.c_void_p), ("gamma", ctypes.c_float),
+                ("reserved", ctypes.c_int32)]
+
+
 class Suspend(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in ("board", "meta", "total", "list", "count")]
 
@@ -170,7 +177,7 @@ def _declare(L):
     L.g2048_actor_grad_waves.argtypes = []
     L.g2048_actor_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, vp, vp, vp, i64, i64, vp, vp, vp, i64, i32, vp]
     L.g2048_critic_grad.argtypes = [vp, vp, i32, i32, i32, i32, f, i32, f, vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, vp,
-                                    vp, i32, i64, i32, vp]
+                                    vp, i32, i64, i32, P(TdRows), vp]
     L.g2048_dw2.argtypes = [vp, vp, i32, i32, i64, i64, i64, i64, vp, i64, vp]
     L.g2048_fold_partials.argtypes = [vp, i64, i64, vp, vp]
     L.g2048_dw2_factored.argtypes = [vp, vp, vp, i32, i32, i64, i64, i64, i64, vp, i64, vp]
@@ -191,7 +198,7 @@ def _declare(L):
     L.g2048_deep_grad_parts.restype = i32
     L.g2048_deep_grad_pack.argtypes = [vp, i32, i32, vp, vp, i64, vp]
     L.g2048_deep_grad.argtypes = [vp, vp, i32, vp, i32, i32, f, i32, vp, vp, vp, i32, i32, f, vp, vp, vp, vp, i64, vp,
-                                  i64, vp]
+                                  i64, P(TdRows), vp]
     L.g2048_onehot_layer1.argtypes = [vp, vp, i32, i32, vp, i64, i64, vp, vp]
     L.g2048_onehot_dw1_slab.argtypes = [i32]
     L.g2048_onehot_dw1_slab.restype = i64

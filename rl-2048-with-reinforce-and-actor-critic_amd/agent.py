@@ -636,7 +636,7 @@ class ReinforceAgent:
                                                   scale, use_mask, L.ptr(b), L.ptr(acts), L.ptr(coef), int(critic),
                                                   loss, float(c.huber_delta), L.ptr(tgt),
                                                   L.ptr(deltas[k, s0:s0 + m]) if critic else None, None, L.ptr(d0),
-                                                  m, L.ptr(part), nparts, self._stream))
+                                                  m, L.ptr(part), nparts, None, self._stream))
                 self._fold(part, acc)
                 if onehot:
                     self._onehot_dw1_into(b, d0, acc1, h1=h0)
@@ -654,6 +654,13 @@ class ReinforceAgent:
             gb[l] += acc[pb[l]:pb[l] + Hp[l]][:hidden[l]]
         gW[nh] += acc[pw[nh]:pw[nh] + Hp[-1] * 4].view(Hp[-1], 4)[:hidden[-1], :out_dim]
         gb[nh] += acc[pb[nh]:pb[nh] + 4][:out_dim]
+
+    def _td_rows(self, steps: "_Steps", hn_f: torch.Tensor, s0: int, cnt: int, v_next: torch.Tensor,
+                 v_out: torch.Tensor):
+        """g2048_td_rows of time row [s0, s0 + cnt): the kernel forms r + (gamma V(s')) m from the later row's
+        lane-indexed values v_next and writes this row's V(s) by lane into v_out (src/reinforce_agent.py:423-443)."""
+        return L.TdRows(L.ptr(steps.lane[s0:s0 + cnt]), L.ptr(steps.rewards[s0:s0 + cnt]), L.ptr(hn_f[s0:s0 + cnt]),
+                        L.ptr(v_next), L.ptr(v_out), float(self.agent_config.gamma), 0)
 
     def _deep_critic_rows(self, params, dspec, steps: "_Steps", K: int, gW: list[torch.Tensor],
                           gb: list[torch.Tensor], step_w: torch.Tensor, deltas: torch.Tensor) -> None:
@@ -701,7 +708,7 @@ class ReinforceAgent:
         allb = steps.boards.reshape(-1)[steps.vidx].contiguous()     # the steps' boards, gathered once
         hn_f = steps.has_next.to(torch.float32)
 
-        def launch(s0: int, cnt: int, tgt: torch.Tensor, k: int) -> None:
+        def launch(s0: int, cnt: int, tgt, k: int, td=None) -> None:
             nonlocal used
             b = allb[s0:s0 + cnt]
             if k:
@@ -712,7 +719,8 @@ class ReinforceAgent:
             L.check(self._lib.g2048_deep_grad(L.ptr(packed), L.ptr(bpacked), len(hidden), harr, act, obs_code, scale,
                                               0, L.ptr(b), None, L.ptr(step_w[s0:s0 + cnt]), 1, loss,
                                               float(c.huber_delta), L.ptr(tgt), L.ptr(deltas[k, s0:s0 + cnt]),
-                                              L.ptr(vout), L.ptr(d0), cnt, L.ptr(part), nparts, self._stream))
+                                              L.ptr(vout), L.ptr(d0), cnt, L.ptr(part), nparts,
+                                              ctypes.byref(td) if td is not None else None, self._stream))
             self._fold(part, acc)
             if onehot:
                 bbuf[used:used + cnt] = b
@@ -733,10 +741,7 @@ class ReinforceAgent:
                 if cnt == 0:
                     continue
                 s0 = starts[t]
-                lanes = steps.lane[s0:s0 + cnt]
-                tgt = vb[(t + 1) & 1].index_select(0, lanes).mul_(gamma).mul_(hn_f[s0:s0 + cnt])
-                launch(s0, cnt, tgt.add_(steps.rewards[s0:s0 + cnt]), k)
-                vb[t & 1].index_copy_(0, lanes, vout[:cnt])
+                launch(s0, cnt, None, k, td=self._td_rows(steps, hn_f, s0, cnt, vb[(t + 1) & 1], vb[t & 1]))
         flush_d0()
         pw, pb = self._deep_slab_layout(hidden, onehot)
         Hp = [_round32(h) for h in hidden]
@@ -886,7 +891,7 @@ class ReinforceAgent:
             L.check(self._lib.g2048_critic_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, loss,
                                                 float(c.huber_delta), L.ptr(b), L.ptr(tgt), L.ptr(w),
                                                 L.ptr(deltas[k, s0:s0 + m]), None, m, ld, 0, ld, L.ptr(a1t),
-                                                L.ptr(d2t), L.ptr(part), 0, waves, 0, self._stream))
+                                                L.ptr(d2t), L.ptr(part), 0, waves, 0, None, self._stream))
 
         if self._critic_by_rows(steps):
             self._critic_grad_rows(steps, step_w, K, gW, gb, deltas, spec)
@@ -983,7 +988,7 @@ class ReinforceAgent:
         allb = flat[steps.vidx].contiguous()
         hn_f = steps.has_next.to(torch.float32)
 
-        def grad_launch(s0: int, cnt: int, tgt: torch.Tensor, k: int) -> None:
+        def grad_launch(s0: int, cnt: int, tgt, k: int, td=None) -> None:
             nonlocal col, since_fold
             b = allb[s0:s0 + cnt]
             if k:
@@ -995,7 +1000,8 @@ class ReinforceAgent:
             L.check(self._lib.g2048_critic_grad(L.ptr(packed), L.ptr(gpacked), h1, h2, act, obs_code, scale, loss,
                                                 float(c.huber_delta), L.ptr(b), L.ptr(tgt), L.ptr(step_w[s0:s0 + cnt]),
                                                 L.ptr(deltas[k, s0:s0 + cnt]), L.ptr(vout), cnt, ld, col, ncols,
-                                                L.ptr(a1t), L.ptr(d2t), L.ptr(part), 1, waves, int(fac), self._stream))
+                                                L.ptr(a1t), L.ptr(d2t), L.ptr(part), 1, waves, int(fac),
+                                                ctypes.byref(td) if td is not None else None, self._stream))
             launched.append((k, s0, cnt, col))
             col += ncols
             since_fold += 1
@@ -1029,12 +1035,9 @@ class ReinforceAgent:
                 if cnt == 0:
                     continue
                 s0 = starts[t]
-                lanes = steps.lane[s0:s0 + cnt]
-                # r + (gamma V(s')) m, the same roundings as the chunked path, in three in-place kernels
-                tgt = vb[(t + 1) & 1].index_select(0, lanes).mul_(gamma).mul_(hn_f[s0:s0 + cnt])
-                tgt.add_(steps.rewards[s0:s0 + cnt])
-                grad_launch(s0, cnt, tgt, k)
-                vb[t & 1].index_copy_(0, lanes, vout[:cnt])
+                # r + (gamma V(s')) m in the kernel from the lane-indexed values of row t + 1 (g2048_td_rows; the
+                # same roundings as the chunked path), its V(s) written by lane for row t - 1
+                grad_launch(s0, cnt, None, k, td=self._td_rows(steps, hn_f, s0, cnt, vb[(t + 1) & 1], vb[t & 1]))
         flush(col)
         small = small.to(torch.float32)
         big = big.to(torch.float32)

@@ -868,6 +868,8 @@ struct DeepGradArgs {
     float* delta_out;             // critic: target - V (NULL ok)
     float* v_out;                 // critic: V (NULL ok)
     float* d0_out;                // one-hot: delta_0 [n][H0p] for g2048_onehot_dw1
+    g2048_td_rows td;             // has_td: the critic's target and V(s) through lane-indexed values
+    int has_td;
     float* part;                  // [gridDim.x][pslab]
     float obs_scale;
     uint32_t n;
@@ -952,7 +954,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         // the sample's coefficient / action / target, loaded now so that the forward covers their latency
         const float cf = (tid < 32 && valid) ? a.coef[jc] : 0.0f;
         const uint32_t act_j = (tid < 32 && !a.critic) ? a.actions[jc] : 0u;
-        const float tg = (tid < 32 && a.critic) ? a.target[jc] : 0.0f;
+        const float tg = (tid < 32 && a.critic)
+                             ? (a.has_td ? ((a.td.v_next[a.td.lane[jc]] * a.td.gamma) * a.td.has_next[jc]) + a.td.reward[jc]
+                                         : a.target[jc])
+                             : 0.0f;
         __syncthreads();
         DEEP_STAMP(0);
         // ---- forward: layer 0
@@ -1059,7 +1064,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 g[0] = gd * cf;
                 g[1] = g[2] = g[3] = 0.0f;
                 if (valid && a.delta_out) a.delta_out[j] = tg - lg[0];
-                if (valid && a.v_out) a.v_out[j] = lg[0];
+                if (valid) {
+                    if (a.has_td) a.td.v_out[a.td.lane[j]] = lg[0];
+                    else if (a.v_out) a.v_out[j] = lg[0];
+                }
             }
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -1875,7 +1883,7 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
                     int activation, int obs_mode, float obs_scale, int use_mask, const uint64_t* boards,
                     const uint8_t* actions, const float* coef, int critic, int loss, float huber_delta,
                     const float* target, float* delta_out, float* value_out, float* d0_out, int64_t n,
-                    float* partials, int64_t nparts, void* stream) {
+                    float* partials, int64_t nparts, const g2048_td_rows* td, void* stream) {
     if (n < 0 || n > (int64_t)0x7FFFFFE0) return dfail(G2048_EINVAL, "n out of range");
     if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
         return dfail(G2048_EINVAL, "Unsupported activation");
@@ -1884,8 +1892,10 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
                                    "64 dense 32x32 weight-gradient tiles)");
     if (critic && loss != 0 && loss != 1) return dfail(G2048_EINVAL, "Unknown critic loss type");
     if (!packed || !partials || (n > 0 && (!boards || !coef)) || (n > 0 && !critic && !actions) ||
-        (n > 0 && critic && !target) || (n > 0 && obs_mode == G2048_OBS_ONEHOT && !d0_out))
+        (n > 0 && critic && !target && !td) || (n > 0 && obs_mode == G2048_OBS_ONEHOT && !d0_out))
         return dfail(G2048_EINVAL, "deep gradient: NULL buffer");
+    if (td && (!critic || (n > 0 && (!td->lane || !td->reward || !td->has_next || !td->v_next || !td->v_out))))
+        return dfail(G2048_EINVAL, "deep gradient: TD rows are for the critic, with every buffer set");
     if (nparts < 1 || nparts > 65535) return dfail(G2048_EINVAL, "deep gradient: nparts out of range");
     DeepNet net;
     deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, net);
@@ -1920,6 +1930,8 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
     a.delta_out = delta_out;
     a.v_out = value_out;
     a.d0_out = d0_out;
+    a.has_td = td != nullptr;
+    if (td) a.td = *td;
     a.part = partials;
     a.obs_scale = obs_scale;
     a.n = (uint32_t)n;

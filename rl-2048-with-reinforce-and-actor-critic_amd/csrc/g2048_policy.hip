@@ -678,6 +678,8 @@ struct GradArgs {
     const float* target;     // [n]
     float* delta_out;        // [n] or NULL
     float* v_out;            // [n] or NULL: V(s) of each sample (critic mode)
+    g2048_td_rows td;        // has_td: target and V(s) through the lane-indexed value buffers (g2048_td_rows)
+    int has_td;
     // column window: sample j's a1^T / d2^T column is col_off + j; groups of 32 processed: ngroups (columns
     // col_off .. col_off + 32 ngroups - 1; those past n are written as zero-coefficient padding)
     uint32_t col_off, ngroups;
@@ -685,6 +687,13 @@ struct GradArgs {
     int d2_form;             // 1 (critic, ReLU) / 2 (actor, ReLU): d2t receives one 1 KiB record per 16-column block
                              // instead of d2 columns (include/g2048.h; the FAC kernel variants)
 };
+
+// the critic's TD target of sample j: given, or r + (gamma V(s')) m from the lane-indexed values (g2048_td_rows; the
+// host's fp32 operation order -- the TU is built with -ffp-contract=off, so nothing fuses)
+__device__ __forceinline__ float td_target(const GradArgs& a, uint32_t j) {
+    if (!a.has_td) return a.target[j];
+    return ((a.td.v_next[a.td.lane[j]] * a.td.gamma) * a.td.has_next[j]) + a.td.reward[j];
+}
 
 template <int NT1, int NT2>
 struct GradSmem {
@@ -905,13 +914,16 @@ __global__ void __launch_bounds__(kPolBlock, 1) grad_kernel(GradArgs a) {
             for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf;
         } else {
             // ---- the critic's value-loss gradient (update_batch :403-498, _get_grad_logits_critic :884-910)
-            const float tg = valid ? a.target[j] : 0.0f;
+            const float tg = valid ? td_target(a, j) : 0.0f;
             const float diff = lg[0] - tg;
             const float gd = (a.huber && fabsf(diff) > a.huber_delta) ? copysignf(a.huber_delta, diff) : diff;
             g[0] = gd * cf;
             g[1] = g[2] = g[3] = 0.0f;
             if (valid && h == 0 && a.delta_out) a.delta_out[j] = tg - lg[0];
-            if (valid && h == 0 && a.v_out) a.v_out[j] = lg[0];
+            if (valid && h == 0) {
+                if (a.has_td) a.td.v_out[a.td.lane[j]] = lg[0];
+                else if (a.v_out) a.v_out[j] = lg[0];
+            }
         }
         lds_fence();   // the previous group's reads of S.g are done
         if (h == 0) {
@@ -1307,13 +1319,16 @@ __global__ void __launch_bounds__(kPolBlock, 2) grad_coop_kernel(GradArgs a) {
 #pragma unroll
             for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf;
         } else {
-            const float tg = valid ? a.target[j] : 0.0f;
+            const float tg = valid ? td_target(a, j) : 0.0f;
             const float diff = lg[0] - tg;
             const float gd = (a.huber && fabsf(diff) > a.huber_delta) ? copysignf(a.huber_delta, diff) : diff;
             g[0] = gd * cf;
             g[1] = g[2] = g[3] = 0.0f;
             if (valid && w == 0 && h == 0 && a.delta_out) a.delta_out[j] = tg - lg[0];
-            if (valid && w == 0 && h == 0 && a.v_out) a.v_out[j] = lg[0];
+            if (valid && w == 0 && h == 0) {
+                if (a.has_td) a.td.v_out[a.td.lane[j]] = lg[0];
+                else if (a.v_out) a.v_out[j] = lg[0];
+            }
         }
         if (h == 0) {
 #pragma unroll
@@ -1724,7 +1739,8 @@ static int actor_or_critic_grad(const float* packed, const float* grad_packed, i
                          float obs_scale, int use_mask, const uint64_t* boards, const uint8_t* actions,
                          const float* coef, int64_t n, int64_t ld, int64_t col_off, int64_t ncols, float* a1t, float* d2t,
                          float* partials, int accumulate, int64_t waves, void* stream, int critic, int huber,
-                         float huber_delta, const float* target, float* delta_out, float* v_out, int d2_form = 0) {
+                         float huber_delta, const float* target, float* delta_out, float* v_out, int d2_form = 0,
+                         const g2048_td_rows* td = nullptr) {
     if (n < 0 || ld < n || (ld & 31) || ld > ((int64_t)1 << 21)) return pfail(G2048_EINVAL, "fused gradient: bad n / ld");
     if (col_off < 0 || (col_off & 31) || ncols < n || (ncols & 31) || col_off + ncols > ld)
         return pfail(G2048_EINVAL, "fused gradient: bad column window (col_off / ncols multiples of 32, n <= ncols, "
@@ -1759,6 +1775,8 @@ static int actor_or_critic_grad(const float* packed, const float* grad_packed, i
     a.target = target;
     a.delta_out = delta_out;
     a.v_out = v_out;
+    a.has_td = td != nullptr;
+    a.td = td ? *td : g2048_td_rows{};
     a.col_off = (uint32_t)col_off;
     a.ngroups = (uint32_t)(ncols >> 5);
     a.part_accum = accumulate;
@@ -1791,12 +1809,14 @@ int g2048_critic_grad(const float* packed, const float* grad_packed, int h1, int
                       float obs_scale, int loss, float huber_delta, const uint64_t* boards, const float* target,
                       const float* weight, float* delta_out, float* value_out, int64_t n, int64_t ld, int64_t col_off,
                       int64_t ncols, float* a1t, float* d2t, float* partials, int accumulate, int64_t waves,
-                      int d2_form, void* stream) {
+                      int d2_form, const g2048_td_rows* td, void* stream) {
     if (loss != 0 && loss != 1) return pfail(G2048_EINVAL, "Unknown critic loss type");
-    if (n > 0 && !target) return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
+    if (n > 0 && !target && !td) return pfail(G2048_EINVAL, "fused gradient: NULL buffer");
+    if (td && n > 0 && (!td->lane || !td->reward || !td->has_next || !td->v_next || !td->v_out))
+        return pfail(G2048_EINVAL, "fused gradient: NULL TD-row buffer");
     return actor_or_critic_grad(packed, grad_packed, h1, h2, activation, obs_mode, obs_scale, 0, boards, nullptr, weight,
                                 n, ld, col_off, ncols, a1t, d2t, partials, accumulate, waves, stream, 1, loss,
-                                huber_delta, target, delta_out, value_out, d2_form);
+                                huber_delta, target, delta_out, value_out, d2_form, td);
 }
 
 int g2048_rollout(const float* packed, int h1, int h2, int activation, const g2048_env_cfg* cfg, int greedy,

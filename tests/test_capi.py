@@ -124,7 +124,7 @@ def test_argument_validation_without_gpu(L):
     gargs[12], gargs[5] = 64, L.OBS_ONEHOT
     assert lib.g2048_actor_grad(*gargs) == L.G2048_EINVAL and b"obs_mode" in lib.g2048_last_error()
     cargs = [p, p, 32, 32, L.ACT_RELU, L.OBS_LOG2, 1.0, 2, 1.0, p, p, p, None, None, 40, 128, 0, 64, p, p, p, 0, 1024,
-             0, None]
+             0, None, None]
     assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"critic loss" in lib.g2048_last_error()
     cargs[7] = 0
     for col_off, ncols in ((16, 64), (0, 32), (96, 64), (-32, 64)):   # unaligned, < n, past ld, negative
@@ -135,6 +135,15 @@ def test_argument_validation_without_gpu(L):
     assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"factored" in lib.g2048_last_error()
     cargs[4], cargs[23] = L.ACT_RELU, 2
     assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"factored" in lib.g2048_last_error()
+    # in-kernel TD targets (g2048_td_rows, ABI 14): every buffer required; the deep kernel takes them for the critic only
+    td = L.TdRows(8, 8, 8, None, 8, 0.99, 0)
+    cargs[4], cargs[23], cargs[10], cargs[24] = L.ACT_RELU, 0, None, ctypes.byref(td)
+    assert lib.g2048_critic_grad(*cargs) == L.G2048_EINVAL and b"TD-row" in lib.g2048_last_error()
+    td.v_next = 8
+    hs2 = (ctypes.c_int32 * 2)(64, 32)
+    gd = [p, p, 2, hs2, L.ACT_RELU, L.OBS_LOG2, 1.0, 0, p, p, p, 0, 0, 1.0, None, None, None, None, 10, p, 4,
+          ctypes.byref(td), None]
+    assert lib.g2048_deep_grad(*gd) == L.G2048_EINVAL and b"TD rows are for the critic" in lib.g2048_last_error()
     dargs = [p, p, None, 32, 32, 64, 0, 64, 64, p, 1, None]   # factored dW2 without W3
     assert lib.g2048_dw2_factored(*dargs) == L.G2048_EINVAL and b"NULL" in lib.g2048_last_error()
 
