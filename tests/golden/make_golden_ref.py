@@ -1,6 +1,7 @@
 """Generate env / agent / runner fixtures from the REAL reference (build container only).
 
     python tests/golden/make_golden_ref.py [--ref /root/reference] [--only env,obs,sym,update,small,runner]
+                                           [--update-from K]   (append update cases K.. to update.npz)
 
 Imports the reference's own modules -- src/env.py, src/reinforce_agent.py, src/MLP.py, src/utils/*, runner.py --
 by package path from ``--ref`` with ``sys.dont_write_bytecode`` set (nothing is written into the reference tree).
@@ -287,6 +288,12 @@ def _update_cases():
             hidden_sizes=[64, 32], activation="ReLU", init_distribution="HeNormal", last_init_normal=True),
             agent=dict(gamma=0.99, learning_rate=1e-2, baseline_mode="batch", augmentation=True, use_critic=True,
                        model_seed=112), n=4),
+        # round 5: a one-hot [256, 256] actor-critic -- 64 dense 32x32 weight-gradient tiles, the largest net
+        # g2048_deep_grad holds in registers (its 8-wave, 8-tiles-per-wave instantiation)
+        dict(name="onehot-relu-256x256-critic-adam", env=dict(ENV_B, obs_mode="onehot", max_steps=300), mlp=dict(
+            hidden_sizes=[256, 256], activation="ReLU", init_distribution="HeNormal", last_init_normal=True),
+            agent=dict(gamma=0.99, learning_rate=1e-3, baseline_mode="batch", optimizer="adam", use_critic=True,
+                       critic_learning_rate=1e-3, model_seed=113), n=4, updates=1),
     ]
     for e in extra:
         e.setdefault("n", 6)
@@ -392,10 +399,21 @@ def run_update_case(E, RA, M, case, ci):
     return out
 
 
-def gen_update(E, RA, M):
+def gen_update(E, RA, M, start: int = 0):
+    """All update cases, or (start > 0) only cases start.. appended to the existing update.npz, whose first `start`
+    cases must be the current list's (their arrays are kept as they are)."""
     cases = _update_cases()
     data = {"cases": np.array(json.dumps(cases))}
+    if start:
+        with np.load(os.path.join(HERE, "update.npz")) as z:
+            old = json.loads(str(z["cases"]))
+            assert old[:start] == json.loads(json.dumps(cases[:start])), "existing cases differ from the list"
+            for k in z.files:
+                if k != "cases" and int(k[1:k.index("_")]) < start:
+                    data[k] = z[k]
     for ci, case in enumerate(cases):
+        if ci < start:
+            continue
         data.update(run_update_case(E, RA, M, case, ci))
         print(f"  update case {ci} {case['name']}: "
               f"{[int(data[f'u{ci}_up{u}_lengths'].sum()) for u in range(case['updates'])]} steps")
@@ -504,9 +522,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--only", default="")
+    ap.add_argument("--update-from", type=int, default=0, help="append update cases from this index on")
     a = ap.parse_args()
     E, RA, M = import_reference(a.ref)
-    jobs = dict(env=gen_env, obs=gen_obs, sym=gen_sym, update=gen_update, small=gen_small)
+    jobs = dict(env=gen_env, obs=gen_obs, sym=gen_sym, update=lambda E_, RA_, M_: gen_update(E_, RA_, M_, a.update_from),
+                small=gen_small)
     for name, fn in jobs.items():
         if a.only and name not in a.only.split(","):
             continue

@@ -314,7 +314,9 @@ def test_deep_rollout_suspend_resume_equals_stepwise(env, hidden):
 @pytest.mark.parametrize("env,hidden,act,critic", [(REFCONF_ENV, [256, 128, 64], "ReLU", True),
                                                    (dict(REFCONF_ENV, max_steps=200), [40, 33, 20, 10], "Sigmoid", False),
                                                    (dict(obs_mode="log2", obs_log2_scale=0.0625, max_steps=None),
-                                                    [64, 48, 32], "ReLU", True)])
+                                                    [64, 48, 32], "ReLU", True),
+                                                   # round 5: 64 dense tiles (the 8-wave, 8-tiles-per-wave kernel)
+                                                   (REFCONF_ENV, [256, 256], "ReLU", True)])
 def test_deep_update_at_size_vs_fp64(env, hidden, act, critic, fused, rows):
     """update_from_batch on nets the register-specialised kernels do not cover (the reference runner's documented
     config first: one-hot obs, 256-128-64, actor-critic) over 16,384 episodes of its own rollout: the pre-clip
