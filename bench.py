@@ -508,7 +508,7 @@ def main():
     # kernel run 10-30 % slower, profiles/round3/step_cold_trace.log); the headline env below starts from the
     # synthetic random-state boards untouched.
     warm = {"launches": 0, "seconds": 0.0}
-    if args.chip_warmup_seconds > 0 and not args.trace_steps:
+    if args.chip_warmup_seconds > 0:
         wenv = make_env(torch, args, B, rank * B, device)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -531,8 +531,12 @@ def main():
             torch.cuda.synchronize()
             rf = float(((env.flags & L.F_RESET) != 0).float().mean())
             act = float(env.active.float().mean())
+            inv = float(((env.flags & L.F_INVALID) != 0).float().mean())
+            tiles = float(((((env.board.unsqueeze(1) >> torch.arange(0, 64, 4, device=device)) & 15) != 0)
+                           .float().sum(1)).mean())
             print(json.dumps({"step": k, "us": round(s_.elapsed_time(e_) * 1e3, 2), "reset_frac": round(rf, 5),
-                              "active_frac": round(act, 4)}), flush=True)
+                              "active_frac": round(act, 4), "invalid_frac": round(inv, 4),
+                              "tiles_per_board": round(tiles, 2)}), flush=True)
         return
     for k in range(W):
         env.step_into(actions[k])

@@ -433,6 +433,12 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     return m;
 }
 
+// G2048_STEP_SEED (tools/ A/B builds only): 0 = a lane's first pending reset reads its seed inside the sweep, behind
+// the lane's reset test (shipped); 1 = every lane issues that read (lanes without a new reset re-read lane w0's seed),
+// so the sweep's vector-memory count is the same on every path
+#ifndef G2048_STEP_SEED
+#define G2048_STEP_SEED 0
+#endif
 // One sweep of one wave: the step of board w0 + lane (inputs already in registers), its mask, the wave's obs.
 // A lane's first pending reset has its seed read here (`pseed`), so the read is long complete at the tail.
 template <int OBS, int RNG, int XO, int RK>
@@ -443,6 +449,20 @@ __device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, 
     uint32_t mbits = 0;
     uint64_t b = 0;
     if (i < a.n) b = step_lane<RNG, XO, RK>(a, i, x, lut, code, wobs, reset, mbits);
+#if G2048_STEP_SEED == 1   // A/B: the seed read issued by every lane (non-resetting lanes re-read lane w0's line)
+    if constexpr (RNG == G2048_RNG_PCG64) {
+        const uint64_t sd = ld(a.L.seed, (reset && !pending) ? i : (w0 < a.n ? w0 : a.n - 1u));
+        if (reset) {
+            if (!pending) pseed = sd;
+            pending |= 1ull << k;
+        }
+    } else {
+        if (reset) {
+            if (!pending) pseed = x.seed;
+            pending |= 1ull << k;
+        }
+    }
+#else
     if (reset) {
         if (!pending) {
             if constexpr (RNG == G2048_RNG_PCG64) pseed = ld(a.L.seed, i);
@@ -450,6 +470,7 @@ __device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, 
         }
         pending |= 1ull << k;
     }
+#endif
     if constexpr (XO == 3) {
         if (wobs) st(a.out.mask_bits, i, (uint8_t)mbits);
     } else {
