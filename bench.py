@@ -96,19 +96,26 @@ def parse():
 
 
 # ---------------------------------------------------------------------------------------------- inputs
-def synthetic_boards(torch, B: int, lane_offset: int, device, seed: int = 0x2048):
+def synthetic_boards(torch, B: int, lane_offset: int, device, seed: int = 0x2048, chunk: int = 1 << 16):
     """Random-state boards: cell empty w.p. 6/16, else exponent uniform over 1..12.
-    A counter hash of (global lane, cell) so shards of an N-GPU run are slices of the 1-GPU global batch."""
+    A counter hash of (global lane, cell) so shards of an N-GPU run are slices of the 1-GPU global batch.
+    Built in chunks of 65,536 boards: the whole-batch form made ~10 temporaries of 128 MiB (16 cells x 1M int64)
+    whose traffic evicted the step kernel's working set from the 256 MB Infinity Cache (MALL) right before the timed
+    launches, which then ran ~2.5 us slower until the working set was back (tools/step_launch_probe.py, round 5)."""
     M = 0x7FFFFFFFFFFFFFFF
-    idx = (torch.arange(B * 16, dtype=torch.int64, device=device) + lane_offset * 16) ^ seed
-    h = idx * -0x61C8864680B583EB - 0x61C8864680B583EB  # splitmix64 (0x9E3779B97F4A7C15 as int64), wraps
-    h = (h ^ ((h >> 30) & (M >> 29))) * -0x40A7B892E31B1A47
-    h = (h ^ ((h >> 27) & (M >> 26))) * -0x6B2FB644ECCEEE15
-    h = h ^ ((h >> 31) & (M >> 30))
-    u = h & 0xFFFF
-    exps = torch.where((u & 15) < 6, torch.zeros_like(u), 1 + ((u >> 4) % 12)).view(B, 16)
+    out = torch.empty(B, dtype=torch.int64, device=device)
     shifts = torch.arange(0, 64, 4, dtype=torch.int64, device=device)
-    return (exps << shifts).sum(dim=1)
+    for c0 in range(0, B, chunk):
+        n = min(chunk, B - c0)
+        idx = (torch.arange(n * 16, dtype=torch.int64, device=device) + (lane_offset + c0) * 16) ^ seed
+        h = idx * -0x61C8864680B583EB - 0x61C8864680B583EB  # splitmix64 (0x9E3779B97F4A7C15 as int64), wraps
+        h = (h ^ ((h >> 30) & (M >> 29))) * -0x40A7B892E31B1A47
+        h = (h ^ ((h >> 27) & (M >> 26))) * -0x6B2FB644ECCEEE15
+        h = h ^ ((h >> 31) & (M >> 30))
+        u = h & 0xFFFF
+        exps = torch.where((u & 15) < 6, torch.zeros_like(u), 1 + ((u >> 4) % 12)).view(n, 16)
+        out[c0:c0 + n] = (exps << shifts).sum(dim=1)
+    return out
 
 
 def make_env(torch, args, B, lane_offset, device):

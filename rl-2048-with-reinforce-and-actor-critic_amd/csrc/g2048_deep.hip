@@ -264,7 +264,10 @@ __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, co
 // agree bit for bit; the halves' items keep the idle waves of a 2- or 4-tile layer busy.  The second half's chain
 // is parked in the output tile's own LDS cells until the first half adds it (one barrier inside).  The rollout /
 // policy kernels keep the single chain (their layers are already spread over their 4 waves).
-template <int ACT, int NW>
+// MODE 1 (the 8-wave gradient kernels): split when ntout < 8 (and ntin >= 2); MODE 2 (the 4-wave one): split only
+// when the two halves of every output tile give each of the 4 waves at most one item (2 ntout <= 4) -- the 64-unit
+// layer of [256, 128, 64] -- so a wave keeps one chain in registers.
+template <int ACT, int NW, int MODE = 1>
 __device__ __forceinline__ void dense_fwd_split(const float* in, float* out, const float4* __restrict__ frag,
                                                 const float* bias, int ntin, int ntout, int w) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
@@ -280,13 +283,14 @@ __device__ __forceinline__ void dense_fwd_split(const float* in, float* out, con
 #pragma unroll
         for (int r = 0; r < 16; r++) *cell(o, r) = activate<ACT>(c[r] + bv[r]);
     };
-    if (!(ntout < 8 && ntin >= 2)) {
+    const bool split = ntin >= 2 && (MODE == 1 ? ntout < 8 : 2 * ntout <= 4);
+    if (!split) {
         for (int o = w; o < ntout; o += NW) finish(o, chain(o, 0, ntin));
         return;
     }
     const int kh = ntin >> 1;
-    constexpr int kKeep = (7 + NW - 1) / NW;       // first-half items per wave (ntout <= 7)
-    constexpr int kSecond = (14 + NW - 1) / NW;    // item slots per wave that may hold a second half
+    constexpr int kKeep = MODE == 1 ? (7 + NW - 1) / NW : 1;      // first-half items per wave
+    constexpr int kSecond = MODE == 1 ? (14 + NW - 1) / NW : 1;   // item slots per wave that may hold a second half
     floatx16 c0[kKeep];
 #pragma unroll
     for (int r = 0; r < kKeep; r++) {
@@ -449,7 +453,7 @@ __device__ __forceinline__ void load_l0_block(const float* __restrict__ a0, uint
 
 // KSPLIT: the dense layers by dense_fwd_split (the gradient kernel's forward, for the pattern probe).  A0IN (one-hot,
 // the probe): layer 0 from onehot_l0_mfma_kernel's block of group gi (a0) -- the update's layer-0 bits.
-template <int OBS, int ACT, bool KSPLIT = false, bool A0IN = false>
+template <int OBS, int ACT, int KSPLIT = 0, bool A0IN = false>
 __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, DeepSmem& S, float obs_scale,
                              const float* a0 = nullptr, uint32_t n = 0, uint32_t gi = 0) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
@@ -511,8 +515,8 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
         const int ntin = net.nt[l - 1], ntout = net.nt[l];
         const float4* __restrict__ frag = reinterpret_cast<const float4*>(P + net.w[l]) + lane;
         const float* bias = P + net.b[l];
-        if constexpr (KSPLIT) {
-            dense_fwd_split<ACT, kDeepBlock / 64>(in, out, frag, bias, ntin, ntout, w);
+        if constexpr (KSPLIT != 0) {
+            dense_fwd_split<ACT, kDeepBlock / 64, KSPLIT>(in, out, frag, bias, ntin, ntout, w);
             __syncthreads();
             continue;
         }
@@ -640,7 +644,7 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_policy_kernel(DeepPolArgs 
 // are unused): out[j * ld + u] for u < 32 nt[layer] -- bit for bit what deep_grad_kernel computes (dense layers by
 // dense_fwd_split when the net's gradient instantiation splits k, else deep_forward's chain), for tests that impose
 // the gradient kernel's own activation pattern on an fp64 evaluation.
-template <int OBS, int ACT, bool KSPLIT, bool A0IN>
+template <int OBS, int ACT, int KSPLIT, bool A0IN>
 __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net, const float* packed,
                                                                      const uint64_t* boards, uint32_t n, float obs_scale,
                                                                      float* out, uint32_t ld, const float* a0) {
@@ -848,6 +852,10 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArg
 //     accumulator registers per wave.
 // (A 4-wave workgroup alone per CU with 12 tiles per wave took the whole register file, one wave per SIMD.)
 constexpr int kDeepGradMaxBlock = 512;
+// the 4-wave instantiation's k-split of its 64-unit layer (dense_fwd_split MODE 2): 1 on, 0 off (A/B builds)
+#ifndef G2048_DEEP_SPLIT4
+#define G2048_DEEP_SPLIT4 0
+#endif
 struct DeepGradVariant {
     int nw, tpw, ksplit, per_cu;
 };
@@ -904,7 +912,7 @@ __device__ __forceinline__ float act_deriv(float a) {   // from the activation (
     else return a * (1.0f - a);
 }
 
-template <int OBS, int ACT, int NW, int TPW, bool KSPLIT>
+template <int OBS, int ACT, int NW, int TPW, int KSPLIT>
 __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs a) {
     constexpr int kBlock = 64 * NW;
     extern __shared__ float dyn[];
@@ -954,10 +962,19 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         // the sample's coefficient / action / target, loaded now so that the forward covers their latency
         const float cf = (tid < 32 && valid) ? a.coef[jc] : 0.0f;
         const uint32_t act_j = (tid < 32 && !a.critic) ? a.actions[jc] : 0u;
-        const float tg = (tid < 32 && a.critic)
-                             ? (a.has_td ? ((a.td.v_next[a.td.lane[jc]] * a.td.gamma) * a.td.has_next[jc]) + a.td.reward[jc]
-                                         : a.target[jc])
-                             : 0.0f;
+        // the critic's target, or (TD rows) its reward / has-next / lane now and V(s') once layer 0 is done (the
+        // lane index has arrived by then: no dependent load in front of the first barrier)
+        float tg = 0.0f, td_r = 0.0f, td_h = 0.0f, td_v = 0.0f;
+        int64_t td_l = 0;
+        if (tid < 32 && a.critic) {
+            if (a.has_td) {
+                td_l = a.td.lane[jc];
+                td_r = a.td.reward[jc];
+                td_h = a.td.has_next[jc];
+            } else {
+                tg = a.target[jc];
+            }
+        }
         __syncthreads();
         DEEP_STAMP(0);
         // ---- forward: layer 0
@@ -990,14 +1007,15 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         }
         __syncthreads();
         DEEP_STAMP(1);
+        if (tid < 32 && a.critic && a.has_td) td_v = a.td.v_next[td_l];
         // ---- forward: dense layers (each into its own region)
         for (int l = 1; l < L; l++) {
             const float* in = actl(l - 1);
             float* out = actl(l);
             const int ntin = net.nt[l - 1], ntout = net.nt[l];
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(P + net.w[l]) + lane;
-            if constexpr (KSPLIT) {
-                dense_fwd_split<ACT, NW>(in, out, frag, P + net.b[l], ntin, ntout, w);
+            if constexpr (KSPLIT != 0) {
+                dense_fwd_split<ACT, NW, KSPLIT>(in, out, frag, P + net.b[l], ntin, ntout, w);
             } else {   // deep_forward's chain: the rollout / policy kernels' bits
                 for (int o = w; o < ntout; o += NW) {
                     const floatx16 c = frag_chain(frag + (int64_t)o * ntin * 256, in, 0, ntin, h, col);
@@ -1059,6 +1077,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf;
             } else {
                 // the critic's value-loss gradient (update_batch :403-498, _get_grad_logits_critic :884-910)
+                if (a.has_td) tg = ((td_v * a.td.gamma) * td_h) + td_r;   // the host's fp32 operation order
                 const float diff = lg[0] - tg;
                 const float gd = (a.huber && fabsf(diff) > a.huber_delta) ? copysignf(a.huber_delta, diff) : diff;
                 g[0] = gd * cf;
@@ -1335,7 +1354,7 @@ int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, 
 // of 10 or 8 dense tiles per wave, hipcc spills whole accumulator tiles (~300-650 VGPRs).
 DeepGradVariant deep_grad_variant(const DeepNet& n) {
     const int tiles = deep_grad_layout(n).ntiles;
-    if (n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024) return {4, 10, 0, 2};
+    if (n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024) return {4, 10, G2048_DEEP_SPLIT4 ? 2 : 0, 2};
     if (tiles <= 48 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 6, 1, 1};
     if (n.onehot && tiles <= 64 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 8, 1, 1};
     return {0, 0, 0, 0};
@@ -1759,7 +1778,7 @@ int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, 
         return dfail(G2048_EINVAL, "Unsupported activation");
     if (!packed || (n > 0 && (!boards || !out))) return dfail(G2048_EINVAL, "deep hidden: NULL buffer");
     if (n == 0) return G2048_OK;
-    const bool ksplit = deep_grad_variant(net).ksplit != 0;   // the full net's gradient instantiation
+    const int ksplit = deep_grad_variant(net).ksplit;   // the full net's gradient instantiation's k-split rule
     hipStream_t s = (hipStream_t)stream;
     float* a0 = nullptr;   // one-hot: the update's layer 0 (onehot_l0_mfma_kernel) in a scratch buffer
     if (obs_mode == G2048_OBS_ONEHOT) {
@@ -1773,11 +1792,14 @@ int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, 
     const int grid = (int)(groups < cap ? groups : cap);
 #define G2048_HIDDEN(O, A, A0)                                                                                      \
     do {                                                                                                            \
-        if (ksplit)                                                                                                 \
-            hipLaunchKernelGGL((deep_hidden_kernel<O, A, true, A0>), dim3(grid), dim3(kDeepBlock), 0, s, net,       \
+        if (ksplit == 1)                                                                                            \
+            hipLaunchKernelGGL((deep_hidden_kernel<O, A, 1, A0>), dim3(grid), dim3(kDeepBlock), 0, s, net,          \
+                               packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld, a0);                      \
+        else if (ksplit == 2)                                                                                       \
+            hipLaunchKernelGGL((deep_hidden_kernel<O, A, 2, A0>), dim3(grid), dim3(kDeepBlock), 0, s, net,          \
                                packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld, a0);                      \
         else                                                                                                        \
-            hipLaunchKernelGGL((deep_hidden_kernel<O, A, false, A0>), dim3(grid), dim3(kDeepBlock), 0, s, net,      \
+            hipLaunchKernelGGL((deep_hidden_kernel<O, A, 0, A0>), dim3(grid), dim3(kDeepBlock), 0, s, net,          \
                                packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld, a0);                      \
     } while (0)
     if (obs_mode == G2048_OBS_ONEHOT) {
@@ -1842,7 +1864,7 @@ int g2048_deep_grad_pack(const float* const* W, int obs_mode, int n_hidden, cons
 }  // extern "C"
 
 namespace {
-template <int OBS, int ACT, int NW, int TPW, bool KSPLIT>
+template <int OBS, int ACT, int NW, int TPW, int KSPLIT>
 int launch_deep_grad_v(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t s) {
     // the dynamic-LDS attribute is per kernel and device: one bit per device id, set on the first launch there
     // (two threads racing both set it, which is harmless)
@@ -1863,10 +1885,10 @@ int launch_deep_grad_v(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t
 template <int OBS, int ACT>
 int launch_deep_grad(const DeepGradArgs& a, const DeepGradVariant& v, int grid, int64_t lds, hipStream_t s) {
     if constexpr (OBS == G2048_OBS_ONEHOT) {
-        if (v.nw == 4) return launch_deep_grad_v<OBS, ACT, 4, 10, false>(a, grid, lds, s);
-        if (v.tpw == 8) return launch_deep_grad_v<OBS, ACT, 8, 8, true>(a, grid, lds, s);
+        if (v.nw == 4) return launch_deep_grad_v<OBS, ACT, 4, 10, G2048_DEEP_SPLIT4 ? 2 : 0>(a, grid, lds, s);
+        if (v.tpw == 8) return launch_deep_grad_v<OBS, ACT, 8, 8, 1>(a, grid, lds, s);
     }
-    return launch_deep_grad_v<OBS, ACT, 8, 6, true>(a, grid, lds, s);
+    return launch_deep_grad_v<OBS, ACT, 8, 6, 1>(a, grid, lds, s);
 }
 }  // namespace
 

@@ -14,6 +14,14 @@ G2048_LIB=<path> loads an A/B build.    zfreshS / mfreshS -- as freshS with obs_
               the synthetic random-state boards and lane state again, S untimed steps, then the timed K
   evolvedS -- a new env (freshly initialised buffers) given the long-running env's evolved boards and lane state,
               S untimed steps, then the timed K
+  noresetS -- as freshS with auto-reset off (finished lanes go inactive: no reset pass, no reset writes)
+  truncN   -- reset rate at will: the long-running env's evolved boards with max_steps = N and lane step counts spread
+              uniformly over 0..N-1, so ~1/N of the lanes truncate and auto-reset every step (board state as steady as
+              `evolved`); 60 untimed steps, then the timed K
+  pollM    -- as trunc1000, then M x 64 MiB of unrelated writes (a scratch fill) just before the timed K: evicts the
+              step kernel's working set from the 256 MB Infinity Cache (MALL) without touching the env
+  bigS     -- as freshS with the synthetic boards built in one whole-batch pass (~10 temporaries of 128 MiB each, the
+              pre-round-5 bench.synthetic_boards) instead of 65,536-board chunks
 Also the host cost of one step_into call.  Prints one JSON line per repetition.
 """
 import argparse
@@ -85,9 +93,33 @@ def main():
             for k in range(skip):
                 fenv.step_into(actions[k % K])
             torch.cuda.synchronize()
-        elif mode[0] in "frsmz":
-            skip = int(mode.lstrip("freshsparetmz") or 5)
+        elif mode.startswith("trunc") or mode.startswith("poll"):
+            N = int(mode[5:]) if mode.startswith("trunc") else 1000
             fenv = bench.make_env(torch, args, B, 0, dev)
+            fenv.board.copy_(env.board)
+            fenv.state.copy_(env.state)
+            fenv._cfg.max_steps = N
+            fenv.set_lane_state(step_count=torch.randint(0, N, (B,), device=dev, generator=g), active=True)
+            for k in range(60):
+                fenv.step_into(actions[k % K])
+            if mode.startswith("poll"):
+                scratch = torch.empty(int(mode[4:]) << 24, dtype=torch.float32, device=dev)
+                scratch.fill_(1.0)
+                del scratch
+            torch.cuda.synchronize()
+        elif mode.startswith("noreset"):
+            skip = int(mode.lstrip("noreset") or 5)
+            fenv = bench.make_env(torch, argparse.Namespace(obs="log2", rng="pcg64", gpus=1, no_auto_reset=True), B, 0,
+                                  dev)
+            for k in range(skip):
+                fenv.step_into(actions[k % K])
+            torch.cuda.synchronize()
+        elif mode[0] in "frsmzb":
+            skip = int(mode.lstrip("freshsparetmzbig") or 5)
+            fenv = bench.make_env(torch, args, B, 0, dev)
+            if mode.startswith("big"):
+                fenv.board.copy_(bench.synthetic_boards(torch, B, 0, dev, chunk=B))
+                fenv.set_lane_state(step_count=0, max_tile_exp=2, active=True)
             if mode.startswith("zfresh"):      # obs values all 0.0 (same stores)
                 fenv._cfg.obs_log2_scale = 0.0
             elif mode.startswith("mfresh"):    # max_tile_seen starts at 2^12 instead of 4
@@ -109,7 +141,7 @@ def main():
         e0.record()
         if mode == "graph":
             gr.replay()
-        elif mode[0] in "frsmze":
+        elif mode[0] in "frsmzentpb":
             for k in range(K):
                 fenv.step_into(actions[k])
         else:
