@@ -950,6 +950,12 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     const float4* wout = reinterpret_cast<const float4*>(wol);
     const float* bo = wol + 4 * HL;
     const uint32_t groups = (a.n + 31u) >> 5;
+#if G2048_DEEP_STAGGER   // A/B builds: delay one of each pair of workgroups by G2048_DEEP_STAGGER x 10 ns
+    if (G2048_DEEP_STAGGER_SEL == 0 ? blockIdx.x >= gridDim.x / 2 : (blockIdx.x & 1u) != 0u) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)G2048_DEEP_STAGGER) __builtin_amdgcn_s_sleep(4);
+    }
+#endif
 #if G2048_DEEP_DIAG
     uint64_t dph[kDiagSlots] = {};
     uint64_t dlast = __builtin_amdgcn_s_memtime();

@@ -41,7 +41,9 @@ pmc_passes() {   # $1 = dir, rest = command
     timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE $P -d "$d/fetch" -o run -- "$@" > "$d/fetch.log" 2>&1 &&
     timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE $P -d "$d/write" -o run -- "$@" > "$d/write.log" 2>&1 &&
     timeout -s KILL 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum $P -d "$d/tcc" -o run -- "$@" > "$d/tcc.log" 2>&1 &&
-    python3 tools/pmc_grad_summary.py "$d" > "$d/summary.jsonl" && cat "$d/summary.jsonl"
+    python3 tools/pmc_grad_summary.py "$d" > "$d/summary.jsonl" && cat "$d/summary.jsonl" &&
+    # the per-dispatch CSVs run to 100s of MiB (gpurun copies back at most 64 MiB): keep the summary and the stats
+    find "$d" \( -name '*_counter_collection.csv' -o -name '*_kernel_trace.csv' \) -size +4M -delete
 }
 
 for step in "$@"; do
