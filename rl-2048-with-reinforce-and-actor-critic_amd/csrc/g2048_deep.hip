@@ -856,6 +856,13 @@ constexpr int kDeepGradMaxBlock = 512;
 #ifndef G2048_DEEP_SPLIT4
 #define G2048_DEEP_SPLIT4 0
 #endif
+// the one-hot gradient kernel's next-group layer-0 prefetch: 1 on, 0 off (A/B builds)
+#ifndef G2048_DEEP_L0_PREFETCH
+#define G2048_DEEP_L0_PREFETCH 1
+#endif
+#ifndef G2048_DEEP_D0_UNROLL   // the delta_0 row stores per batch
+#define G2048_DEEP_D0_UNROLL 32
+#endif
 struct DeepGradVariant {
     int nw, tpw, ksplit, per_cu;
 };
@@ -960,6 +967,30 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     uint64_t dph[kDiagSlots] = {};
     uint64_t dlast = __builtin_amdgcn_s_memtime();
 #endif
+    // one-hot: the layer-0 block of the workgroup's next group (onehot_l0_mfma_kernel's output, [unit][32], 32 KiB at
+    // H0 = 256) copied by LDS-DMA (global_load_lds_dwordx4: no registers -- the register form spilled) into a linear
+    // staging area over the dead deeper layers as soon as the current group's last delta chain is done, so its HBM
+    // latency runs under the delta_0 stores; the group's end barrier is a raw s_barrier (a __syncthreads() fence
+    // would drain the DMA there), and the next group's first barrier retires it.  Its forward then only re-strides
+    // the block from LDS (the load had been 10 % of the group).  Whole groups only; the launch's last, ragged group
+    // reads its block in place.
+    constexpr bool kPrefetch = OBS == G2048_OBS_ONEHOT && G2048_DEEP_L0_PREFETCH;
+    const int H0a = 32 * net.nt[0];
+    float* stage = dyn + a.aoff[0] + H0a * kActStride;   // [unit][32]: deep_grad_act_floats leaves room
+    const auto whole = [&](uint32_t g) { return g < groups && a.n - g * 32u >= 32u; };
+    const auto prefetch = [&](uint32_t g) {   // wave w, piece k: float4s [k kBlock + 64 w, + 64) of the block
+        typedef __attribute__((address_space(1))) void gvoid;
+        typedef __attribute__((address_space(3))) void lvoid;
+        const float4* b4 = reinterpret_cast<const float4*>(a.d0_out + (size_t)g * 32u * (uint32_t)H0a);
+        for (int k = 0; k * kBlock < 8 * H0a; k++) {
+            const int e0 = k * kBlock + 64 * w;
+            if (e0 < 8 * H0a)   // wave-uniform (8 H0 is a multiple of 256)
+                __builtin_amdgcn_global_load_lds((gvoid*)(b4 + e0 + lane), (lvoid*)(stage + 4 * e0), 16, 0, 0);
+        }
+    };
+    if constexpr (kPrefetch) {
+        if (whole(blockIdx.x)) prefetch(blockIdx.x);   // retired by the first group's first barrier
+    }
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
         const uint32_t j = gi * 32u + (uint32_t)(tid & 31);
         const bool valid = j < a.n;
@@ -990,7 +1021,20 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             if constexpr (OBS == G2048_OBS_ONEHOT) {
                 // the group's block from onehot_l0_mfma_kernel (in d0_out: this workgroup overwrites the same rows
                 // with the group's layer-0 deltas at its end)
-                load_l0_block<kBlock>(a.d0_out, a.n, gi, 32 * nt0, out);
+                if (kPrefetch && whole(gi)) {   // the staged block (its DMA retired by the barrier above)
+                    const float4* st4 = reinterpret_cast<const float4*>(stage);
+#pragma unroll 4
+                    for (int e4 = tid; e4 < 8 * H0a; e4 += kBlock) {
+                        const float4 v = st4[e4];
+                        float* o = out + (e4 >> 3) * kActStride + ((e4 & 7) << 2);
+                        o[0] = v.x;
+                        o[1] = v.y;
+                        o[2] = v.z;
+                        o[3] = v.w;
+                    }
+                } else {
+                    load_l0_block<kBlock>(a.d0_out, a.n, gi, 32 * nt0, out);
+                }
             } else {
                 const uint64_t b = bds[col];
                 float x[8];
@@ -1173,19 +1217,22 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             DEEP_STAMP(7);
         }
         // ---- first layer's weight gradient
+        if constexpr (kPrefetch) {
+            if (whole(gi + gridDim.x)) prefetch(gi + gridDim.x);   // the deeper layers' LDS is dead from here on
+        }
         if constexpr (OBS == G2048_OBS_ONEHOT) {
             // delta_0 out for the one-hot scatter (g2048_onehot_dw1): row j, unit tid (coalesced rows)
             const int H0 = 32 * net.nt[0];
             if (tid < H0) {
+                // through a buffer resource over the group's rows (base and row offsets in SGPRs, no 64-bit
+                // per-lane address to keep live; the rows past a ragged group's end fall outside num_records)
                 const float* drow = actl(0) + tid * kActStride;
-                float* dst = a.d0_out + (size_t)gi * 32u * H0 + tid;
-                const uint32_t left = a.n - gi * 32u;
-                if (left >= 32u) {   // a whole group: 32 stores without a per-store branch
-#pragma unroll
-                    for (int n2 = 0; n2 < 32; n2++) dst[(size_t)n2 * H0] = drow[n2];
-                } else {
-                    for (uint32_t n2 = 0; n2 < left; n2++) dst[(size_t)n2 * H0] = drow[n2];
-                }
+                const uint32_t left = a.n - gi * 32u < 32u ? a.n - gi * 32u : 32u;
+                const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                    a.d0_out + (size_t)gi * 32u * (uint32_t)H0, 0, (int)(left * (uint32_t)H0 * 4u), 0x00020000);
+#pragma unroll G2048_DEEP_D0_UNROLL
+                for (int n2 = 0; n2 < 32; n2++)
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(drow[n2]), rd, tid * 4, n2 * H0 * 4, 0);
             }
         } else {
             // dW_0^T tile t (32 units x 32 features, features >= 16 zero): A = delta_0 [unit][sample], B = x [sample][feature]
@@ -1205,7 +1252,12 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 }
             }
         }
-        __syncthreads();   // the next group rewrites the boards and layer 0
+        // the next group rewrites the boards and layer 0: every LDS access done (a raw barrier keeps the DMA in flight)
+        if constexpr (kPrefetch) {
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        } else {
+            __syncthreads();
+        }
         DEEP_STAMP(8);
 #if G2048_DEEP_DIAG
         dph[kDiagSlots - 1] += 1;
@@ -1345,11 +1397,18 @@ DeepGradLayout deep_grad_layout(const DeepNet& n) {
 }
 
 // floats of the output layer's final reduction (deep_grad_kernel: [oq][HL][5], oq HL <= the block size)
+// (one-hot: and the next group's layer-0 staging block [H0][32] right after layer 0's rows)
 int64_t deep_grad_act_floats(const DeepNet& n, int nw) {
     int64_t units = 0;
     for (int l = 0; l < n.L; l++) units += 32 * n.nt[l];
+    int64_t f = units * kActStride;
     const int64_t red = 5 * 64 * nw;
-    return units * kActStride > red ? units * kActStride : red;
+    if (red > f) f = red;
+    if (n.onehot && G2048_DEEP_L0_PREFETCH) {
+        const int64_t st = 32 * n.nt[0] * (kActStride + 32);
+        if (st > f) f = st;
+    }
+    return f;
 }
 int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, bias sums, output weights / bias
     return (deep_grad_act_floats(n, nw) + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256 + 256 * 4 + 4) * 4;
