@@ -397,9 +397,14 @@ __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNe
         }
     }
     const uint32_t groups = (n + 31u) >> 5;
+    const auto board_of = [&](uint32_t g) {   // lane col's board of group g (clamped: always a valid address)
+        const uint32_t j = g * 32u + (uint32_t)col;
+        return boards[j < n ? j : n - 1u];
+    };
+    uint64_t bnext = board_of(blockIdx.x < groups ? blockIdx.x : 0u);
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
-        const uint32_t j = gi * 32u + (uint32_t)col;
-        const uint64_t b = boards[j < n ? j : n - 1u];
+        const uint64_t b = bnext;
+        bnext = board_of(gi + gridDim.x < groups ? gi + gridDim.x : gi);   // the next group's, one group ahead
         floatx16 hi = {}, lo = {};
 #pragma unroll
         for (int c = 0; c < 16; c++) {
@@ -451,11 +456,35 @@ __device__ __forceinline__ void load_l0_block(const float* __restrict__ a0, uint
     }
 }
 
+// Tools-only phase clock (-DG2048_DEEP_DIAG=1 builds; see deep_grad_kernel's DEEP_STAMP): deep_forward stamps its
+// layer phases into it when the caller passes one (the rollout kernel), an empty type in the product.
+constexpr int kDiagSlots = 10;
+#if G2048_DEEP_DIAG
+struct DiagClock {
+    uint64_t ph[kDiagSlots];
+    uint64_t last;
+    __device__ void stamp(int i) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        ph[i] += t - last;
+        last = t;
+    }
+};
+#define FWD_STAMP(dc, i)          \
+    do {                          \
+        if (dc) (dc)->stamp(i);   \
+    } while (0)
+#else
+struct DiagClock {};
+#define FWD_STAMP(dc, i) \
+    do {                 \
+    } while (0)
+#endif
+
 // KSPLIT: the dense layers by dense_fwd_split (the gradient kernel's forward, for the pattern probe).  A0IN (one-hot,
 // the probe): layer 0 from onehot_l0_mfma_kernel's block of group gi (a0) -- the update's layer-0 bits.
 template <int OBS, int ACT, int KSPLIT = 0, bool A0IN = false>
 __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, DeepSmem& S, float obs_scale,
-                             const float* a0 = nullptr, uint32_t n = 0, uint32_t gi = 0) {
+                             const float* a0 = nullptr, uint32_t n = 0, uint32_t gi = 0, DiagClock* dc = nullptr) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
     // ---- first hidden layer -> S.act[0]
     {
@@ -508,6 +537,7 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
         }
     }
     __syncthreads();
+    FWD_STAMP(dc, 1);
     // ---- dense hidden layers 1 .. L-1 (ping-pong)
     for (int l = 1; l < net.L; l++) {
         const float* in = S.act[(l - 1) & 1];
@@ -531,6 +561,7 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
         }
         __syncthreads();
     }
+    FWD_STAMP(dc, 2);
     // ---- output layer partials: thread (p = tid >> 5, board = tid & 31) sums units [p Hp / 8, (p + 1) Hp / 8)
     {
         const float* in = S.act[(net.L - 1) & 1];
@@ -552,6 +583,7 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
         S.part[p][bb][3] = s3;
     }
     __syncthreads();
+    FWD_STAMP(dc, 3);
 }
 
 // the 4 outputs of board `bb` from the partials (threads 0..31 after deep_forward)
@@ -707,6 +739,7 @@ struct DeepRollArgs {
     g2048_suspend sus;
     g2048_traj tr;
     uint32_t n, cap;
+    uint64_t* diag;   // -DG2048_DEEP_DIAG=1 builds only: per-wave phase cycles (tools/diag_deep.py --rollout)
 };
 
 __device__ __forceinline__ Pcg64 load_stream(const uint64_t* rs, const uint64_t* inc, const uint64_t* buf, uint32_t e) {
@@ -775,6 +808,19 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArg
         if (need && idx < a.n_order) start(a.order ? (uint32_t)a.order[idx] : idx);
         drained = __ballot(need && idx >= a.n_order) != 0ull;
     };
+#if G2048_ROLL_STAGGER   // A/B builds: delay one of each pair of workgroups by G2048_ROLL_STAGGER x 10 ns
+    if (G2048_DEEP_STAGGER_SEL == 0 ? blockIdx.x >= gridDim.x / 2 : (blockIdx.x & 1u) != 0u) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)G2048_ROLL_STAGGER) __builtin_amdgcn_s_sleep(4);
+    }
+#endif
+#if G2048_DEEP_DIAG
+    DiagClock dclk{};
+    dclk.last = __builtin_amdgcn_s_memtime();
+    DiagClock* dc = a.diag ? &dclk : nullptr;
+#else
+    DiagClock* dc = nullptr;
+#endif
     if (tid < 64) claim();
     while (true) {
         if (tid < 64) {
@@ -783,8 +829,9 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArg
             if (owner) S.board[tid] = ep != kNoEpisode ? b : 0ull;
         }
         __syncthreads();
+        FWD_STAMP(dc, 0);
         if (!go) break;                                // block-uniform
-        deep_forward<OBS, ACT>(a.net, a.packed, S, a.obs_scale);
+        deep_forward<OBS, ACT>(a.net, a.packed, S, a.obs_scale, nullptr, 0, 0, dc);
         if (owner && ep != kNoEpisode) {
             float lg[4];
             deep_logits(a.net, a.packed, S, tid, lg);
@@ -820,8 +867,20 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArg
                 ep = kNoEpisode;
             }
         }
+        FWD_STAMP(dc, 4);
         if (tid < 64) claim();
+        FWD_STAMP(dc, 5);
+#if G2048_DEEP_DIAG
+        dclk.ph[kDiagSlots - 1] += 1;
+#endif
     }
+#if G2048_DEEP_DIAG
+    if (a.diag && (tid & 63) == 0) {
+        uint64_t* slot = a.diag + ((size_t)blockIdx.x * (kDeepBlock / 64) + (tid >> 6)) * kDiagSlots;
+#pragma unroll
+        for (int i = 0; i < kDiagSlots; i++) slot[i] += dclk.ph[i];
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------ update (fused, any depth)
@@ -899,7 +958,6 @@ struct DeepGradArgs {
 // Phase-time attribution (tools-only build, -DG2048_DEEP_DIAG=1): each wave adds the s_memtime cycles of every
 // phase (ending at the barrier that closes it, so a phase includes waiting for the slowest wave) to its own slot
 // diag[(block * NW + wave) * kDiagSlots + phase]; slot kDiagSlots - 1 counts the groups.  No stamp in the product.
-constexpr int kDiagSlots = 10;
 #if G2048_DEEP_DIAG
 #define DEEP_STAMP(i)                                             \
     do {                                                          \
@@ -912,6 +970,22 @@ constexpr int kDiagSlots = 10;
     do {              \
     } while (0)
 #endif
+
+// The gradient kernel's in-loop barriers order LDS accesses only: a raw s_barrier behind lgkmcnt(0).
+// __syncthreads() adds a workgroup release fence, i.e. vmcnt(0): every barrier would wait for the wave's global
+// stores (the V(s) / delta_0 rows) and for the weight-fragment loads a chain's window left in flight, none of which
+// another wave reads (loaded values are waited for at their use, as always).  The group's first barrier keeps
+// __syncthreads(): it retires the layer-0 LDS-DMA.  G2048_DEEP_RAW_BARRIER=0: __syncthreads() everywhere (A/B).
+#ifndef G2048_DEEP_RAW_BARRIER
+#define G2048_DEEP_RAW_BARRIER 1
+#endif
+__device__ __forceinline__ void lds_barrier() {
+#if G2048_DEEP_RAW_BARRIER
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+    __syncthreads();
+#endif
+}
 
 template <int ACT>
 __device__ __forceinline__ float act_deriv(float a) {   // from the activation (src/reinforce_agent.py:624-636)
@@ -1055,7 +1129,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
         DEEP_STAMP(1);
         if (tid < 32 && a.critic && a.has_td) td_v = a.td.v_next[td_l];
         // ---- forward: dense layers (each into its own region)
@@ -1077,7 +1151,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     for (int r = 0; r < 16; r++) out[(32 * o + tile_row(r, h)) * kActStride + col] = activate<ACT>(c[r] + bv[r]);
                 }
             }
-            __syncthreads();
+            lds_barrier();
         }
         DEEP_STAMP(2);
         // ---- output layer partials (as deep_forward; threads 0..255)
@@ -1098,7 +1172,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             part[pp][bb][2] = s2;
             part[pp][bb][3] = s3;
         }
-        __syncthreads();
+        lds_barrier();
         DEEP_STAMP(3);
         // ---- logits -> g (threads 0..31, one sample each)
         if (tid < 32) {
@@ -1144,7 +1218,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 dbo4[k] += g[k];
             }
         }
-        __syncthreads();
+        lds_barrier();
         DEEP_STAMP(4);
         // ---- output layer backward: dW_out, db_{L-1}, delta_{L-1} in place; thread (unit u, sample range q) of
         //      oq ranges, so every thread works (one thread per unit ran 32 serial steps on one or two waves)
@@ -1171,7 +1245,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             dwo[0] = d0; dwo[1] = d1; dwo[2] = d2; dwo[3] = d3;
             dbl = db;
         }
-        __syncthreads();
+        lds_barrier();
         DEEP_STAMP(5);
         // ---- dense layers top down: dW_l (MFMA over the 32 samples), then delta_{l-1} (MFMA chain) in place
         for (int l = L - 1; l >= 1; l--) {
@@ -1193,7 +1267,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     acc[k] = c;
                 }
             }
-            __syncthreads();                               // every read of a_{l-1} by the dW tiles is done
+            lds_barrier();                               // every read of a_{l-1} by the dW tiles is done
             DEEP_STAMP(6);
             // delta_{l-1} = (W_l delta_l) act'(a_{l-1}): output tiles = layer l-1's units, k = layer l's units
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(a.bpacked + a.boff[l]) + lane;
@@ -1206,7 +1280,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     *pa = c[r] * act_deriv<ACT>(*pa);
                 }
             }
-            __syncthreads();
+            lds_barrier();
             // db_{l-1} of unit tid
             if (tid < 32 * ntin) {
                 const float* drow = Aw + tid * kActStride;
@@ -1252,11 +1326,11 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 }
             }
         }
-        // the next group rewrites the boards and layer 0: every LDS access done (a raw barrier keeps the DMA in flight)
+        // the next group rewrites the boards and layer 0: every LDS access done (raw: keeps the DMA in flight)
         if constexpr (kPrefetch) {
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         } else {
-            __syncthreads();
+            lds_barrier();
         }
         DEEP_STAMP(8);
 #if G2048_DEEP_DIAG
@@ -1684,6 +1758,13 @@ int launch_onehot_l0(const DeepNet& net, const float* packed, const uint64_t* bo
 }
 }  // namespace
 
+#if G2048_DEEP_DIAG
+namespace {
+uint64_t* g_deep_diag = nullptr;
+}
+extern "C" void g2048_diag_deep_stamps(uint64_t* p) { g_deep_diag = p; }   // tools-only build (no header entry)
+#endif
+
 extern "C" {
 
 int64_t g2048_deep_packed_size(int obs_mode, int n_hidden, const int32_t* hidden) {
@@ -1790,6 +1871,11 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
     int cus = 256;
     if ((rc = g2048_internal::device_tables(tab, cus))) return rc;
     DeepRollArgs a;
+#if G2048_DEEP_DIAG
+    a.diag = g_deep_diag;
+#else
+    a.diag = nullptr;
+#endif
     a.net = net;
     a.packed = packed;
     a.tab = tab;
@@ -1957,12 +2043,6 @@ int launch_deep_grad(const DeepGradArgs& a, const DeepGradVariant& v, int grid, 
 }
 }  // namespace
 
-#if G2048_DEEP_DIAG
-namespace {
-uint64_t* g_deep_diag = nullptr;
-}
-extern "C" void g2048_diag_deep_stamps(uint64_t* p) { g_deep_diag = p; }   // tools-only build (no header entry)
-#endif
 
 extern "C" {
 
