@@ -278,6 +278,9 @@ class ReinforceAgent:
         self.use_fused_rollout = True
         # update_batch's actor gradient through the fused g2048_actor_grad kernel when the net fits it (batched path)
         self.use_fused_grad = True
+        # two-layer log2 / raw nets through the cooperative g2048_actor_grad / g2048_critic_grad kernels (+ g2048_dw2);
+        # False routes them to g2048_deep_grad where it covers the net (tools/bench_update.py --deep-grad A/B)
+        self.use_two_layer_grad = True
         # ... and the fused critic per time row, V(s') taken from the next row's pass (large batches)
         self.use_critic_rows = True
         self.critic_factored_d2 = True   # ReLU critic rows: the factored d2 records + g2048_dw2_factored
@@ -431,11 +434,11 @@ class ReinforceAgent:
 
     def _fused_grad_spec(self):
         """The same net check for g2048_actor_grad (else the batched torch backprop runs)."""
-        return self._net_spec() if self.use_fused_grad else None
+        return self._net_spec() if self.use_fused_grad and self.use_two_layer_grad else None
 
     def _fused_critic_spec(self):
         """... and for the critic (value head of width 1) through g2048_critic_grad."""
-        if not self.use_fused_grad or self.critic_params is None:
+        if not self.use_fused_grad or not self.use_two_layer_grad or self.critic_params is None:
             return None
         return self._net_spec(self.critic_params, 1)
 

@@ -182,6 +182,14 @@ struct DeepSmem {
     float part[8][32][4];             // output-layer partial sums [unit slice][board][output]
     uint64_t board[32];               // the group's boards
 };
+// The forward's view of its LDS: the static DeepSmem (policy / probe kernels) or the rollout's net-sized dynamic
+// layout (deep_roll_layout).
+struct DeepLds {
+    float* act[2];
+    float (*part)[32][4];
+    uint64_t* board;
+};
+__device__ __forceinline__ DeepLds lds_of(DeepSmem& S) { return DeepLds{{S.act[0], S.act[1]}, S.part, S.board}; }
 
 // The k-ordered MFMA chain of one output tile over k-tiles [t0, t1): A = the tile's weight fragments `fo` (4 float4
 // per lane per k-tile, streamed from L2), B = the activation rows `in` (LDS).  Two fragment register sets, fa for
@@ -483,7 +491,7 @@ struct DiagClock {};
 // KSPLIT: the dense layers by dense_fwd_split (the gradient kernel's forward, for the pattern probe).  A0IN (one-hot,
 // the probe): layer 0 from onehot_l0_mfma_kernel's block of group gi (a0) -- the update's layer-0 bits.
 template <int OBS, int ACT, int KSPLIT = 0, bool A0IN = false>
-__device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, DeepSmem& S, float obs_scale,
+__device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, const DeepLds& S, float obs_scale,
                              const float* a0 = nullptr, uint32_t n = 0, uint32_t gi = 0, DiagClock* dc = nullptr) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
     // ---- first hidden layer -> S.act[0]
@@ -587,7 +595,7 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
 }
 
 // the 4 outputs of board `bb` from the partials (threads 0..31 after deep_forward)
-__device__ __forceinline__ void deep_logits(const DeepNet& net, const float* __restrict__ P, const DeepSmem& S, int bb,
+__device__ __forceinline__ void deep_logits(const DeepNet& net, const float* __restrict__ P, const DeepLds& S, int bb,
                                             float lg[4]) {
     const float* bo = P + net.b[net.L];
 #pragma unroll
@@ -623,7 +631,8 @@ __device__ __forceinline__ uint32_t mask_word_of(uint64_t b) {
 
 template <int OBS, int ACT, int RNG>
 __global__ void __launch_bounds__(kDeepBlock, 2) deep_policy_kernel(DeepPolArgs a) {
-    __shared__ DeepSmem S;
+    __shared__ DeepSmem Ss;
+    const DeepLds S = lds_of(Ss);
     const uint32_t groups = (a.n + 31u) >> 5;
     const int tid = threadIdx.x;
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
@@ -680,7 +689,8 @@ template <int OBS, int ACT, int KSPLIT, bool A0IN>
 __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net, const float* packed,
                                                                      const uint64_t* boards, uint32_t n, float obs_scale,
                                                                      float* out, uint32_t ld, const float* a0) {
-    __shared__ DeepSmem S;
+    __shared__ DeepSmem Ss;
+    const DeepLds S = lds_of(Ss);
     const uint32_t groups = (n + 31u) >> 5;
     const int tid = threadIdx.x, layer = net.L - 1, H = 32 * net.nt[layer];
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
@@ -718,6 +728,9 @@ struct GCode {
     __device__ uint32_t operator()(uint32_t o) const { return (p[o >> 1] >> ((o & 1u) << 2)) & 15u; }
 };
 
+#ifndef G2048_ROLL_PER_CU
+#define G2048_ROLL_PER_CU 2
+#endif
 struct DeepRollArgs {
     DeepNet net;
     const float* packed;
@@ -739,8 +752,47 @@ struct DeepRollArgs {
     g2048_suspend sus;
     g2048_traj tr;
     uint32_t n, cap;
+    int lds_act1, lds_part, lds_board;   // float offsets of deep_roll_layout's regions
     uint64_t* diag;   // -DG2048_DEEP_DIAG=1 builds only: per-wave phase cycles (tools/diag_deep.py --rollout)
 };
+
+// The rollout's LDS sized to its net (round 5; the static DeepSmem reserved 2 x 256 units): layers alternate
+// between region A (act[0]: layers 0, 2, ..) and region B (act[1]: layers 1, 3, ..), each as large as its widest
+// layer; the output partials [8][32][4] share the region the last hidden layer does NOT occupy (dead by then;
+// the next step's first write to it comes after the owners read the logits), then the 32 boards.  [256, 128, 64]:
+// 50.9 KiB instead of 71.8 KiB, so three workgroups fit a CU (deep_roll_per_cu) instead of two.
+struct DeepRollLayout {
+    int act1, part, board, floats;
+};
+DeepRollLayout deep_roll_layout(const DeepNet& n) {
+    int ua = 0, ub = 0;
+    for (int l = 0; l < n.L; l++) {
+        int& u = (l & 1) ? ub : ua;
+        if (32 * n.nt[l] > u) u = 32 * n.nt[l];
+    }
+    int fa = ua * kActStride, fb = ub * kActStride;
+    const int kPart = 8 * 32 * 4;
+    if ((n.L - 1) & 1) {   // the last hidden layer in B: the partials in A
+        if (fa < kPart) fa = kPart;
+    } else if (fb < kPart) {
+        fb = kPart;
+    }
+    DeepRollLayout r;
+    r.act1 = fa;
+    r.part = ((n.L - 1) & 1) ? 0 : fa;
+    r.board = fa + fb;   // 8-byte aligned: fa, fb are multiples of 32 floats
+    r.floats = r.board + 64;
+    return r;
+}
+// workgroups per CU: at most G2048_ROLL_PER_CU (the kernel's launch bounds) and what the LDS allows.  Two: a third
+// workgroup per CU (the layout fits [256, 128, 64] three times) made the rollout slower, 0.275 -> 0.315 s at 1M
+// episodes -- the dense layers' weight-fragment streams and the one-hot gathers of three workgroups share one CU's
+// L2 -> L1 bandwidth (stamps: dense 24.7 k -> 61.1 k cycles per step; `profiles/round5/r5q/`).
+int deep_roll_per_cu(const DeepNet& n) {
+    const int64_t bytes = (int64_t)deep_roll_layout(n).floats * 4 + 256;   // + the static `go` flag
+    const int64_t k = (160 * 1024) / bytes;
+    return k >= G2048_ROLL_PER_CU ? G2048_ROLL_PER_CU : (k < 1 ? 1 : (int)k);
+}
 
 __device__ __forceinline__ Pcg64 load_stream(const uint64_t* rs, const uint64_t* inc, const uint64_t* buf, uint32_t e) {
     Pcg64 g;
@@ -764,8 +816,10 @@ __device__ __forceinline__ void store_stream(uint64_t* rs, uint64_t* buf, uint32
 constexpr uint32_t kNoEpisode = 0xFFFFFFFFu;
 
 template <int OBS, int ACT>
-__global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArgs a) {
-    __shared__ DeepSmem S;
+__global__ void __launch_bounds__(kDeepBlock, G2048_ROLL_PER_CU) deep_rollout_kernel(DeepRollArgs a) {
+    extern __shared__ float dyn[];
+    const DeepLds S{{dyn, dyn + a.lds_act1}, reinterpret_cast<float (*)[32][4]>(dyn + a.lds_part),
+                    reinterpret_cast<uint64_t*>(dyn + a.lds_board)};
     __shared__ int go;
     const int tid = threadIdx.x;
     const bool owner = tid < 32;
@@ -914,6 +968,11 @@ constexpr int kDeepGradMaxBlock = 512;
 // the 4-wave instantiation's k-split of its 64-unit layer (dense_fwd_split MODE 2): 1 on, 0 off (A/B builds)
 #ifndef G2048_DEEP_SPLIT4
 #define G2048_DEEP_SPLIT4 0
+#endif
+// log2 / raw nets of 49..64 dense tiles (configs[2]'s [256, 256]) on the 8 x 8 instantiation too: 1 = on (A/B builds
+// only -- it spills ~300 VGPRs; the shipped path is the two-layer cooperative kernel)
+#ifndef G2048_DEEP_LOG2_64
+#define G2048_DEEP_LOG2_64 0
 #endif
 // the one-hot gradient kernel's next-group layer-0 prefetch: 1 on, 0 off (A/B builds)
 #ifndef G2048_DEEP_L0_PREFETCH
@@ -1495,7 +1554,7 @@ DeepGradVariant deep_grad_variant(const DeepNet& n) {
     const int tiles = deep_grad_layout(n).ntiles;
     if (n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024) return {4, 10, G2048_DEEP_SPLIT4 ? 2 : 0, 2};
     if (tiles <= 48 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 6, 1, 1};
-    if (n.onehot && tiles <= 64 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 8, 1, 1};
+    if ((n.onehot || G2048_DEEP_LOG2_64) && tiles <= 64 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 8, 1, 1};
     return {0, 0, 0, 0};
 }
 
@@ -1746,6 +1805,25 @@ int check_hip() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : dfail(G2048_EHIP, hipGetErrorString(e));
 }
+template <int OBS, int ACT>
+int launch_deep_roll(const DeepRollArgs& a, int grid, size_t lds, hipStream_t s) {
+    // nets whose layout passes 64 KiB need the dynamic-LDS attribute: one bit per device id, set on the first
+    // launch there (two threads racing both set it, which is harmless)
+    static std::atomic<uint64_t> attr_set{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return dfail(G2048_EHIP, "deep rollout: hipGetDevice failed");
+    const uint64_t bit = 1ull << (dev & 63);
+    if (!(attr_set.load(std::memory_order_acquire) & bit)) {
+        // the kernel's static `go` flag shares the 160 KiB: the dynamic part may take the rest
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&deep_rollout_kernel<OBS, ACT>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256) != hipSuccess)
+            return (void)hipGetLastError(), dfail(G2048_EHIP, "deep rollout: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+        attr_set.fetch_or(bit, std::memory_order_acq_rel);
+    }
+    hipLaunchKernelGGL((deep_rollout_kernel<OBS, ACT>), dim3(grid), dim3(kDeepBlock), (unsigned)lds, s, a);
+    return check_hip();
+}
+
 int launch_onehot_l0(const DeepNet& net, const float* packed, const uint64_t* boards, uint32_t n, int activation,
                      float* out, hipStream_t s) {
     const int64_t groups = ((int64_t)n + 31) / 32, cap = device_cus();
@@ -1898,21 +1976,24 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
     a.tr = *traj;
     a.n = (uint32_t)n;
     a.cap = (uint32_t)cap;
+    const DeepRollLayout lay = deep_roll_layout(net);
+    a.lds_act1 = lay.act1;
+    a.lds_part = lay.part;
+    a.lds_board = lay.board;
+    const size_t lds = (size_t)lay.floats * 4;
     int64_t grid = (n_order + 31) / 32;
-    if (grid > 2 * (int64_t)cus) grid = 2 * (int64_t)cus;   // persistent; the slots refill from the queue
+    const int64_t cap_grid = (int64_t)deep_roll_per_cu(net) * cus;
+    if (grid > cap_grid) grid = cap_grid;   // persistent; the slots refill from the queue
     hipStream_t s = (hipStream_t)stream;
     const int obs = cfg->obs_mode;
-    if (obs == G2048_OBS_ONEHOT) {
-        if (activation == G2048_ACT_RELU) hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_ONEHOT, 0>), dim3(grid), dim3(kDeepBlock), 0, s, a);
-        else hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_ONEHOT, 1>), dim3(grid), dim3(kDeepBlock), 0, s, a);
-    } else if (obs == G2048_OBS_LOG2) {
-        if (activation == G2048_ACT_RELU) hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_LOG2, 0>), dim3(grid), dim3(kDeepBlock), 0, s, a);
-        else hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_LOG2, 1>), dim3(grid), dim3(kDeepBlock), 0, s, a);
-    } else {
-        if (activation == G2048_ACT_RELU) hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_RAW, 0>), dim3(grid), dim3(kDeepBlock), 0, s, a);
-        else hipLaunchKernelGGL((deep_rollout_kernel<G2048_OBS_RAW, 1>), dim3(grid), dim3(kDeepBlock), 0, s, a);
-    }
-    return check_hip();
+    if (obs == G2048_OBS_ONEHOT)
+        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_ONEHOT, 0>(a, (int)grid, lds, s)
+                                            : launch_deep_roll<G2048_OBS_ONEHOT, 1>(a, (int)grid, lds, s);
+    if (obs == G2048_OBS_LOG2)
+        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_LOG2, 0>(a, (int)grid, lds, s)
+                                            : launch_deep_roll<G2048_OBS_LOG2, 1>(a, (int)grid, lds, s);
+    return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_RAW, 0>(a, (int)grid, lds, s)
+                                        : launch_deep_roll<G2048_OBS_RAW, 1>(a, (int)grid, lds, s);
 }
 
 int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, int activation, int obs_mode,
@@ -2026,7 +2107,7 @@ int launch_deep_grad_v(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t
     if (!(attr_set.load(std::memory_order_acquire) & bit)) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(&deep_grad_kernel<OBS, ACT, NW, TPW, KSPLIT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-            return dfail(G2048_EHIP, "deep gradient: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+            return (void)hipGetLastError(), dfail(G2048_EHIP, "deep gradient: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
         attr_set.fetch_or(bit, std::memory_order_acq_rel);
     }
     hipLaunchKernelGGL((deep_grad_kernel<OBS, ACT, NW, TPW, KSPLIT>), dim3(grid), dim3(64 * NW), (unsigned)lds, s, a);
@@ -2037,6 +2118,8 @@ template <int OBS, int ACT>
 int launch_deep_grad(const DeepGradArgs& a, const DeepGradVariant& v, int grid, int64_t lds, hipStream_t s) {
     if constexpr (OBS == G2048_OBS_ONEHOT) {
         if (v.nw == 4) return launch_deep_grad_v<OBS, ACT, 4, 10, G2048_DEEP_SPLIT4 ? 2 : 0>(a, grid, lds, s);
+        if (v.tpw == 8) return launch_deep_grad_v<OBS, ACT, 8, 8, 1>(a, grid, lds, s);
+    } else if constexpr (G2048_DEEP_LOG2_64 != 0) {
         if (v.tpw == 8) return launch_deep_grad_v<OBS, ACT, 8, 8, 1>(a, grid, lds, s);
     }
     return launch_deep_grad_v<OBS, ACT, 8, 6, 1>(a, grid, lds, s);

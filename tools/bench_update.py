@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--repeats", type=int, default=2)
     ap.add_argument("--lib", default=None, help="another build of libg2048 (A/B scripts)")
     ap.add_argument("--repo", default=None, help="import rl2048_amd from this checkout")
+    ap.add_argument("--deep-grad", action="store_true",
+                    help="the two-layer net through g2048_deep_grad (use_two_layer_grad = False; a --lib build with "
+                         "G2048_DEEP_LOG2_64=1 covers log2 [256, 256])")
     ap.add_argument("--no-actor-records", action="store_true",
                     help="actor d2 as columns + g2048_dw2 instead of d2_form 2 records + g2048_dw2_actor (A/B)")
     args = ap.parse_args()
@@ -49,6 +52,8 @@ def main():
                                ReinforceAgentConfig(baseline_mode="batch", use_critic=args.critic), device=dev)
         if args.no_actor_records:
             agent.actor_d2_records = False
+        if args.deep_grad:
+            agent.use_two_layer_grad = False
         for rep in range(args.repeats + 1):
             base = 1000 + rep * n
             es = np.arange(base, base + n, dtype=np.int64)   # seed arrays (SeedStream.take_array form)
@@ -68,7 +73,7 @@ def main():
             print(json.dumps({"episodes": n, "critic": args.critic, "T": batch.T, "samples": samples,
                               "rollout_s": round(t1 - t0, 4), "update_s": round(t2 - t1, 4),
                               "rollout_steps_per_s": samples / (t1 - t0), "update_samples_per_s": samples / (t2 - t1),
-                              "update_tflops": flop / (t2 - t1) / 1e12}), flush=True)
+                              "update_tflops": flop / (t2 - t1) / 1e12, "paths": agent.last_paths()}), flush=True)
 
 
 if __name__ == "__main__":
