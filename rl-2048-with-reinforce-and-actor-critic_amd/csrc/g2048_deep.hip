@@ -177,19 +177,14 @@ __device__ __forceinline__ float obs_value(uint64_t b, int cell, float scale) {
     else return e ? (float)(1u << e) : 0.0f;
 }
 
+// (Always the static struct: passing the forward its LDS as pointers -- for a rollout layout sized to the net --
+// made hipcc emit FLAT instead of LDS instructions for the forward's accesses, in every form tried, and the
+// rollout ran 0.318-0.348 s against 0.275 s; `profiles/round5/r5u/`, `r5v/`.)
 struct DeepSmem {
     float act[2][256 * kActStride];   // ping-pong activations [unit][board]
     float part[8][32][4];             // output-layer partial sums [unit slice][board][output]
     uint64_t board[32];               // the group's boards
 };
-// The forward's view of its LDS: the static DeepSmem (policy / probe kernels) or the rollout's net-sized dynamic
-// layout (deep_roll_layout).
-struct DeepLds {
-    float* act[2];
-    float (*part)[32][4];
-    uint64_t* board;
-};
-__device__ __forceinline__ DeepLds lds_of(DeepSmem& S) { return DeepLds{{S.act[0], S.act[1]}, S.part, S.board}; }
 
 // The k-ordered MFMA chain of one output tile over k-tiles [t0, t1): A = the tile's weight fragments `fo` (4 float4
 // per lane per k-tile, streamed from L2), B = the activation rows `in` (LDS).  Two fragment register sets, fa for
@@ -491,7 +486,7 @@ struct DiagClock {};
 // KSPLIT: the dense layers by dense_fwd_split (the gradient kernel's forward, for the pattern probe).  A0IN (one-hot,
 // the probe): layer 0 from onehot_l0_mfma_kernel's block of group gi (a0) -- the update's layer-0 bits.
 template <int OBS, int ACT, int KSPLIT = 0, bool A0IN = false>
-__device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, const DeepLds& S, float obs_scale,
+__device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, DeepSmem& S, float obs_scale,
                              const float* a0 = nullptr, uint32_t n = 0, uint32_t gi = 0, DiagClock* dc = nullptr) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
     // ---- first hidden layer -> S.act[0]
@@ -595,7 +590,7 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, co
 }
 
 // the 4 outputs of board `bb` from the partials (threads 0..31 after deep_forward)
-__device__ __forceinline__ void deep_logits(const DeepNet& net, const float* __restrict__ P, const DeepLds& S, int bb,
+__device__ __forceinline__ void deep_logits(const DeepNet& net, const float* __restrict__ P, const DeepSmem& S, int bb,
                                             float lg[4]) {
     const float* bo = P + net.b[net.L];
 #pragma unroll
@@ -631,8 +626,7 @@ __device__ __forceinline__ uint32_t mask_word_of(uint64_t b) {
 
 template <int OBS, int ACT, int RNG>
 __global__ void __launch_bounds__(kDeepBlock, 2) deep_policy_kernel(DeepPolArgs a) {
-    __shared__ DeepSmem Ss;
-    const DeepLds S = lds_of(Ss);
+    __shared__ DeepSmem S;
     const uint32_t groups = (a.n + 31u) >> 5;
     const int tid = threadIdx.x;
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
@@ -689,8 +683,7 @@ template <int OBS, int ACT, int KSPLIT, bool A0IN>
 __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net, const float* packed,
                                                                      const uint64_t* boards, uint32_t n, float obs_scale,
                                                                      float* out, uint32_t ld, const float* a0) {
-    __shared__ DeepSmem Ss;
-    const DeepLds S = lds_of(Ss);
+    __shared__ DeepSmem S;
     const uint32_t groups = (n + 31u) >> 5;
     const int tid = threadIdx.x, layer = net.L - 1, H = 32 * net.nt[layer];
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
@@ -728,9 +721,6 @@ struct GCode {
     __device__ uint32_t operator()(uint32_t o) const { return (p[o >> 1] >> ((o & 1u) << 2)) & 15u; }
 };
 
-#ifndef G2048_ROLL_PER_CU
-#define G2048_ROLL_PER_CU 2
-#endif
 struct DeepRollArgs {
     DeepNet net;
     const float* packed;
@@ -752,47 +742,8 @@ struct DeepRollArgs {
     g2048_suspend sus;
     g2048_traj tr;
     uint32_t n, cap;
-    int lds_act1, lds_part, lds_board;   // float offsets of deep_roll_layout's regions
     uint64_t* diag;   // -DG2048_DEEP_DIAG=1 builds only: per-wave phase cycles (tools/diag_deep.py --rollout)
 };
-
-// The rollout's LDS sized to its net (round 5; the static DeepSmem reserved 2 x 256 units): layers alternate
-// between region A (act[0]: layers 0, 2, ..) and region B (act[1]: layers 1, 3, ..), each as large as its widest
-// layer; the output partials [8][32][4] share the region the last hidden layer does NOT occupy (dead by then;
-// the next step's first write to it comes after the owners read the logits), then the 32 boards.  [256, 128, 64]:
-// 50.9 KiB instead of 71.8 KiB, so three workgroups fit a CU (deep_roll_per_cu) instead of two.
-struct DeepRollLayout {
-    int act1, part, board, floats;
-};
-DeepRollLayout deep_roll_layout(const DeepNet& n) {
-    int ua = 0, ub = 0;
-    for (int l = 0; l < n.L; l++) {
-        int& u = (l & 1) ? ub : ua;
-        if (32 * n.nt[l] > u) u = 32 * n.nt[l];
-    }
-    int fa = ua * kActStride, fb = ub * kActStride;
-    const int kPart = 8 * 32 * 4;
-    if ((n.L - 1) & 1) {   // the last hidden layer in B: the partials in A
-        if (fa < kPart) fa = kPart;
-    } else if (fb < kPart) {
-        fb = kPart;
-    }
-    DeepRollLayout r;
-    r.act1 = fa;
-    r.part = ((n.L - 1) & 1) ? 0 : fa;
-    r.board = fa + fb;   // 8-byte aligned: fa, fb are multiples of 32 floats
-    r.floats = r.board + 64;
-    return r;
-}
-// workgroups per CU: at most G2048_ROLL_PER_CU (the kernel's launch bounds) and what the LDS allows.  Two: a third
-// workgroup per CU (the layout fits [256, 128, 64] three times) made the rollout slower, 0.275 -> 0.315 s at 1M
-// episodes -- the dense layers' weight-fragment streams and the one-hot gathers of three workgroups share one CU's
-// L2 -> L1 bandwidth (stamps: dense 24.7 k -> 61.1 k cycles per step; `profiles/round5/r5q/`).
-int deep_roll_per_cu(const DeepNet& n) {
-    const int64_t bytes = (int64_t)deep_roll_layout(n).floats * 4 + 256;   // + the static `go` flag
-    const int64_t k = (160 * 1024) / bytes;
-    return k >= G2048_ROLL_PER_CU ? G2048_ROLL_PER_CU : (k < 1 ? 1 : (int)k);
-}
 
 __device__ __forceinline__ Pcg64 load_stream(const uint64_t* rs, const uint64_t* inc, const uint64_t* buf, uint32_t e) {
     Pcg64 g;
@@ -816,10 +767,8 @@ __device__ __forceinline__ void store_stream(uint64_t* rs, uint64_t* buf, uint32
 constexpr uint32_t kNoEpisode = 0xFFFFFFFFu;
 
 template <int OBS, int ACT>
-__global__ void __launch_bounds__(kDeepBlock, G2048_ROLL_PER_CU) deep_rollout_kernel(DeepRollArgs a) {
-    extern __shared__ float dyn[];
-    const DeepLds S{{dyn, dyn + a.lds_act1}, reinterpret_cast<float (*)[32][4]>(dyn + a.lds_part),
-                    reinterpret_cast<uint64_t*>(dyn + a.lds_board)};
+__global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArgs a) {
+    __shared__ DeepSmem S;
     __shared__ int go;
     const int tid = threadIdx.x;
     const bool owner = tid < 32;
@@ -1806,21 +1755,8 @@ int check_hip() {
     return e == hipSuccess ? G2048_OK : dfail(G2048_EHIP, hipGetErrorString(e));
 }
 template <int OBS, int ACT>
-int launch_deep_roll(const DeepRollArgs& a, int grid, size_t lds, hipStream_t s) {
-    // nets whose layout passes 64 KiB need the dynamic-LDS attribute: one bit per device id, set on the first
-    // launch there (two threads racing both set it, which is harmless)
-    static std::atomic<uint64_t> attr_set{0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return dfail(G2048_EHIP, "deep rollout: hipGetDevice failed");
-    const uint64_t bit = 1ull << (dev & 63);
-    if (!(attr_set.load(std::memory_order_acquire) & bit)) {
-        // the kernel's static `go` flag shares the 160 KiB: the dynamic part may take the rest
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&deep_rollout_kernel<OBS, ACT>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256) != hipSuccess)
-            return (void)hipGetLastError(), dfail(G2048_EHIP, "deep rollout: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-        attr_set.fetch_or(bit, std::memory_order_acq_rel);
-    }
-    hipLaunchKernelGGL((deep_rollout_kernel<OBS, ACT>), dim3(grid), dim3(kDeepBlock), (unsigned)lds, s, a);
+int launch_deep_roll(const DeepRollArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((deep_rollout_kernel<OBS, ACT>), dim3(grid), dim3(kDeepBlock), 0, s, a);
     return check_hip();
 }
 
@@ -1976,24 +1912,18 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
     a.tr = *traj;
     a.n = (uint32_t)n;
     a.cap = (uint32_t)cap;
-    const DeepRollLayout lay = deep_roll_layout(net);
-    a.lds_act1 = lay.act1;
-    a.lds_part = lay.part;
-    a.lds_board = lay.board;
-    const size_t lds = (size_t)lay.floats * 4;
     int64_t grid = (n_order + 31) / 32;
-    const int64_t cap_grid = (int64_t)deep_roll_per_cu(net) * cus;
-    if (grid > cap_grid) grid = cap_grid;   // persistent; the slots refill from the queue
+    if (grid > 2 * (int64_t)cus) grid = 2 * (int64_t)cus;   // persistent; the slots refill from the queue
     hipStream_t s = (hipStream_t)stream;
     const int obs = cfg->obs_mode;
     if (obs == G2048_OBS_ONEHOT)
-        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_ONEHOT, 0>(a, (int)grid, lds, s)
-                                            : launch_deep_roll<G2048_OBS_ONEHOT, 1>(a, (int)grid, lds, s);
+        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_ONEHOT, 0>(a, (int)grid, s)
+                                            : launch_deep_roll<G2048_OBS_ONEHOT, 1>(a, (int)grid, s);
     if (obs == G2048_OBS_LOG2)
-        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_LOG2, 0>(a, (int)grid, lds, s)
-                                            : launch_deep_roll<G2048_OBS_LOG2, 1>(a, (int)grid, lds, s);
-    return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_RAW, 0>(a, (int)grid, lds, s)
-                                        : launch_deep_roll<G2048_OBS_RAW, 1>(a, (int)grid, lds, s);
+        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_LOG2, 0>(a, (int)grid, s)
+                                            : launch_deep_roll<G2048_OBS_LOG2, 1>(a, (int)grid, s);
+    return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_RAW, 0>(a, (int)grid, s)
+                                        : launch_deep_roll<G2048_OBS_RAW, 1>(a, (int)grid, s);
 }
 
 int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, int activation, int obs_mode,
