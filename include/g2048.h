@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 14
+#define G2048_ABI_VERSION 15
 
 /* status codes */
 #define G2048_OK 0
@@ -322,7 +322,11 @@ int g2048_rollout(const float* packed, int h1, int h2, int activation, const g20
 /* ---- nets of any depth and one-hot first layers (g2048_deep.hip; ABI 13) ----------------------------------------
  * forward_logits (src/MLP.py:159-196) for 1..G2048_DEEP_MAX_HIDDEN hidden layers of 1..256 units, ReLU / Sigmoid,
  * on log2 / raw obs (16 features) or one-hot obs (272: the first layer is a gather of W1's rows 17 c + e_c, the
- * one-hot encoding of src/env.py:143-150 read off the bitboard -- no obs buffer).  Packed layout: g2048_deep.hip. */
+ * one-hot encoding of src/env.py:143-150 read off the bitboard -- no obs buffer).  Packed layout: g2048_deep.hip.
+ * ABI 15: a one-hot net's packed form also holds W1 split exactly into three bf16 planes in MFMA fragment order
+ * (g2048_deep_packed_size grows by 12,288 floats per 32-unit tile of layer 0), and every one-hot forward -- policy,
+ * rollout, pattern probe, the update's layer 0 -- computes x W1 as one exact bf16 product per cell and plane,
+ * accumulated hi plane / mid + lo planes, so all of them produce the same bits. */
 #define G2048_DEEP_MAX_HIDDEN 4
 /* floats of the packed net, or -1 if the shape is not covered (hidden: n_hidden sizes) */
 int64_t g2048_deep_packed_size(int obs_mode, int n_hidden, const int32_t* hidden);

@@ -21,7 +21,7 @@ SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
 SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip"), os.path.join(PKG_DIR, "csrc", "g2048_dw2.hip"),
            os.path.join(PKG_DIR, "csrc", "g2048_deep.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 14
+ABI_VERSION = 15
 DEEP_MAX_HIDDEN = 4
 
 # include/g2048.h constants

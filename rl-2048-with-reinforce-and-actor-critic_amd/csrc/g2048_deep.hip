@@ -68,6 +68,7 @@ constexpr int kMaxHidden = G2048_DEEP_MAX_HIDDEN;   // hidden layers
 constexpr int kDeepBlock = 256;                      // 4 waves; two workgroups per CU
 constexpr int kActStride = 33;                       // LDS activation row stride in floats: [unit][32 boards + 1]
 constexpr int kOneHotRows = 272;                     // 16 cells x 17 one-hot features (src/env.py:143-150)
+constexpr int kOneHotPlaneFloats = 16 * 3 * 64 * 4;   // one unit tile's W1 plane fragments
 
 // the hidden unit held by accumulator register r of lane half h of a v_mfma_f32_32x32x2_f32 result tile
 __host__ __device__ inline int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
@@ -80,11 +81,15 @@ __host__ __device__ inline int tile_row(int r, int h) { return (r & 3) + 8 * (r 
 //                     [o][t][q][l][u] = W_l[32 t + 2 s + (l >> 5)][32 o + (l & 31)]
 //   bias l            [32 nt_l]
 //   output layer      [32 nt_{L-1}][4] row-major (a value head is output 0), bias [4]
+//   one-hot W1 planes [nt0][16 cells][3 planes][64 lanes] dwords x 4 (round 5): the A fragment of
+//                     v_mfma_f32_32x32x16_bf16 for unit tile t, cell c, plane p -- lane l holds bf16 plane p of
+//                     W1[17 c + 8 (l >> 5) + j][32 t + (l & 31)], j = 0..7 (split3_bf16: w = p0 + p1 + p2 exactly)
 struct DeepNet {
     int L;                            // hidden layers
     int onehot;                       // first layer is the one-hot gather table
     int nt[kMaxHidden];
     int64_t w[kMaxHidden + 1], b[kMaxHidden + 1];
+    int64_t wpl;                      // one-hot: W1's bf16-plane A fragments (see the layout note above)
     int64_t total;
 };
 
@@ -109,6 +114,8 @@ bool deep_layout(int L, const int* hidden, int onehot, DeepNet& n) {
     off += (int64_t)32 * n.nt[L - 1] * 4;
     n.b[L] = off;
     off += 4;
+    n.wpl = onehot ? off : -1;
+    if (onehot) off += (int64_t)n.nt[0] * kOneHotPlaneFloats;
     n.total = off;
     return true;
 }
@@ -126,6 +133,22 @@ struct DeepPackArgs {
 __global__ void __launch_bounds__(256) deep_pack_kernel(DeepPackArgs a) {
     const DeepNet& n = a.net;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n.total; q += (int64_t)gridDim.x * blockDim.x) {
+        if (n.onehot && q >= n.wpl) {   // W1 plane fragment dword: the same split as onehot_l0_mfma_kernel's
+            const int64_t x = q - n.wpl;
+            const int d = (int)(x & 3), lane = (int)((x >> 2) & 63);
+            const int64_t r = x >> 8;
+            const int p = (int)(r % 3), c = (int)((r / 3) % 16), t = (int)(r / 48);
+            const int hh = lane >> 5, j = 32 * t + (lane & 31);
+            float v8[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; jj++) v8[jj] = j < a.h[0] ? a.W[0][(int64_t)(17 * c + 8 * hh + jj) * a.h[0] + j] : 0.0f;
+            bf16x8 p0, p1, p2;
+            split3_bf16(v8, p0, p1, p2);
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 pv = __builtin_bit_cast(u32x4, p == 0 ? p0 : (p == 1 ? p1 : p2));
+            a.dst[q] = __uint_as_float(pv[d]);
+            continue;
+        }
         float v = 0.0f;
         int l = n.L;
         while (l > 0 && q < n.w[l]) l--;          // the segment: [w[l], b[l]) weights, [b[l], w[l+1]) bias
@@ -330,6 +353,10 @@ __device__ __forceinline__ void dense_fwd_split(const float* in, float* out, con
 #ifndef G2048_DEEP_GATHER_UNROLL
 #define G2048_DEEP_GATHER_UNROLL 4
 #endif
+// deep_forward's one-hot layer 0: 0 = the bf16-plane MFMA form (round 5), 1 = round 4's W1-row gather (A/B builds)
+#ifndef G2048_DEEP_L0_GATHER
+#define G2048_DEEP_L0_GATHER 0
+#endif
 
 // One-hot layer-0 gather of one board: acc[m] += W1 row (17 c + e_c), units 32 (m0 + m) + 4 k .. + 3 (`tab` points
 // at unit 32 m0 + 4 k of row 0), summed over the 16 cells in cell order, for the tiles m < mcount (wave-uniform).
@@ -495,7 +522,50 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
         const int nt0 = net.nt[0];
         if constexpr (A0IN) {
             load_l0_block<kDeepBlock>(a0, n, gi, 32 * nt0, out);
+        } else if constexpr (OBS == G2048_OBS_ONEHOT && !G2048_DEEP_L0_GATHER) {
+            // the update's layer-0 arithmetic (onehot_l0_mfma_kernel), W1's plane fragments streamed from the
+            // packed net: wave w, unit tiles w, w + 4; per cell one exact one-hot B operand and 3 MFMAs (hi plane
+            // into `hi`, the mid and lo planes into `lo`), cell by cell; act((hi + lo) + b1) -- the same bits in
+            // rollout, policy, probe and update, and 32 x 16 x 3 fragments of 1 KiB per tile instead of 16 KiB of
+            // W1 rows per board gathered from L2.  Fragments stream two cells ahead.
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const uint64_t b = S.board[col];
+            const u32x4* fr = reinterpret_cast<const u32x4*>(P + net.wpl) + lane;
+            for (int t = w; t < nt0; t += 4) {   // wave-uniform
+                const u32x4* ft = fr + (int64_t)t * (kOneHotPlaneFloats / 4);
+                float bv[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++) bv[i] = P[net.b[0] + 32 * t + tile_row(i, h)];
+                u32x4 f[3][3];
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+#pragma unroll
+                    for (int pl = 0; pl < 3; pl++) f[q][pl] = ft[(q * 3 + pl) * 64];
+                floatx16 hi = {}, lo = {};
+#pragma unroll
+                for (int c = 0; c < 16; c++) {
+                    if (c + 2 < 16) {
+#pragma unroll
+                        for (int pl = 0; pl < 3; pl++) f[(c + 2) % 3][pl] = ft[((c + 2) * 3 + pl) * 64];
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
+                    u32x4 dv;
+#pragma unroll
+                    for (int jj = 0; jj < 4; jj++)
+                        dv[jj] = (nib == (uint32_t)(8 * h + 2 * jj) ? 0x3F80u : 0u) |
+                                 (nib == (uint32_t)(8 * h + 2 * jj + 1) ? 0x3F800000u : 0u);
+                    const bf16x8 bvv = __builtin_bit_cast(bf16x8, dv);
+                    hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c % 3][0]), bvv, hi, 0, 0, 0);
+                    lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c % 3][1]), bvv, lo, 0, 0, 0);
+                    lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c % 3][2]), bvv, lo, 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    out[(32 * t + tile_row(i, h)) * kActStride + col] = activate<ACT>((hi[i] + lo[i]) + bv[i]);
+            }
         } else if constexpr (OBS == G2048_OBS_ONEHOT) {
+            // (A/B builds, G2048_DEEP_L0_GATHER=1: round 4's gather)
             // wave w: boards 8 w .. 8 w + 7, 8 lanes per board; lane k of a board: units 4 k + 32 m (m < nt0)
             const int bb = 8 * w + (lane >> 3), k = lane & 7;
             const uint64_t b = S.board[bb];

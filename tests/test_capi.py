@@ -164,7 +164,9 @@ def test_deep_sizes_and_validation_without_gpu(L):
         n = (272 * 32 * t[0] if obs == L.OBS_ONEHOT else t[0] * 512) + 32 * t[0]
         for l in range(1, len(hs)):
             n += 1024 * t[l] * t[l - 1] + 32 * t[l]
-        return n + 32 * t[-1] * 4 + 4
+        n += 32 * t[-1] * 4 + 4
+        # one-hot: + W1's bf16-plane A fragments, [nt0][16 cells][3 planes][64 lanes][4 dwords] (round 5)
+        return n + (t[0] * 16 * 3 * 64 * 4 if obs == L.OBS_ONEHOT else 0)
 
     for obs, hs in ((L.OBS_ONEHOT, [256, 128, 64]), (L.OBS_LOG2, [40, 33, 20, 10]), (L.OBS_RAW, [1]),
                     (L.OBS_ONEHOT, [128, 64])):

@@ -178,6 +178,48 @@ def test_deep_choice_equals_g2048_sample(greedy, compact):
     assert float((logits[sel].double() - ref).abs().max() / ref.abs().max()) < 2e-6
 
 
+@pytest.mark.parametrize("h1,act", [(256, "ReLU"), (100, "Sigmoid"), (33, "ReLU")])
+def test_onehot_layer0_bits_equal_plane_emulation(h1, act):
+    """A one-hot net's layer 0 (ABI 15: the update's onehot_l0_mfma_kernel, read here through g2048_deep_hidden,
+    and deep_forward in the rollout / policy kernels run the same arithmetic) bit for bit equal to its definition
+    emulated in torch fp32: W1 split into bf16 planes hi + mid + lo (round to nearest even, exact residuals), per
+    board the hi rows of its 16 cells accumulated from 0 in cell order and, separately, ((acc + mid_c) + lo_c) in cell
+    order -- one fp32 rounding per add, which is what each v_mfma_f32_32x32x16_bf16 with a one-hot B operand does (one
+    exact nonzero product per output) -- then act((hi + lo) + b1)."""
+    L = _lib()
+    from rl2048_amd.agent import _round32
+
+    rng = np.random.default_rng(h1 + 11)
+    W, B = _net(rng, 272, [h1], 4)
+    packed, harr = _pack(L, W, B, L.OBS_ONEHOT, [h1], 4)
+    n = 4000 + 5
+    b, e = _boards(rng, n, hi=15)
+    H = _round32(h1)
+    out = torch.empty(n, H, dtype=torch.float32, device=DEV)
+    code = L.ACT_RELU if act == "ReLU" else L.ACT_SIGMOID
+    L.check(L.lib().g2048_deep_hidden(L.ptr(packed), 1, harr, code, L.OBS_ONEHOT, 1.0, L.ptr(b), n, 0, L.ptr(out), H,
+                                      L.stream_handle(DEV)))
+    w1 = W[0]
+    hi = w1.to(torch.bfloat16).float()
+    r = w1 - hi
+    mid = r.to(torch.bfloat16).float()
+    lo = (r - mid).to(torch.bfloat16).float()
+    assert torch.equal(hi + mid + lo, w1)                # the split is exact
+    rows = torch.from_numpy(17 * np.arange(16) + e).to(DEV)
+    acc_h = torch.zeros(n, h1, dtype=torch.float32, device=DEV)
+    acc_l = torch.zeros_like(acc_h)
+    for c in range(16):
+        acc_h = acc_h + hi[rows[:, c]]
+        acc_l = (acc_l + mid[rows[:, c]]) + lo[rows[:, c]]
+    z = (acc_h + acc_l) + B[0]
+    ref = torch.relu(z) if act == "ReLU" else 1.0 / (1.0 + torch.exp(-z))
+    got = out[:, :h1]
+    if act == "ReLU":
+        assert torch.equal(got, ref)
+    else:   # the kernel's expf / divide against torch's: the pre-activation bits are what is pinned here
+        torch.testing.assert_close(got, ref, rtol=0, atol=2e-7)
+
+
 @pytest.mark.parametrize("h1,act", [(256, "ReLU"), (100, "Sigmoid"), (64, "ReLU"), (1, "ReLU")])
 def test_onehot_layer1_matches_fp64(h1, act):
     L = _lib()
