@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "g2048.h"
 #include "g2048_core.h"
@@ -220,6 +221,7 @@ struct DeepSmem {
 #ifndef G2048_DEEP_CHAIN_WINDOW
 #define G2048_DEEP_CHAIN_WINDOW 1
 #endif
+template <int STRIDE = kActStride>
 __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, const float* in, int t0, int t1, int h,
                                                int col) {
     floatx16 c = {};
@@ -227,11 +229,11 @@ __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, co
     float4 fa[4], fb[4];
 #if G2048_DEEP_CHAIN_WINDOW
     const auto seg = [&](float4& f, int t, int q, int tn) {
-        const float* ib = in + (32 * t + h) * kActStride + col + 8 * q * kActStride;
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, ib[0 * kActStride], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, ib[2 * kActStride], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, ib[4 * kActStride], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, ib[6 * kActStride], c, 0, 0, 0);
+        const float* ib = in + (32 * t + h) * STRIDE + col + 8 * q * STRIDE;
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, ib[0 * STRIDE], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, ib[2 * STRIDE], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, ib[4 * STRIDE], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, ib[6 * STRIDE], c, 0, 0, 0);
         f = fo[tn * 256 + q * 64];
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -255,13 +257,13 @@ __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, co
     }
 #else   // round 4's double buffer (A/B builds)
     const auto tile = [&](const float4 (&f)[4], int t) {
-        const float* ib = in + (32 * t + h) * kActStride + col;
+        const float* ib = in + (32 * t + h) * STRIDE + col;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].x, ib[(8 * q + 0) * kActStride], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].y, ib[(8 * q + 2) * kActStride], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].z, ib[(8 * q + 4) * kActStride], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].w, ib[(8 * q + 6) * kActStride], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].x, ib[(8 * q + 0) * STRIDE], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].y, ib[(8 * q + 2) * STRIDE], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].z, ib[(8 * q + 4) * STRIDE], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].w, ib[(8 * q + 6) * STRIDE], c, 0, 0, 0);
         }
     };
 #pragma unroll
@@ -352,6 +354,10 @@ __device__ __forceinline__ void dense_fwd_split(const float* in, float* out, con
 // present; x 4 tiles for the gradient kernel, x 8 / 2 for deep_forward)
 #ifndef G2048_DEEP_GATHER_UNROLL
 #define G2048_DEEP_GATHER_UNROLL 4
+#endif
+// the one-hot rollout on 64-slot 8-wave workgroups (deep_forward64): 1 on, 0 off = 32-slot 4-wave ones (A/B builds)
+#ifndef G2048_ROLL64
+#define G2048_ROLL64 1
 #endif
 // deep_forward's one-hot layer 0: 0 = the bf16-plane MFMA form (round 5), 1 = round 4's W1-row gather (A/B builds)
 #ifndef G2048_DEEP_L0_GATHER
@@ -659,8 +665,123 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
     FWD_STAMP(dc, 3);
 }
 
+// ---- 64 boards per workgroup (the one-hot rollout, round 5): one 8-wave workgroup per CU over 64 episode slots
+// instead of two 4-wave workgroups of 32 -- every weight fragment (W1 planes, dense layers) is read from L2 once per
+// 64 boards instead of once per 32, and the slot owners' step (logits, choice, env step, trajectory row) runs on
+// all 64 lanes of wave 0.  The same arithmetic per board as deep_forward (one-hot layer 0 by the plane MFMAs, each
+// dense output tile a k-ordered chain, the output partials over the same 8 unit slices), so the rollout stays bit
+// for bit the per-step policy path.
+constexpr int kAct64 = 65;   // LDS row stride in floats: [unit][64 boards + 1]
+struct DeepSmem64 {
+    float act[2][256 * kAct64];
+    float part[8][64][4];
+    uint64_t board[64];
+};
+
+template <int ACT>
+__device__ void deep_forward64(const DeepNet& net, const float* __restrict__ P, DeepSmem64& S, DiagClock* dc) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    // ---- layer 0: wave w owns unit tile w for both 32-board column tiles (one fragment stream, two B operands;
+    //      fragments one cell ahead -- two ahead, or the bias loaded before the chain, spilled beside the four
+    //      accumulator tiles)
+    {
+        float* out = S.act[0];
+        const int nt0 = net.nt[0];
+        if (w < nt0) {   // wave-uniform
+            const int t = w;
+            const uint64_t b0 = S.board[col], b1 = S.board[32 + col];
+            const u32x4* ft = reinterpret_cast<const u32x4*>(P + net.wpl) + lane + (int64_t)t * (kOneHotPlaneFloats / 4);
+            u32x4 f[2][3];
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++) f[0][pl] = ft[pl * 64];
+            floatx16 hi0 = {}, lo0 = {}, hi1 = {}, lo1 = {};
+            const auto onehot_b = [&](uint64_t b, int c) {
+                const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
+                u32x4 dv;
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++)
+                    dv[jj] = (nib == (uint32_t)(8 * h + 2 * jj) ? 0x3F80u : 0u) |
+                             (nib == (uint32_t)(8 * h + 2 * jj + 1) ? 0x3F800000u : 0u);
+                return __builtin_bit_cast(bf16x8, dv);
+            };
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                if (c + 1 < 16) {
+#pragma unroll
+                    for (int pl = 0; pl < 3; pl++) f[(c + 1) & 1][pl] = ft[((c + 1) * 3 + pl) * 64];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const bf16x8 x0 = onehot_b(b0, c), x1 = onehot_b(b1, c);
+                const bf16x8 wh = __builtin_bit_cast(bf16x8, f[c & 1][0]), wm = __builtin_bit_cast(bf16x8, f[c & 1][1]),
+                             wl = __builtin_bit_cast(bf16x8, f[c & 1][2]);
+                hi0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, x0, hi0, 0, 0, 0);
+                hi1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, x1, hi1, 0, 0, 0);
+                lo0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, x0, lo0, 0, 0, 0);
+                lo1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, x1, lo1, 0, 0, 0);
+                lo0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, x0, lo0, 0, 0, 0);
+                lo1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, x1, lo1, 0, 0, 0);
+            }
+            float bv[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) bv[i] = P[net.b[0] + 32 * t + tile_row(i, h)];
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                float* o = out + (32 * t + tile_row(i, h)) * kAct64 + col;
+                o[0] = activate<ACT>((hi0[i] + lo0[i]) + bv[i]);
+                o[32] = activate<ACT>((hi1[i] + lo1[i]) + bv[i]);
+            }
+        }
+    }
+    __syncthreads();
+    FWD_STAMP(dc, 1);
+    // ---- dense layers: item i = (output tile i >> 1, column tile i & 1), items w, w + 8, ..: the two column tiles
+    //      of one output tile on neighbouring waves (other SIMDs), so the second read of each fragment hits L1
+    for (int l = 1; l < net.L; l++) {
+        const float* in = S.act[(l - 1) & 1];
+        float* out = S.act[l & 1];
+        const int ntin = net.nt[l - 1], ntout = net.nt[l];
+        const float4* __restrict__ frag = reinterpret_cast<const float4*>(P + net.w[l]) + lane;
+        for (int i = w; i < 2 * ntout; i += 8) {
+            const int o = i >> 1, cc = i & 1;
+            const floatx16 acc = frag_chain<kAct64>(frag + (int64_t)o * ntin * 256, in + 32 * cc, 0, ntin, h, col);
+            const float* bb = P + net.b[l] + 32 * o;
+            float bv[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) bv[r] = bb[tile_row(r, h)];
+#pragma unroll
+            for (int r = 0; r < 16; r++) out[(32 * o + tile_row(r, h)) * kAct64 + 32 * cc + col] = activate<ACT>(acc[r] + bv[r]);
+        }
+        __syncthreads();
+    }
+    FWD_STAMP(dc, 2);
+    // ---- output layer partials: thread (p = tid >> 6, board = tid & 63), units [p Hp / 8, (p + 1) Hp / 8)
+    {
+        const float* in = S.act[(net.L - 1) & 1];
+        const int Hp = 32 * net.nt[net.L - 1];
+        const int p = threadIdx.x >> 6, bb = threadIdx.x & 63, per = Hp >> 3;
+        const float4* wo = reinterpret_cast<const float4*>(P + net.w[net.L]);
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        for (int j = p * per; j < (p + 1) * per; j++) {
+            const float x = in[j * kAct64 + bb];
+            const float4 wv = wo[j];
+            s0 = fmaf(x, wv.x, s0);
+            s1 = fmaf(x, wv.y, s1);
+            s2 = fmaf(x, wv.z, s2);
+            s3 = fmaf(x, wv.w, s3);
+        }
+        S.part[p][bb][0] = s0;
+        S.part[p][bb][1] = s1;
+        S.part[p][bb][2] = s2;
+        S.part[p][bb][3] = s3;
+    }
+    __syncthreads();
+    FWD_STAMP(dc, 3);
+}
+
 // the 4 outputs of board `bb` from the partials (threads 0..31 after deep_forward)
-__device__ __forceinline__ void deep_logits(const DeepNet& net, const float* __restrict__ P, const DeepSmem& S, int bb,
+template <class Smem>
+__device__ __forceinline__ void deep_logits(const DeepNet& net, const float* __restrict__ P, const Smem& S, int bb,
                                             float lg[4]) {
     const float* bo = P + net.b[net.L];
 #pragma unroll
@@ -836,12 +957,16 @@ __device__ __forceinline__ void store_stream(uint64_t* rs, uint64_t* buf, uint32
 
 constexpr uint32_t kNoEpisode = 0xFFFFFFFFu;
 
-template <int OBS, int ACT>
-__global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArgs a) {
-    __shared__ DeepSmem S;
+// NB = 32: 4-wave workgroups, two per CU, deep_forward; NB = 64 (one-hot nets): one 8-wave workgroup per CU,
+// deep_forward64 (above).  Slot owners: lanes 0 .. NB - 1 of wave 0.
+template <int OBS, int ACT, int NB>
+__global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(DeepRollArgs a) {
+    static_assert(NB == 32 || (NB == 64 && OBS == G2048_OBS_ONEHOT), "64 slots: one-hot nets");
+    typedef typename std::conditional<NB == 64, DeepSmem64, DeepSmem>::type Smem;
+    __shared__ Smem S;
     __shared__ int go;
     const int tid = threadIdx.x;
-    const bool owner = tid < 32;
+    const bool owner = tid < NB;
     const GLine lut{reinterpret_cast<const uint16_t*>(a.tab)};
     const GCode code{a.tab + 2 * 65536};
     uint32_t ep = kNoEpisode, t = 0, sc = 0, mt = 2;
@@ -904,7 +1029,8 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArg
         __syncthreads();
         FWD_STAMP(dc, 0);
         if (!go) break;                                // block-uniform
-        deep_forward<OBS, ACT>(a.net, a.packed, S, a.obs_scale, nullptr, 0, 0, dc);
+        if constexpr (NB == 64) deep_forward64<ACT>(a.net, a.packed, S, dc);
+        else deep_forward<OBS, ACT>(a.net, a.packed, S, a.obs_scale, nullptr, 0, 0, dc);
         if (owner && ep != kNoEpisode) {
             float lg[4];
             deep_logits(a.net, a.packed, S, tid, lg);
@@ -949,7 +1075,7 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_rollout_kernel(DeepRollArg
     }
 #if G2048_DEEP_DIAG
     if (a.diag && (tid & 63) == 0) {
-        uint64_t* slot = a.diag + ((size_t)blockIdx.x * (kDeepBlock / 64) + (tid >> 6)) * kDiagSlots;
+        uint64_t* slot = a.diag + ((size_t)blockIdx.x * (NB / 8) + (tid >> 6)) * kDiagSlots;
 #pragma unroll
         for (int i = 0; i < kDiagSlots; i++) slot[i] += dclk.ph[i];
     }
@@ -1824,9 +1950,9 @@ int check_hip() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : dfail(G2048_EHIP, hipGetErrorString(e));
 }
-template <int OBS, int ACT>
+template <int OBS, int ACT, int NB>
 int launch_deep_roll(const DeepRollArgs& a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((deep_rollout_kernel<OBS, ACT>), dim3(grid), dim3(kDeepBlock), 0, s, a);
+    hipLaunchKernelGGL((deep_rollout_kernel<OBS, ACT, NB>), dim3(grid), dim3(NB * 8), 0, s, a);
     return check_hip();
 }
 
@@ -1982,18 +2108,24 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
     a.tr = *traj;
     a.n = (uint32_t)n;
     a.cap = (uint32_t)cap;
-    int64_t grid = (n_order + 31) / 32;
-    if (grid > 2 * (int64_t)cus) grid = 2 * (int64_t)cus;   // persistent; the slots refill from the queue
     hipStream_t s = (hipStream_t)stream;
     const int obs = cfg->obs_mode;
+    if (obs == G2048_OBS_ONEHOT && G2048_ROLL64) {   // persistent: one workgroup per CU, 64 slots each
+        int64_t grid = (n_order + 63) / 64;
+        if (grid > (int64_t)cus) grid = cus;
+        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_ONEHOT, 0, 64>(a, (int)grid, s)
+                                            : launch_deep_roll<G2048_OBS_ONEHOT, 1, 64>(a, (int)grid, s);
+    }
+    int64_t grid = (n_order + 31) / 32;
+    if (grid > 2 * (int64_t)cus) grid = 2 * (int64_t)cus;   // persistent; the slots refill from the queue
     if (obs == G2048_OBS_ONEHOT)
-        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_ONEHOT, 0>(a, (int)grid, s)
-                                            : launch_deep_roll<G2048_OBS_ONEHOT, 1>(a, (int)grid, s);
+        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_ONEHOT, 0, 32>(a, (int)grid, s)
+                                            : launch_deep_roll<G2048_OBS_ONEHOT, 1, 32>(a, (int)grid, s);
     if (obs == G2048_OBS_LOG2)
-        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_LOG2, 0>(a, (int)grid, s)
-                                            : launch_deep_roll<G2048_OBS_LOG2, 1>(a, (int)grid, s);
-    return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_RAW, 0>(a, (int)grid, s)
-                                        : launch_deep_roll<G2048_OBS_RAW, 1>(a, (int)grid, s);
+        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_LOG2, 0, 32>(a, (int)grid, s)
+                                            : launch_deep_roll<G2048_OBS_LOG2, 1, 32>(a, (int)grid, s);
+    return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_RAW, 0, 32>(a, (int)grid, s)
+                                        : launch_deep_roll<G2048_OBS_RAW, 1, 32>(a, (int)grid, s);
 }
 
 int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, int activation, int obs_mode,

@@ -20,6 +20,7 @@ ap.add_argument("--episodes", type=int, default=262144)
 ap.add_argument("--lib", default="tools/libg2048_deepdiag.so")
 ap.add_argument("--label", default="")
 ap.add_argument("--rollout", action="store_true", help="stamp the rollout (deep_rollout_kernel) instead of the update")
+ap.add_argument("--rollout-waves", type=int, default=8, help="waves per rollout workgroup (8: 64 slots, 4: 32 slots)")
 args = ap.parse_args()
 from rl2048_amd import _lib as L  # noqa: E402
 
@@ -48,8 +49,8 @@ buf = torch.zeros(slots, dtype=torch.int64, device=dev)
 E = args.episodes
 RPHASES = ["top+boards", "layer0", "dense", "out_partials", "owners", "claim"]
 for rep in range(2 if args.rollout else 0):
-    # deep_rollout_kernel: per step of a workgroup, wave 0 (whose lanes 0..31 own the episode slots: logits, choice,
-    # env step, trajectory row) and waves 1..3 (which wait for it at the next step's first barrier)
+    # deep_rollout_kernel: per step of a workgroup, wave 0 (whose lanes own the episode slots: logits, choice, env
+    # step, trajectory row) and the other waves (which wait for it at the next step's first barrier)
     es = np.arange(3 + rep * E, 3 + (rep + 1) * E, dtype=np.int64)
     torch.cuda.synchronize()
     buf.zero_()
@@ -57,11 +58,12 @@ for rep in range(2 if args.rollout else 0):
     batch = agent.rollout_batch(es, es + 7 * E)
     torch.cuda.synchronize()
     lib.g2048_diag_deep_stamps(None)
-    d = buf.view(-1, 4, 10).cpu().numpy().astype(np.float64)
+    W = args.rollout_waves
+    d = buf.view(-1, W, 10).cpu().numpy().astype(np.float64)
     d = d[d[:, 0, 9] > 0]
     out = {"label": args.label, "rep": rep, "episodes": E, "steps": int(batch.lengths.sum()), "workgroups": int(d.shape[0]),
            "steps_per_workgroup": float(d[:, 0, 9].mean())}
-    for name, ws in (("wave0", [0]), ("waves1_3", [1, 2, 3])):
+    for name, ws in (("wave0", [0]), ("waves1_%d" % (W - 1), list(range(1, W)))):
         per = (d[:, ws, :6] / d[:, ws, 9:10]).reshape(-1, 6).mean(axis=0)
         out[name] = {"cycles_per_step": round(per.sum()), "phases_cycles": {p: round(v) for p, v in zip(RPHASES, per)}}
     print(json.dumps(out), flush=True)
