@@ -359,6 +359,11 @@ __device__ __forceinline__ void dense_fwd_split(const float* in, float* out, con
 #ifndef G2048_ROLL64
 #define G2048_ROLL64 1
 #endif
+// deep_forward64's layer-0 fragment window in cells: 1 (2 measured 0.2606-0.2615 s against 0.2595-0.2599 s,
+// `profiles/round5/r6a/`; 3 spills)
+#ifndef G2048_ROLL64_L0_AHEAD
+#define G2048_ROLL64_L0_AHEAD 1
+#endif
 // deep_forward's one-hot layer 0: 0 = the bf16-plane MFMA form (round 5), 1 = round 4's W1-row gather (A/B builds)
 #ifndef G2048_DEEP_L0_GATHER
 #define G2048_DEEP_L0_GATHER 0
@@ -683,8 +688,8 @@ __device__ void deep_forward64(const DeepNet& net, const float* __restrict__ P, 
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     // ---- layer 0: wave w owns unit tile w for both 32-board column tiles (one fragment stream, two B operands;
-    //      fragments one cell ahead -- two ahead, or the bias loaded before the chain, spilled beside the four
-    //      accumulator tiles)
+    //      fragments G2048_ROLL64_L0_AHEAD cells ahead; the bias is loaded after the chain, beside which the four
+    //      accumulator tiles are live)
     {
         float* out = S.act[0];
         const int nt0 = net.nt[0];
@@ -692,9 +697,12 @@ __device__ void deep_forward64(const DeepNet& net, const float* __restrict__ P, 
             const int t = w;
             const uint64_t b0 = S.board[col], b1 = S.board[32 + col];
             const u32x4* ft = reinterpret_cast<const u32x4*>(P + net.wpl) + lane + (int64_t)t * (kOneHotPlaneFloats / 4);
-            u32x4 f[2][3];
+            constexpr int kAhead = G2048_ROLL64_L0_AHEAD;   // cells of fragments in flight ahead of the MFMAs
+            u32x4 f[kAhead + 1][3];
 #pragma unroll
-            for (int pl = 0; pl < 3; pl++) f[0][pl] = ft[pl * 64];
+            for (int q = 0; q < kAhead; q++)
+#pragma unroll
+                for (int pl = 0; pl < 3; pl++) f[q][pl] = ft[(q * 3 + pl) * 64];
             floatx16 hi0 = {}, lo0 = {}, hi1 = {}, lo1 = {};
             const auto onehot_b = [&](uint64_t b, int c) {
                 const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
@@ -707,14 +715,15 @@ __device__ void deep_forward64(const DeepNet& net, const float* __restrict__ P, 
             };
 #pragma unroll
             for (int c = 0; c < 16; c++) {
-                if (c + 1 < 16) {
+                if (c + kAhead < 16) {
 #pragma unroll
-                    for (int pl = 0; pl < 3; pl++) f[(c + 1) & 1][pl] = ft[((c + 1) * 3 + pl) * 64];
+                    for (int pl = 0; pl < 3; pl++) f[(c + kAhead) % (kAhead + 1)][pl] = ft[((c + kAhead) * 3 + pl) * 64];
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 const bf16x8 x0 = onehot_b(b0, c), x1 = onehot_b(b1, c);
-                const bf16x8 wh = __builtin_bit_cast(bf16x8, f[c & 1][0]), wm = __builtin_bit_cast(bf16x8, f[c & 1][1]),
-                             wl = __builtin_bit_cast(bf16x8, f[c & 1][2]);
+                const int fs = c % (kAhead + 1);
+                const bf16x8 wh = __builtin_bit_cast(bf16x8, f[fs][0]), wm = __builtin_bit_cast(bf16x8, f[fs][1]),
+                             wl = __builtin_bit_cast(bf16x8, f[fs][2]);
                 hi0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, x0, hi0, 0, 0, 0);
                 hi1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, x1, hi1, 0, 0, 0);
                 lo0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, x0, lo0, 0, 0, 0);
@@ -965,6 +974,7 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
     typedef typename std::conditional<NB == 64, DeepSmem64, DeepSmem>::type Smem;
     __shared__ Smem S;
     __shared__ int go;
+    __shared__ uint32_t park[NB == 64 ? 28 : 1][64];
     const int tid = threadIdx.x;
     const bool owner = tid < NB;
     const GLine lut{reinterpret_cast<const uint16_t*>(a.tab)};
@@ -1029,8 +1039,33 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
         __syncthreads();
         FWD_STAMP(dc, 0);
         if (!go) break;                                // block-uniform
-        if constexpr (NB == 64) deep_forward64<ACT>(a.net, a.packed, S, dc);
-        else deep_forward<OBS, ACT>(a.net, a.packed, S, a.obs_scale, nullptr, 0, 0, dc);
+        if constexpr (NB == 64) {
+            // the slots' episode state (28 words) parked in LDS across the forward and read back by every thread
+            // (the non-owners' copies are never used), so its registers are free for the forward's fragment
+            // windows -- the 8-wave kernel is at 256 VGPRs
+            const int sl = tid & 63;
+            const auto put = [&](int k, uint32_t v) { park[k][sl] = v; };
+            const auto put64 = [&](int k, uint64_t v) { put(k, (uint32_t)v); put(k + 1, (uint32_t)(v >> 32)); };
+            if (owner) {
+                put(0, ep); put(1, t); put(2, sc); put(3, mt);
+                put64(4, b); put64(6, (uint64_t)__double_as_longlong(total));
+                put64(8, ge.s_lo); put64(10, ge.s_hi); put64(12, ge.i_lo); put64(14, ge.i_hi);
+                put(16, ge.has_uint32); put(17, ge.uinteger);
+                put64(18, gp.s_lo); put64(20, gp.s_hi); put64(22, gp.i_lo); put64(24, gp.i_hi);
+                put(26, gp.has_uint32); put(27, gp.uinteger);
+            }
+            deep_forward64<ACT>(a.net, a.packed, S, dc);   // (its barriers order the parking)
+            const auto get = [&](int k) { return park[k][sl]; };
+            const auto get64 = [&](int k) { return (uint64_t)get(k) | ((uint64_t)get(k + 1) << 32); };
+            ep = get(0); t = get(1); sc = get(2); mt = get(3);
+            b = get64(4); total = __longlong_as_double((long long)get64(6));
+            ge.s_lo = get64(8); ge.s_hi = get64(10); ge.i_lo = get64(12); ge.i_hi = get64(14);
+            ge.has_uint32 = get(16); ge.uinteger = get(17);
+            gp.s_lo = get64(18); gp.s_hi = get64(20); gp.i_lo = get64(22); gp.i_hi = get64(24);
+            gp.has_uint32 = get(26); gp.uinteger = get(27);
+        } else {
+            deep_forward<OBS, ACT>(a.net, a.packed, S, a.obs_scale, nullptr, 0, 0, dc);
+        }
         if (owner && ep != kNoEpisode) {
             float lg[4];
             deep_logits(a.net, a.packed, S, tid, lg);
