@@ -1154,13 +1154,58 @@ constexpr int kDeepGradMaxBlock = 512;
 #ifndef G2048_DEEP_LOG2_64
 #define G2048_DEEP_LOG2_64 0
 #endif
-// the one-hot gradient kernel's next-group layer-0 prefetch: 1 on, 0 off (A/B builds)
+// the one-hot gradient kernel's layer 0 computed in the kernel from W1's packed planes (1) instead of read back
+// from onehot_l0_mfma_kernel's blocks (0, with the next-group LDS-DMA prefetch below) -- A/B builds.  Fused measured
+// 1.363-1.365 s against 1.355-1.359 s (`profiles/round5/r6b/`): the separate kernel's 0.126 s go, but the group
+// grows 105.7 k -> 118.3 k cycles (the plane stream one cell ahead is latency-bound beside 10 accumulator tiles)
+#ifndef G2048_DEEP_L0_FUSED
+#define G2048_DEEP_L0_FUSED 0
+#endif
+// the one-hot gradient kernel's next-group layer-0 prefetch (unfused layer 0 only): 1 on, 0 off (A/B builds)
 #ifndef G2048_DEEP_L0_PREFETCH
 #define G2048_DEEP_L0_PREFETCH 1
 #endif
 #ifndef G2048_DEEP_D0_UNROLL   // the delta_0 row stores per batch
 #define G2048_DEEP_D0_UNROLL 32
 #endif
+// One unit tile t of a one-hot layer 0 for 32 boards (lane col: board b) by the exact bf16-plane MFMAs of
+// onehot_l0_mfma_kernel (same bits), W1's plane fragments streamed from the packed net one cell ahead, the bias
+// loaded after the chain; writes act((hi + lo) + b1) to out[unit * stride + col].  The gradient kernel's fused
+// layer 0 (G2048_DEEP_L0_FUSED).
+template <int ACT>
+__device__ __forceinline__ void onehot_l0_tile(const float* __restrict__ P, const DeepNet& net, int t, uint64_t b,
+                                               float* out, int stride) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    const u32x4* ft = reinterpret_cast<const u32x4*>(P + net.wpl) + lane + (int64_t)t * (kOneHotPlaneFloats / 4);
+    u32x4 f[2][3];
+#pragma unroll
+    for (int pl = 0; pl < 3; pl++) f[0][pl] = ft[pl * 64];
+    floatx16 hi = {}, lo = {};
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        if (c + 1 < 16) {
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++) f[(c + 1) & 1][pl] = ft[((c + 1) * 3 + pl) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
+        u32x4 dv;
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++)
+            dv[jj] = (nib == (uint32_t)(8 * h + 2 * jj) ? 0x3F80u : 0u) | (nib == (uint32_t)(8 * h + 2 * jj + 1) ? 0x3F800000u : 0u);
+        const bf16x8 bvv = __builtin_bit_cast(bf16x8, dv);
+        hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][0]), bvv, hi, 0, 0, 0);
+        lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][1]), bvv, lo, 0, 0, 0);
+        lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][2]), bvv, lo, 0, 0, 0);
+    }
+    float bv[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) bv[i] = P[net.b[0] + 32 * t + tile_row(i, h)];
+#pragma unroll
+    for (int i = 0; i < 16; i++) out[(32 * t + tile_row(i, h)) * stride + col] = activate<ACT>((hi[i] + lo[i]) + bv[i]);
+}
+
 struct DeepGradVariant {
     int nw, tpw, ksplit, per_cu;
 };
@@ -1287,7 +1332,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     // would drain the DMA there), and the next group's first barrier retires it.  Its forward then only re-strides
     // the block from LDS (the load had been 10 % of the group).  Whole groups only; the launch's last, ragged group
     // reads its block in place.
-    constexpr bool kPrefetch = OBS == G2048_OBS_ONEHOT && G2048_DEEP_L0_PREFETCH;
+    constexpr bool kPrefetch = OBS == G2048_OBS_ONEHOT && G2048_DEEP_L0_PREFETCH && !G2048_DEEP_L0_FUSED;
     const int H0a = 32 * net.nt[0];
     float* stage = dyn + a.aoff[0] + H0a * kActStride;   // [unit][32]: deep_grad_act_floats leaves room
     const auto whole = [&](uint32_t g) { return g < groups && a.n - g * 32u >= 32u; };
@@ -1334,7 +1379,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             if constexpr (OBS == G2048_OBS_ONEHOT) {
                 // the group's block from onehot_l0_mfma_kernel (in d0_out: this workgroup overwrites the same rows
                 // with the group's layer-0 deltas at its end)
-                if (kPrefetch && whole(gi)) {   // the staged block (its DMA retired by the barrier above)
+                if constexpr (G2048_DEEP_L0_FUSED) {
+                    for (int t = w; t < nt0; t += NW) onehot_l0_tile<ACT>(P, net, t, bds[col], out, kActStride);
+                } else if (kPrefetch && whole(gi)) {   // the staged block (its DMA retired by the barrier above)
                     const float4* st4 = reinterpret_cast<const float4*>(stage);
 #pragma unroll 4
                     for (int e4 = tid; e4 < 8 * H0a; e4 += kBlock) {
@@ -1717,7 +1764,7 @@ int64_t deep_grad_act_floats(const DeepNet& n, int nw) {
     int64_t f = units * kActStride;
     const int64_t red = 5 * 64 * nw;
     if (red > f) f = red;
-    if (n.onehot && G2048_DEEP_L0_PREFETCH) {
+    if (n.onehot && G2048_DEEP_L0_PREFETCH && !G2048_DEEP_L0_FUSED) {
         const int64_t st = 32 * n.nt[0] * (kActStride + 32);
         if (st > f) f = st;
     }
@@ -2359,7 +2406,7 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
     const int64_t lds = deep_grad_lds_bytes(net, v.nw);
     hipStream_t s = (hipStream_t)stream;
     const int grid = (int)nparts;   // every workgroup writes its slab (zeros when it gets no group)
-    if (obs_mode == G2048_OBS_ONEHOT && n > 0) {   // layer 0 on the bf16 MFMA, into d0_out (group blocks)
+    if (obs_mode == G2048_OBS_ONEHOT && n > 0 && !G2048_DEEP_L0_FUSED) {   // layer 0 on the bf16 MFMA, into d0_out
         const int rc = launch_onehot_l0(net, packed, boards, (uint32_t)n, activation, d0_out, s);
         if (rc) return rc;
     }
