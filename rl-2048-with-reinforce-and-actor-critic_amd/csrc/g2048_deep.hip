@@ -79,7 +79,10 @@ __host__ __device__ inline int tile_row(int r, int h) { return (r & 3) + 8 * (r 
 //   layer 0 weights   one-hot: table [272][32 nt0] row-major (row 17 c + e = W1[17 c + e, :]);
 //                     else:    A fragments [nt0][8][64] (k-step s, lane l: W1[2 s + (l >> 5)][32 t + (l & 31)])
 //   layer l >= 1      A fragments [nt_l][nt_{l-1}][4][64][4]: output tile o, k-tile t, lane l, k-step s = 4 q + u at
-//                     [o][t][q][l][u] = W_l[32 t + 2 s + (l >> 5)][32 o + (l & 31)]
+//                     [o][t][q][l][u] = W_l[32 t + tile_row(s, l >> 5)][32 o + (l & 31)] -- k-step s takes the input
+//                     units an MFMA result tile holds in its register s (round 5), so a wave's accumulator tile of
+//                     layer l - 1 is register for register the B operand of layer l (deep_rollout_wave_kernel);
+//                     the LDS-fed chains read the same rows (frag_chain)
 //   bias l            [32 nt_l]
 //   output layer      [32 nt_{L-1}][4] row-major (a value head is output 0), bias [4]
 //   one-hot W1 planes [nt0][16 cells][3 planes][64 lanes] dwords x 4 (round 5): the A fragment of
@@ -181,7 +184,7 @@ __global__ void __launch_bounds__(256) deep_pack_kernel(DeepPackArgs a) {
             const int u = (int)(x & 3), lane = (int)((x >> 2) & 63), qq = (int)((x >> 8) & 3);
             const int64_t tt = x >> 10;
             const int t = (int)(tt % n.nt[l - 1]), o = (int)(tt / n.nt[l - 1]);
-            const int k = 32 * t + 2 * (4 * qq + u) + (lane >> 5), j = 32 * o + (lane & 31);
+            const int k = 32 * t + tile_row(4 * qq + u, lane >> 5), j = 32 * o + (lane & 31);
             v = (k < a.h[l - 1] && j < a.h[l]) ? a.W[l][(int64_t)k * a.h[l] + j] : 0.0f;
         }
         a.dst[q] = v;
@@ -229,11 +232,11 @@ __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, co
     float4 fa[4], fb[4];
 #if G2048_DEEP_CHAIN_WINDOW
     const auto seg = [&](float4& f, int t, int q, int tn) {
-        const float* ib = in + (32 * t + h) * STRIDE + col + 8 * q * STRIDE;
+        const float* ib = in + (32 * t + 4 * h) * STRIDE + col + 8 * q * STRIDE;   // k-step 4 q + u: row 8 q + u + 4 h
         c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, ib[0 * STRIDE], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, ib[2 * STRIDE], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, ib[4 * STRIDE], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, ib[6 * STRIDE], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, ib[1 * STRIDE], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, ib[2 * STRIDE], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, ib[3 * STRIDE], c, 0, 0, 0);
         f = fo[tn * 256 + q * 64];
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -257,13 +260,13 @@ __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, co
     }
 #else   // round 4's double buffer (A/B builds)
     const auto tile = [&](const float4 (&f)[4], int t) {
-        const float* ib = in + (32 * t + h) * STRIDE + col;
+        const float* ib = in + (32 * t + 4 * h) * STRIDE + col;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].x, ib[(8 * q + 0) * STRIDE], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].y, ib[(8 * q + 2) * STRIDE], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].z, ib[(8 * q + 4) * STRIDE], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].w, ib[(8 * q + 6) * STRIDE], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].y, ib[(8 * q + 1) * STRIDE], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].z, ib[(8 * q + 2) * STRIDE], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].w, ib[(8 * q + 3) * STRIDE], c, 0, 0, 0);
         }
     };
 #pragma unroll
@@ -1694,7 +1697,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
 }
 
 // backward fragments of the dense layers: layer l (1..L-1) at boff[l], [nt_{l-1}][nt_l][4][64][4]: output tile o
-// (a unit tile of layer l-1), k-tile t (of layer l), lane, k-step s = 4 q + u -> W_l[32 o + (lane & 31)][32 t + 2 s + (lane >> 5)]
+// (a unit tile of layer l-1), k-tile t (of layer l), lane, k-step s = 4 q + u -> W_l[32 o + (lane & 31)][32 t + tile_row(s, lane >> 5)]
+// (the k order of frag_chain, as the forward fragments)
 struct DeepGradPackArgs {
     const float* W[kMaxHidden];
     int h[kMaxHidden];
@@ -1713,7 +1717,7 @@ __global__ void __launch_bounds__(256) deep_grad_pack_kernel(DeepGradPackArgs a)
         const int u = (int)(x & 3), lane = (int)((x >> 2) & 63), qq = (int)((x >> 8) & 3);
         const int64_t tt = x >> 10;
         const int t = (int)(tt % a.nt[l]), o = (int)(tt / a.nt[l]);
-        const int i = 32 * o + (lane & 31), k = 32 * t + 2 * (4 * qq + u) + (lane >> 5);
+        const int i = 32 * o + (lane & 31), k = 32 * t + tile_row(4 * qq + u, lane >> 5);
         a.dst[q] = (i < a.h[l - 1] && k < a.h[l]) ? a.W[l][(int64_t)i * a.h[l] + k] : 0.0f;
     }
 }
