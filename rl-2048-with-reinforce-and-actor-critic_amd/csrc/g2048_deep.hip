@@ -81,8 +81,8 @@ __host__ __device__ inline int tile_row(int r, int h) { return (r & 3) + 8 * (r 
 //   layer l >= 1      A fragments [nt_l][nt_{l-1}][4][64][4]: output tile o, k-tile t, lane l, k-step s = 4 q + u at
 //                     [o][t][q][l][u] = W_l[32 t + tile_row(s, l >> 5)][32 o + (l & 31)] -- k-step s takes the input
 //                     units an MFMA result tile holds in its register s (round 5), so a wave's accumulator tile of
-//                     layer l - 1 is register for register the B operand of layer l (deep_rollout_wave_kernel);
-//                     the LDS-fed chains read the same rows (frag_chain)
+//                     layer l - 1 can be the B operand of layer l register for register (the two-layer
+//                     g2048_policy's layout); the LDS-fed chains read the same rows (frag_chain)
 //   bias l            [32 nt_l]
 //   output layer      [32 nt_{L-1}][4] row-major (a value head is output 0), bias [4]
 //   one-hot W1 planes [nt0][16 cells][3 planes][64 lanes] dwords x 4 (round 5): the A fragment of
