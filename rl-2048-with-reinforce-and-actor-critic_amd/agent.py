@@ -281,6 +281,9 @@ class ReinforceAgent:
         # two-layer log2 / raw nets through the cooperative g2048_actor_grad / g2048_critic_grad kernels (+ g2048_dw2);
         # False routes them to g2048_deep_grad where it covers the net (tools/bench_update.py --deep-grad A/B)
         self.use_two_layer_grad = True
+        # nets past g2048_deep_grad's one-launch tile budget through it anyway, one launch per tile range (tests);
+        # off: they take the gather + hipBLASLt path, which measured faster for them (_deep_grad_spec)
+        self.deep_grad_multi_launch = False
         # ... and the fused critic per time row, V(s') taken from the next row's pass (large batches)
         self.use_critic_rows = True
         self.critic_factored_d2 = True   # ReLU critic rows: the factored d2 records + g2048_dw2_factored
@@ -558,11 +561,19 @@ class ReinforceAgent:
         self._fold(part, acc)
 
     def _deep_grad_spec(self, params, out_dim: int):
-        """_deep_spec when g2048_deep_grad covers the net (at most 64 dense 32x32 weight-gradient tiles), else None."""
+        """_deep_spec when g2048_deep_grad covers the net in one launch per chunk (at most 64 dense 32x32
+        weight-gradient tiles on one-hot obs, 48 on log2 / raw), else None.  Larger nets run it as one launch per
+        range of tiles (each redoing the forward and delta chains) only with deep_grad_multi_launch: measured slower
+        than the gather + hipBLASLt path for one-hot [256, 256, 256] (update 1.37 s against 1.15 s at 262,144
+        episodes, profiles/round5/r6e/)."""
         if not self.use_fused_grad:
             return None
         d = self._deep_spec(params, out_dim)
         if d is None or int(self._lib.g2048_deep_grad_slab(d[0], len(d[1]), d[3])) < 0:
+            return None
+        t = [(h + 31) // 32 for h in d[1]]
+        tiles = sum(t[l - 1] * t[l] for l in range(1, len(t)))
+        if tiles > (64 if d[0] == L.OBS_ONEHOT else 48) and not self.deep_grad_multi_launch:
             return None
         return d
 

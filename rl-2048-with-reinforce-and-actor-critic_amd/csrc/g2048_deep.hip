@@ -1210,7 +1210,7 @@ __device__ __forceinline__ void onehot_l0_tile(const float* __restrict__ P, cons
 }
 
 struct DeepGradVariant {
-    int nw, tpw, ksplit, per_cu;
+    int nw, tpw, ksplit, per_cu, passes;   // passes > 1: the dense dW tiles in ranges of nw x tpw, one launch each
 };
 
 struct DeepGradArgs {
@@ -1240,6 +1240,8 @@ struct DeepGradArgs {
     int aoff[kMaxHidden];         // LDS float offset of layer l's activations / deltas
     int lds_tail;                 // LDS float offset of the output partials, g, boards and bias sums
     uint64_t* diag;               // -DG2048_DEEP_DIAG=1 builds only (tools/diag_deep.py): per-wave phase cycles
+    int tile0;                    // this launch's dense dW tiles: [tile0, tile0 + NW TPW) (nets past one pass)
+    int first_pass, last_pass;    // first: writes the bias / output-layer / first-layer partials; last: delta_0 rows
 };
 
 // Phase-time attribution (tools-only build, -DG2048_DEEP_DIAG=1): each wave adds the s_memtime cycles of every
@@ -1544,7 +1546,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             const int f0 = a.tile_begin[l], f1 = f0 + ntin * ntout;
 #pragma unroll
             for (int k = 0; k < TPW; k++) {
-                const int f = w + NW * k;
+                const int f = a.tile0 + w + NW * k;
                 if (f >= f0 && f < f1) {                     // wave-uniform
                     const int ti = (f - f0) / ntout, tj = (f - f0) % ntout;
                     const float* ap = A + (32 * ti + col) * kActStride + h;
@@ -1584,9 +1586,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             if (whole(gi + gridDim.x)) prefetch(gi + gridDim.x);   // the deeper layers' LDS is dead from here on
         }
         if constexpr (OBS == G2048_OBS_ONEHOT) {
-            // delta_0 out for the one-hot scatter (g2048_onehot_dw1): row j, unit tid (coalesced rows)
+            // delta_0 out for the one-hot scatter (g2048_onehot_dw1): row j, unit tid (coalesced rows) -- by the last
+            // launch only (the earlier ones still read the layer-0 blocks these rows overwrite)
             const int H0 = 32 * net.nt[0];
-            if (tid < H0) {
+            if (tid < H0 && a.last_pass) {
                 // through a buffer resource over the group's rows (base and row offsets in SGPRs, no 64-bit
                 // per-lane address to keep live; the rows past a ragged group's end fall outside num_records)
                 const float* drow = actl(0) + tid * kActStride;
@@ -1664,7 +1667,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     float* out = a.part + (size_t)blockIdx.x * a.pslab;
 #pragma unroll
     for (int k = 0; k < TPW; k++) {
-        const int f = w + NW * k;
+        const int f = a.tile0 + w + NW * k;
         if (f < a.ntiles) {
             int l = 1;
             while (l + 1 < L && f >= a.tile_begin[l + 1]) l++;
@@ -1676,6 +1679,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 out[a.pw[l] + (int64_t)(32 * ti + tile_row(r, h)) * Ho + 32 * tj + col] = acc[k][r];
         }
     }
+    if (!a.first_pass) return;   // the launches after the first write their dense tiles only
     if constexpr (OBS != G2048_OBS_ONEHOT) {
         const int H0 = 32 * net.nt[0];
 #pragma unroll
@@ -1783,10 +1787,18 @@ int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, 
 // of 10 or 8 dense tiles per wave, hipcc spills whole accumulator tiles (~300-650 VGPRs).
 DeepGradVariant deep_grad_variant(const DeepNet& n) {
     const int tiles = deep_grad_layout(n).ntiles;
-    if (n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024) return {4, 10, G2048_DEEP_SPLIT4 ? 2 : 0, 2};
-    if (tiles <= 48 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 6, 1, 1};
-    if ((n.onehot || G2048_DEEP_LOG2_64) && tiles <= 64 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 8, 1, 1};
-    return {0, 0, 0, 0};
+    if (n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024) return {4, 10, G2048_DEEP_SPLIT4 ? 2 : 0, 2, 1};
+    if (tiles <= 48 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 6, 1, 1, 1};
+    if ((n.onehot || G2048_DEEP_LOG2_64) && tiles <= 64 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 8, 1, 1, 1};
+    // past one launch's accumulator budget (round 5; e.g. one-hot [256, 256, 256], log2 [256, 256]): the dense dW
+    // tiles in ranges, one launch per range, each redoing the forward and the delta chains (the dW MFMAs, a third
+    // of the work, are split); 64 tiles per launch on one-hot nets, 48 on log2 / raw (whose 8 x 8 instantiation
+    // spills)
+    if (deep_grad_lds_bytes(n, 8) <= 160 * 1024) {
+        const int cap = n.onehot ? 64 : 48;
+        return {8, n.onehot ? 8 : 6, 1, 1, (tiles + cap - 1) / cap};
+    }
+    return {0, 0, 0, 0, 0};
 }
 
 // ------------------------------------------------------------------------------------ one-hot layer 1 (update)
@@ -2333,7 +2345,7 @@ int launch_deep_grad_v(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t
 }
 
 template <int OBS, int ACT>
-int launch_deep_grad(const DeepGradArgs& a, const DeepGradVariant& v, int grid, int64_t lds, hipStream_t s) {
+int launch_deep_grad_pass(const DeepGradArgs& a, const DeepGradVariant& v, int grid, int64_t lds, hipStream_t s) {
     if constexpr (OBS == G2048_OBS_ONEHOT) {
         if (v.nw == 4) return launch_deep_grad_v<OBS, ACT, 4, 10, G2048_DEEP_SPLIT4 ? 2 : 0>(a, grid, lds, s);
         if (v.tpw == 8) return launch_deep_grad_v<OBS, ACT, 8, 8, 1>(a, grid, lds, s);
@@ -2341,6 +2353,20 @@ int launch_deep_grad(const DeepGradArgs& a, const DeepGradVariant& v, int grid, 
         if (v.tpw == 8) return launch_deep_grad_v<OBS, ACT, 8, 8, 1>(a, grid, lds, s);
     }
     return launch_deep_grad_v<OBS, ACT, 8, 6, 1>(a, grid, lds, s);
+}
+// one launch per range of dense dW tiles (v.passes; one for every net within the accumulator budget): each writes
+// its tiles' partials, the first also the bias / output / first-layer ones, so the slab is complete after the last
+template <int OBS, int ACT>
+int launch_deep_grad(const DeepGradArgs& a0, const DeepGradVariant& v, int grid, int64_t lds, hipStream_t s) {
+    DeepGradArgs a = a0;
+    for (int p = 0; p < v.passes; p++) {
+        a.tile0 = p * v.nw * v.tpw;
+        a.first_pass = p == 0;
+        a.last_pass = p == v.passes - 1;
+        const int rc = launch_deep_grad_pass<OBS, ACT>(a, v, grid, lds, s);
+        if (rc) return rc;
+    }
+    return G2048_OK;
 }
 }  // namespace
 

@@ -181,10 +181,15 @@ def test_deep_sizes_and_validation_without_gpu(L):
         t = [_round32(h) // 32 for h in hs]
         nb = sum(t[l] * t[l - 1] * 1024 for l in range(1, len(hs)))
         assert lib.g2048_deep_grad_pack_size(obs, len(hs), arr(hs)) == max(nb, 1)
-    # past 64 tiles; log2 / raw nets past 48 tiles (their 64-tile instantiation would spill, see g2048_deep.hip --
-    # log2 [256, 256] is the two-layer fused kernels' net anyway)
+    # past one launch's accumulator budget (64 tiles one-hot, 48 log2 / raw): covered by one launch per tile range
+    # (round 5), the same slab
     for obs, hs in ((L.OBS_ONEHOT, [256, 256, 256]), (L.OBS_ONEHOT, [256, 256, 32]), (L.OBS_LOG2, [256, 256]),
-                    (L.OBS_LOG2, [32] * 5)):
+                    (L.OBS_ONEHOT, [256] * 4)):
+        pw, pb = ReinforceAgent._deep_slab_layout(hs, obs == L.OBS_ONEHOT)
+        assert lib.g2048_deep_grad_slab(obs, len(hs), arr(hs)) == pb[-1] + 4, (obs, hs)
+        assert lib.g2048_deep_grad_parts(obs, len(hs), arr(hs)) > 0, (obs, hs)
+    # not a net of the any-depth kernels at all (5 hidden layers)
+    for obs, hs in ((L.OBS_LOG2, [32] * 5),):
         assert lib.g2048_deep_grad_slab(obs, len(hs), arr(hs)) == -1, (obs, hs)
         assert lib.g2048_deep_grad_parts(obs, len(hs), arr(hs)) == -1, (obs, hs)
     # workgroups that fill the chip: two 4-wave workgroups per CU for one-hot nets of <= 40 tiles, else one

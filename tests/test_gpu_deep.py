@@ -358,7 +358,12 @@ def test_deep_rollout_suspend_resume_equals_stepwise(env, hidden):
                                                    (dict(obs_mode="log2", obs_log2_scale=0.0625, max_steps=None),
                                                     [64, 48, 32], "ReLU", True),
                                                    # round 5: 64 dense tiles (the 8-wave, 8-tiles-per-wave kernel)
-                                                   (REFCONF_ENV, [256, 256], "ReLU", True)])
+                                                   (REFCONF_ENV, [256, 256], "ReLU", True),
+                                                   # round 5: 128 tiles, two launches (one per range of 64 dW tiles)
+                                                   (dict(REFCONF_ENV, max_steps=300), [256, 256, 256], "ReLU", True),
+                                                   # 80 log2 tiles, two launches of <= 48 (Sigmoid, a 3-layer net)
+                                                   (dict(obs_mode="log2", obs_log2_scale=0.0625, max_steps=300),
+                                                    [256, 256, 64], "Sigmoid", False)])
 def test_deep_update_at_size_vs_fp64(env, hidden, act, critic, fused, rows):
     """update_from_batch on nets the register-specialised kernels do not cover (the reference runner's documented
     config first: one-hot obs, 256-128-64, actor-critic) over 16,384 episodes of its own rollout: the pre-clip
@@ -376,6 +381,7 @@ def test_deep_update_at_size_vs_fp64(env, hidden, act, critic, fused, rows):
     a = _agent(env, hidden, act, baseline_mode="batch", gamma=0.99, use_critic=critic, optimizer="adam",
                learning_rate=0.01, critic_learning_rate=5e-4)
     a.use_fused_grad = fused
+    a.deep_grad_multi_launch = True   # nets past one launch's tile budget: the multi-launch form under test
     if rows:
         a.critic_rows_min_avg = 0
         a.critic_tail_row_max = 256
