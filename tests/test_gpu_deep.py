@@ -352,6 +352,28 @@ def test_deep_rollout_suspend_resume_equals_stepwise(env, hidden):
         assert float(b1.total_reward[i]) == total
 
 
+@pytest.mark.parametrize("n", [1, 5, 63, 64, 65, 129])
+def test_deep_rollout_ragged_slot_counts(n):
+    """The 64-slot one-hot rollout (deep_forward64: one 8-wave workgroup per CU, 64 slots) at episode counts that
+    leave slots, workgroups and the last claim ragged -- fewer episodes than one workgroup's slots, one more than a
+    full workgroup -- bit for bit the per-step path (g2048_deep_policy + g2048_step) on the same seeds."""
+    from rl2048_amd import _lib as L
+
+    es = np.arange(90_000, 90_000 + n, dtype=np.int64)
+    ps = es + 10 ** 9
+    a = _agent(dict(REFCONF_ENV, max_steps=120), [256, 128, 64])
+    b1 = a.rollout_batch(es, ps, record_probs=True)
+    assert a.last_paths()["rollout"].startswith("g2048_deep_rollout")
+    a.use_fused_rollout = False
+    b2 = a.rollout_batch(es, ps, record_probs=True)
+    assert b1.T == b2.T and torch.equal(b1.lengths, b2.lengths)
+    valid = torch.arange(b1.T, device=DEV).unsqueeze(1) < b1.lengths.unsqueeze(0)
+    for name in ("boards", "actions", "rewards", "probs"):
+        assert torch.equal(getattr(b1, name)[valid], getattr(b2, name)[valid]), name
+    assert torch.equal((b1.flags & ~L.F_INACTIVE)[valid], (b2.flags & ~L.F_INACTIVE)[valid])
+    assert torch.equal(b1.total_reward, b2.total_reward) and torch.equal(b1.final_boards, b2.final_boards)
+
+
 @pytest.mark.parametrize("fused,rows", [(True, False), (False, False), (True, True)])
 @pytest.mark.parametrize("env,hidden,act,critic", [(REFCONF_ENV, [256, 128, 64], "ReLU", True),
                                                    (dict(REFCONF_ENV, max_steps=200), [40, 33, 20, 10], "Sigmoid", False),
