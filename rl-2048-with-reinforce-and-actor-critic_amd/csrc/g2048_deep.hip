@@ -2010,6 +2010,133 @@ __global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_mfma_kernel(
     }
 }
 
+// onehot_dw1_mfma_kernel with its deltas and boards staged through an LDS ring by LDS-DMA (round 5; the shipped
+// dW1 path when d1 rows are 16-byte aligned, G2048_DW1_RING=0 for the register form).  The register form kept three
+// steps of loads in flight on paper, but the register allocator reused in-flight load destinations as temporaries,
+// so the wait-count pass drained every load each step (vmcnt(0) in the loop): 2.9 TB/s, MFMA busy 0.40.  Here a
+// step's 16 rows (16 KiB at h1 = 256) and 16 boards go straight to LDS (global_load_lds_dwordx4: no registers) in
+// an 8-slot ring, five steps in flight across each step's raw barrier (s_waitcnt vmcnt(15): 5 steps x 3 DMA
+// instructions per wave).  Row r's 16-byte chunks are stored XOR-swizzled by 8 chunks when r >= 8 so the two lane
+// halves (rows 8 h + k) read disjoint banks.  Rows past the range are clamped loads (valid memory) masked to 0 at
+// the read, and their boards to 0: the same operands, MFMAs and order as onehot_dw1_mfma_kernel, the same bits.
+#ifndef G2048_DW1_RING
+#define G2048_DW1_RING 1
+#endif
+constexpr int kDw1Slots = 8;
+#define G2048_DW1_STEP_WAIT "s_waitcnt vmcnt(15)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier"
+static_assert((kDw1Slots - 3) * 3 == 15, "G2048_DW1_STEP_WAIT: (slots - 3) steps x 3 DMA instructions in flight");
+
+__global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_ring_kernel(
+    const uint64_t* __restrict__ boards, const float* __restrict__ d1, int h1, int64_t m, int64_t ld, int64_t per,
+    float* __restrict__ part) {
+    __shared__ float ring[kDw1Slots][kDw1Step * 256];            // [slot][row][16-byte chunk (swizzled)][4]
+    __shared__ uint32_t bring[kDw1Slots][kDw1MaxWaves][64];      // [slot][wave: its own copy][16 boards, twice]
+    __shared__ uint4 abuf[2][8][64];                             // as onehot_dw1_mfma_kernel's
+    typedef __attribute__((address_space(3))) void lvoid;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t s0 = (int64_t)blockIdx.x * per, s1 = s0 + per < m ? s0 + per : m;
+    const int u = 32 * w + r;
+    const bool live = u < h1;
+    const uint32_t q = (uint32_t)r >> 4, e = (uint32_t)r & 15u;
+    const int nsteps = s1 > s0 ? (int)((s1 - s0 + kDw1Step - 1) / kDw1Step) : 0;
+    const int nch = (h1 + 3) >> 2;                                   // 16-byte chunks per row
+    const int word = (((u >> 2) ^ (h << 3)) << 2) | (u & 3);        // unit u of rows 8 h .. 8 h + 7 in the slot
+    floatx16 acc[8];
+#pragma unroll
+    for (int p = 0; p < 8; p++) acc[p] = floatx16{};
+    float db = 0.0f;
+    if (nsteps > 0) {   // block-uniform
+        const int64_t slast = s1 - 1;
+        // The DMA is issued from inline asm: with the builtin, the wait-count pass cannot tell the ring slots (or
+        // abuf) apart from the slot being filled and put vmcnt(0) before every LDS read.  The asm barrier below
+        // (vmcnt(15), "memory") is the only ordering these reads need.
+        const uint32_t ring_lds = (uint32_t)(uintptr_t)(lvoid*)&ring[0][0], bring_lds = (uint32_t)(uintptr_t)(lvoid*)&bring[0][0][0];
+        const int wu = __builtin_amdgcn_readfirstlane(w);
+        const auto issue = [&](int st) {   // step st into slot st % kDw1Slots: wave w rows 2 w, 2 w + 1, its boards
+            const int sl = st % kDw1Slots;
+            const int64_t base = s0 + (int64_t)st * kDw1Step;
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int row = 2 * w + i;
+                const int64_t smp = base + row < slast ? base + row : slast;
+                const int g = lane ^ (((row >> 3) & 1) << 3);
+                const float* src = d1 + smp * ld + 4 * (g < nch ? g : 0);
+                const uint32_t dst = ring_lds + (uint32_t)((sl * kDw1Step + 2 * wu + i) * 256 * 4);
+                asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(dst)
+                             : "memory", "m0");
+            }
+            const int j = (lane & 31) >> 1;   // lanes 32 .. 63 load the same 16 boards again (one DMA shape per wave)
+            const int64_t smp = base + j < slast ? base + j : slast;
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(boards + smp) + (lane & 1);
+            const uint32_t dst = bring_lds + (uint32_t)((sl * kDw1MaxWaves + wu) * 64 * 4);
+            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(dst)
+                         : "memory", "m0");
+        };
+        const auto build_a = [&](int st, int buf) {   // this wave's cell pair of step st's one-hot (0 past the range)
+            const int sl = st % kDw1Slots;
+            const int64_t lim = s1 - s0 - (int64_t)st * kDw1Step;
+            const uint8_t* bb = reinterpret_cast<const uint8_t*>(&bring[sl][w][0]);
+            uint32_t d[4];
+#pragma unroll
+            for (int k2 = 0; k2 < 4; k2++) {
+                const int j0 = 8 * h + 2 * k2, j1 = j0 + 1;
+                const uint32_t b0 = bb[8 * j0 + w] & (j0 < lim ? 0xFFu : 0u), b1 = bb[8 * j1 + w] & (j1 < lim ? 0xFFu : 0u);
+                const uint32_t x0 = (b0 >> (4u * q)) & 15u, x1 = (b1 >> (4u * q)) & 15u;
+                d[k2] = (x0 == e ? 0x3F80u : 0u) | (x1 == e ? 0x3F800000u : 0u);
+            }
+            abuf[buf][w][lane] = make_uint4(d[0], d[1], d[2], d[3]);
+        };
+        for (int j = 0; j < kDw1Slots - 1; j++) issue(j);
+        asm volatile(G2048_DW1_STEP_WAIT ::: "memory");   // steps 0, 1 landed
+        build_a(0, 0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        for (int st = 0; st < nsteps; st++) {
+            const int buf = st & 1;
+            issue(st + kDw1Slots - 1);   // into the slot step st - 1 read (its end barrier passed); clamped past the end
+            const int sl = st % kDw1Slots;
+            const int64_t lim = s1 - s0 - (int64_t)st * kDw1Step;
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t x = __float_as_uint(ring[sl][(8 * h + k) * 256 + word]);   // masked, not branched
+                v[k] = __uint_as_float(x & (live && 8 * h + k < lim ? 0xFFFFFFFFu : 0u));
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) db += v[k];
+            bf16x8 pl[3];
+            split3_bf16(v, pl[0], pl[1], pl[2]);
+            build_a(st + 1, buf ^ 1);   // past the last step: an image nobody reads
+            uint4 a = abuf[buf][0][lane];
+#pragma unroll
+            for (int p = 0; p < 8; p++) {
+                const bf16x8 av = __builtin_bit_cast(bf16x8, a);
+                if (p < 7) a = abuf[buf][p + 1][lane];
+                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, pl[0], acc[p], 0, 0, 0);
+                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, pl[1], acc[p], 0, 0, 0);
+                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, pl[2], acc[p], 0, 0, 0);
+            }
+            asm volatile(G2048_DW1_STEP_WAIT ::: "memory");   // steps <= st + 2 landed; this step's slots free
+        }
+    }
+    db += __shfl_xor(db, 32);
+    if (!live) return;
+    float* slab = part + (int64_t)blockIdx.x * kDw1Rows * h1;
+#pragma unroll
+    for (int p = 0; p < 8; p++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int row = tile_row(i, h);
+            slab[(int64_t)(17 * (2 * p + (row >> 4)) + (row & 15)) * h1 + u] = acc[p][i];
+        }
+    }
+    if (h == 0) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) slab[(int64_t)(17 * c + 16) * h1 + u] = 0.0f;
+        slab[(int64_t)kOneHotRows * h1 + u] = db;
+    }
+}
+
 int device_cus() {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) {
@@ -2480,8 +2607,12 @@ int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m,
     hipLaunchKernelGGL(onehot_dw1_kernel, dim3((h1 + 63) / 64, (unsigned)nparts), dim3(64 * kDw1Waves), 0, (hipStream_t)stream,
                        boards, d1, h1, m, ld, per, partials);
 #else
-    hipLaunchKernelGGL(onehot_dw1_mfma_kernel, dim3((unsigned)nparts), dim3(64 * kDw1MaxWaves), 0, (hipStream_t)stream,
-                       boards, d1, h1, m, ld, per, partials);
+    if (G2048_DW1_RING && ld % 4 == 0 && ((uintptr_t)d1 & 15u) == 0)   // 16-byte rows for the LDS-DMA ring
+        hipLaunchKernelGGL(onehot_dw1_ring_kernel, dim3((unsigned)nparts), dim3(64 * kDw1MaxWaves), 0,
+                           (hipStream_t)stream, boards, d1, h1, m, ld, per, partials);
+    else
+        hipLaunchKernelGGL(onehot_dw1_mfma_kernel, dim3((unsigned)nparts), dim3(64 * kDw1MaxWaves), 0,
+                           (hipStream_t)stream, boards, d1, h1, m, ld, per, partials);
 #endif
     return check_hip();
 }

@@ -272,6 +272,31 @@ def test_onehot_dw1_matches_fp64(h1, m, per):
     assert bool((acc[:272 * h1].view(272, h1)[~seen] == 0).all())
 
 
+@pytest.mark.parametrize("h1,m,per", [(256, 20000, 1024), (256, 9001, 4096), (100, 5000, 777), (200, 33, 16),
+                                       (64, 3, 1024), (6, 1000, 48), (256, 300, 2000)])
+def test_onehot_dw1_ring_bits_equal_register_form(h1, m, per):
+    """The LDS-DMA ring dW1 kernel (16-byte rows: ld % 4 == 0, round 5) against the register form (taken for any
+    other row stride), bit for bit, on the same deltas: same MFMAs, same order.  NaN in the row padding: neither
+    may read past unit h1 into a result."""
+    L = _lib()
+    lib, st = L.lib(), L.stream_handle(DEV)
+    rng = np.random.default_rng(7 * h1 + m)
+    b, _ = _boards(rng, m, hi=15)
+    d = torch.from_numpy(rng.standard_normal((m, h1)).astype(np.float32)).to(DEV)
+    slab = int(lib.g2048_onehot_dw1_slab(h1))
+    nparts = -(-m // per)
+    parts = []
+    for ld in (4 * (-(-h1 // 4)) + 4, 4 * (-(-h1 // 4)) + 1):   # ring, register form
+        buf = torch.full((m, ld), float("nan"), dtype=torch.float32, device=DEV)
+        buf[:, :h1] = d
+        part = torch.empty(nparts, slab, dtype=torch.float32, device=DEV)
+        L.check(lib.g2048_onehot_dw1(L.ptr(b), L.ptr(buf), h1, m, ld, per, L.ptr(part), nparts, st))
+        parts.append(part)
+    torch.cuda.synchronize()
+    assert not bool(torch.isnan(parts[0]).any())
+    assert torch.equal(parts[0].view(torch.int32), parts[1].view(torch.int32))
+
+
 REFCONF_ENV = dict(obs_mode="onehot", obs_log2_scale=1.0, reward_mode="log2", base_reward_scale=1.0,
                    use_action_mask=True, invalid_action_penalty=-1.0, max_steps=None, empty_tile_reward=0.05)
 
