@@ -406,6 +406,18 @@ __device__ __forceinline__ void onehot_gather(const float* tab, uint64_t b, int 
     }
 }
 
+// Entry 2 e + hh of the one-hot B-operand table: exponent e as 8 bf16 (1.0 at k = e, else 0) for the lane half hh
+// (k = 8 hh .. 8 hh + 7).  Looked up per cell from LDS by the layer-0 kernels: built by compares and selects it was
+// ~21 VALU per cell and operand, which made onehot_l0_mfma_kernel VALU-bound.
+__device__ __forceinline__ uint4 onehot_entry(uint32_t idx) {
+    const uint32_t e = idx >> 1, hh = idx & 1;
+    uint32_t d[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; jj++)
+        d[jj] = (e == 8 * hh + 2 * jj ? 0x3F80u : 0u) | (e == 8 * hh + 2 * jj + 1 ? 0x3F800000u : 0u);
+    return make_uint4(d[0], d[1], d[2], d[3]);
+}
+
 // One-hot first layer on the bf16 MFMA for the update (round 5): a0[u][s] = act(sum_c W1[17 c + e_c(s)][u] + b1[u])
 // per 32-sample group, written as a group block [unit][left] (left = the group's valid samples, 32 but for the last
 // group) -- the layout g2048_deep_grad reads back into its LDS activations (in the d0_out buffer, whose rows the
@@ -423,13 +435,16 @@ __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNe
                                                                           const uint64_t* __restrict__ boards,
                                                                           uint32_t n, float* __restrict__ out) {
     __shared__ float bias[256];
+    __shared__ bf16x8 wlo[kL0Waves][16][64];   // the lo plane (wave, cell, lane): 128 KiB, read once per cell
+    __shared__ uint4 ohtab[32];                 // [2 exponent + lane half]: the one-hot B operand (k = 8 h .. 8 h + 7)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, col = lane & 31;
     const int nt0 = net.nt[0], H = 32 * nt0;
     for (int u = threadIdx.x; u < H; u += blockDim.x) bias[u] = P[net.b[0] + u];
+    if (threadIdx.x < 32) ohtab[threadIdx.x] = onehot_entry(threadIdx.x);
     __syncthreads();
-    if (w >= nt0) return;   // wave-uniform; no barrier below
+    if (w >= nt0) return;   // wave-uniform; no barrier below (each wave reads only its own wlo rows)
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    bf16x8 wp[16][3];
+    bf16x8 wp[16][2];   // hi, mid planes in registers (128 VGPRs)
     {
         const float* tab = P + net.w[0] + 32 * w + col;
 #pragma unroll
@@ -437,7 +452,9 @@ __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNe
             float v[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) v[j] = tab[(int64_t)(17 * c + 8 * h + j) * H];
-            split3_bf16(v, wp[c][0], wp[c][1], wp[c][2]);
+            bf16x8 p2;
+            split3_bf16(v, wp[c][0], wp[c][1], p2);
+            wlo[w][c][lane] = p2;
         }
     }
     const uint32_t groups = (n + 31u) >> 5;
@@ -445,33 +462,68 @@ __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNe
         const uint32_t j = g * 32u + (uint32_t)col;
         return boards[j < n ? j : n - 1u];
     };
-    uint64_t bnext = board_of(blockIdx.x < groups ? blockIdx.x : 0u);
-    for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
-        const uint64_t b = bnext;
-        bnext = board_of(gi + gridDim.x < groups ? gi + gridDim.x : gi);   // the next group's, one group ahead
-        floatx16 hi = {}, lo = {};
+    // Software-pipelined by one group: group g's 16 results are stored at the top of the next group's iteration,
+    // before that group's board prefetch and MFMAs.  vmcnt counts stores and loads in one queue, and the wait-count
+    // pass makes a store's data registers wait for the store before they are rewritten: stored at the end of their
+    // own iteration (round 5 as first shipped), the next group's first VALU waited for the previous group's stores
+    // (vmcnt(1) at the loop top, the HBM write latency once per group); now the results are rewritten a whole
+    // MFMA phase after their stores issue, and the board a group needs was loaded before the stores ahead of it.
+    floatx16 hi, lo;
+    const auto layer0 = [&](const uint64_t b) {
+        hi = floatx16{};
+        lo = floatx16{};
+        asm volatile("" ::: "memory");   // wlo is re-read per group: hoisted out of the loop it would be 64 VGPRs
+        const auto onehot = [&](int c) {   // cell c's exponent as the B operand, from the LDS table
+            const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
+            return __builtin_bit_cast(bf16x8, ohtab[(nib << 1) | (uint32_t)h]);
+        };
+        // one cell ahead (B operand, lo-plane fragment), a scheduling barrier per cell: left free, the scheduler
+        // built all 16 B operands first and the kernel spilled
+        bf16x8 bv = onehot(0), lv = wlo[w][0][lane];
 #pragma unroll
         for (int c = 0; c < 16; c++) {
-            const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
-            u32x4 d;
-#pragma unroll
-            for (int jj = 0; jj < 4; jj++)
-                d[jj] = (nib == (uint32_t)(8 * h + 2 * jj) ? 0x3F80u : 0u) | (nib == (uint32_t)(8 * h + 2 * jj + 1) ? 0x3F800000u : 0u);
-            const bf16x8 bv = __builtin_bit_cast(bf16x8, d);
+            const bf16x8 bn = onehot(c < 15 ? c + 1 : 15), ln = wlo[w][c < 15 ? c + 1 : 15][lane];
             hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][0], bv, hi, 0, 0, 0);
             lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][1], bv, lo, 0, 0, 0);
-            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][2], bv, lo, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lv, bv, lo, 0, 0, 0);
+            bv = bn;
+            lv = ln;
+            __builtin_amdgcn_sched_barrier(0);
         }
-        const uint32_t left = n - gi * 32u < 32u ? n - gi * 32u : 32u;
-        float* blk = out + (size_t)gi * 32u * (uint32_t)H;
-        if ((uint32_t)col < left) {
+    };
+    float res[16];
+    const auto finish = [&]() {
 #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int u = 32 * w + tile_row(i, h);
-                blk[(uint32_t)u * left + (uint32_t)col] = activate<ACT>((hi[i] + lo[i]) + bias[u]);
-            }
-        }
+        for (int i = 0; i < 16; i++) res[i] = activate<ACT>((hi[i] + lo[i]) + bias[32 * w + tile_row(i, h)]);
+    };
+    const uint32_t wu = (uint32_t)__builtin_amdgcn_readfirstlane(w);   // the row offset is scalar (soffset)
+    // buffer stores, issued by every lane (a lane past `left` stores past num_records: dropped): no branch
+    const auto store = [&](uint32_t g) {
+        const uint32_t left = n - g * 32u < 32u ? n - g * 32u : 32u;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            out + (size_t)g * 32u * (uint32_t)H, 0, (int)(left * (uint32_t)H * 4u), 0x00020000);
+        const uint32_t cofs = (uint32_t)col < left ? ((uint32_t)col + 4u * (uint32_t)h * left) * 4u : 0x80000000u;
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(res[i]), rs, (int)cofs,
+                                                  (int)((32u * wu + (uint32_t)tile_row(i, 0)) * left * 4u), 0);
+    };
+    uint32_t gi = blockIdx.x;   // < groups: the grid is at most one workgroup per group
+    uint64_t bnext = board_of(gi + gridDim.x < groups ? gi + gridDim.x : gi);
+    layer0(board_of(gi));
+    finish();
+    // the prefetched board retired before the loop (no store is in flight yet; an empty asm reading it makes the
+    // pass wait here): merged with the back edge, where it is ready, its pending load made the pass wait vmcnt(1) at
+    // the loop top -- i.e. for the previous group's stores
+    asm volatile("" ::"v"(bnext));
+    for (gi += gridDim.x; gi < groups; gi += gridDim.x) {
+        const uint64_t b = bnext;
+        bnext = board_of(gi + gridDim.x < groups ? gi + gridDim.x : gi);   // the next group's, one group ahead
+        store(gi - gridDim.x);   // after the board load: waiting for that board leaves these 16 stores in flight
+        layer0(b);
+        finish();
     }
+    store(gi - gridDim.x);
 }
 
 // layer 0 of a one-hot net from its onehot_l0_mfma_kernel block (group gi, [unit][left]) into LDS [unit][sample]
@@ -684,6 +736,7 @@ struct DeepSmem64 {
     float act[2][256 * kAct64];
     float part[8][64][4];
     uint64_t board[64];
+    uint4 oh[32];   // the one-hot B-operand table (onehot_entry), filled at kernel start
 };
 
 template <int ACT>
@@ -707,14 +760,9 @@ __device__ void deep_forward64(const DeepNet& net, const float* __restrict__ P, 
 #pragma unroll
                 for (int pl = 0; pl < 3; pl++) f[q][pl] = ft[(q * 3 + pl) * 64];
             floatx16 hi0 = {}, lo0 = {}, hi1 = {}, lo1 = {};
-            const auto onehot_b = [&](uint64_t b, int c) {
+            const auto onehot_b = [&](uint64_t b, int c) {   // from the LDS table (same operand as the compares)
                 const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
-                u32x4 dv;
-#pragma unroll
-                for (int jj = 0; jj < 4; jj++)
-                    dv[jj] = (nib == (uint32_t)(8 * h + 2 * jj) ? 0x3F80u : 0u) |
-                             (nib == (uint32_t)(8 * h + 2 * jj + 1) ? 0x3F800000u : 0u);
-                return __builtin_bit_cast(bf16x8, dv);
+                return __builtin_bit_cast(bf16x8, S.oh[(nib << 1) | (uint32_t)h]);
             };
 #pragma unroll
             for (int c = 0; c < 16; c++) {
@@ -979,6 +1027,9 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
     __shared__ int go;
     __shared__ uint32_t park[NB == 64 ? 28 : 1][64];
     const int tid = threadIdx.x;
+    if constexpr (NB == 64) {
+        if (tid < 32) S.oh[tid] = onehot_entry((uint32_t)tid);   // read after the first forward's barriers
+    }
     const bool owner = tid < NB;
     const GLine lut{reinterpret_cast<const uint16_t*>(a.tab)};
     const GCode code{a.tab + 2 * 65536};
