@@ -425,11 +425,16 @@ __device__ __forceinline__ uint4 onehot_entry(uint32_t idx) {
 // (one-hot: cell c's 16 exponents as one k-step of v_mfma_f32_32x32x16_bf16, k = 8 h .. 8 h + 7 per lane half) is
 // exact in bf16; W1 is split exactly into three bf16 planes (w = hi + mid + lo), so every product is exact: each
 // MFMA adds exactly one nonzero term per output (the cell's exponent), hi terms into one accumulator and mid + lo
-// into another (their sum as accurate as the gather's 16-term fp32 sum).  Wave w owns unit tile w and keeps its
-// 16 cells x 3 planes of W1 fragments in registers for the whole launch (192 VGPRs), so the weights are read once
-// per launch instead of 16 KiB of W1 rows per board from L2 (the gather the gradient kernel ran: latency-bound,
-// 24 % of its time).  48 MFMAs per wave per group; the 1 KiB per sample it writes is the bound.
+// into another (their sum as accurate as the gather's 16-term fp32 sum).  Wave w owns unit tile w for the whole
+// launch: its hi / mid plane fragments (16 cells, from the packed net's plane section) in registers (128 VGPRs), the
+// lo plane in LDS (re-read per cell), the one-hot B operands from a 512-byte LDS table; 48 MFMAs per wave per group.
+// A group's results are stored at the top of the next group's iteration (buffer stores, no branch), so the wait for
+// a board never drains the previous group's stores.  Per 32-sample group and CU: 3,072 MFMA cycles per SIMD, 32 KiB
+// written.
 constexpr int kL0Waves = 8;
+#ifndef G2048_L0_PROBE
+#define G2048_L0_PROBE 0   // tools-only timing probes (1: no stores, 2: no MFMAs); 0 ships
+#endif
 template <int ACT>
 __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNet net, const float* __restrict__ P,
                                                                           const uint64_t* __restrict__ boards,
@@ -445,16 +450,14 @@ __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNe
     if (w >= nt0) return;   // wave-uniform; no barrier below (each wave reads only its own wlo rows)
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     bf16x8 wp[16][2];   // hi, mid planes in registers (128 VGPRs)
-    {
-        const float* tab = P + net.w[0] + 32 * w + col;
+    {   // the packed net's plane section (g2048_deep_pack: the same split3_bf16 of W1), coalesced 16-byte loads --
+        // splitting W1 here took 128 strided loads per lane at every launch
+        const u32x4* ft = reinterpret_cast<const u32x4*>(P + net.wpl) + lane + (int64_t)w * (kOneHotPlaneFloats / 4);
 #pragma unroll
         for (int c = 0; c < 16; c++) {
-            float v[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) v[j] = tab[(int64_t)(17 * c + 8 * h + j) * H];
-            bf16x8 p2;
-            split3_bf16(v, wp[c][0], wp[c][1], p2);
-            wlo[w][c][lane] = p2;
+            wp[c][0] = __builtin_bit_cast(bf16x8, ft[(c * 3 + 0) * 64]);
+            wp[c][1] = __builtin_bit_cast(bf16x8, ft[(c * 3 + 1) * 64]);
+            wlo[w][c][lane] = __builtin_bit_cast(bf16x8, ft[(c * 3 + 2) * 64]);
         }
     }
     const uint32_t groups = (n + 31u) >> 5;
@@ -477,17 +480,24 @@ __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNe
             const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
             return __builtin_bit_cast(bf16x8, ohtab[(nib << 1) | (uint32_t)h]);
         };
-        // one cell ahead (B operand, lo-plane fragment), a scheduling barrier per cell: left free, the scheduler
-        // built all 16 B operands first and the kernel spilled
-        bf16x8 bv = onehot(0), lv = wlo[w][0][lane];
+        // two cells ahead (B operand, lo-plane fragment: LDS reads), a scheduling barrier per cell: left free, the
+        // scheduler built all 16 B operands first and the kernel spilled; one cell ahead exposed the LDS latency
+        bf16x8 bv = onehot(0), lv = wlo[w][0][lane], bv1 = onehot(1), lv1 = wlo[w][1][lane];
 #pragma unroll
         for (int c = 0; c < 16; c++) {
-            const bf16x8 bn = onehot(c < 15 ? c + 1 : 15), ln = wlo[w][c < 15 ? c + 1 : 15][lane];
+            const bf16x8 bn = onehot(c < 14 ? c + 2 : 15), ln = wlo[w][c < 14 ? c + 2 : 15][lane];
+#if G2048_L0_PROBE == 2   // tools-only timing probe: no MFMAs (wrong results)
+            hi[c] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, bv)[0]);
+            lo[c] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, lv)[0] ^ __builtin_bit_cast(u32x4, wp[c][0])[1]);
+#else
             hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][0], bv, hi, 0, 0, 0);
             lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][1], bv, lo, 0, 0, 0);
             lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lv, bv, lo, 0, 0, 0);
-            bv = bn;
-            lv = ln;
+#endif
+            bv = bv1;
+            lv = lv1;
+            bv1 = bn;
+            lv1 = ln;
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -499,6 +509,9 @@ __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNe
     const uint32_t wu = (uint32_t)__builtin_amdgcn_readfirstlane(w);   // the row offset is scalar (soffset)
     // buffer stores, issued by every lane (a lane past `left` stores past num_records: dropped): no branch
     const auto store = [&](uint32_t g) {
+#if G2048_L0_PROBE == 1   // tools-only timing probe: no stores (wrong results)
+        if (n != 0xFFFFFFFFu) return;
+#endif
         const uint32_t left = n - g * 32u < 32u ? n - g * 32u : 32u;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             out + (size_t)g * 32u * (uint32_t)H, 0, (int)(left * (uint32_t)H * 4u), 0x00020000);
@@ -2101,7 +2114,9 @@ __global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_ring_kernel(
         const int64_t slast = s1 - 1;
         // The DMA is issued from inline asm: with the builtin, the wait-count pass cannot tell the ring slots (or
         // abuf) apart from the slot being filled and put vmcnt(0) before every LDS read.  The asm barrier below
-        // (vmcnt(15), "memory") is the only ordering these reads need.
+        // (vmcnt(15), "memory") is the only ordering these reads need.  M0 is not in the clobber lists (hipcc
+        // reserves it and ignores such a clobber): nothing the compiler emits in this kernel reads M0 (the ISA's
+        // only M0 writes are these asm statements' own).
         const uint32_t ring_lds = (uint32_t)(uintptr_t)(lvoid*)&ring[0][0], bring_lds = (uint32_t)(uintptr_t)(lvoid*)&bring[0][0][0];
         const int wu = __builtin_amdgcn_readfirstlane(w);
         const auto issue = [&](int st) {   // step st into slot st % kDw1Slots: wave w rows 2 w, 2 w + 1, its boards
@@ -2115,14 +2130,14 @@ __global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_ring_kernel(
                 const float* src = d1 + smp * ld + 4 * (g < nch ? g : 0);
                 const uint32_t dst = ring_lds + (uint32_t)((sl * kDw1Step + 2 * wu + i) * 256 * 4);
                 asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(dst)
-                             : "memory", "m0");
+                             : "memory");
             }
             const int j = (lane & 31) >> 1;   // lanes 32 .. 63 load the same 16 boards again (one DMA shape per wave)
             const int64_t smp = base + j < slast ? base + j : slast;
             const uint32_t* src = reinterpret_cast<const uint32_t*>(boards + smp) + (lane & 1);
             const uint32_t dst = bring_lds + (uint32_t)((sl * kDw1MaxWaves + wu) * 64 * 4);
             asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(dst)
-                         : "memory", "m0");
+                         : "memory");
         };
         const auto build_a = [&](int st, int buf) {   // this wave's cell pair of step st's one-hot (0 past the range)
             const int sl = st % kDw1Slots;
