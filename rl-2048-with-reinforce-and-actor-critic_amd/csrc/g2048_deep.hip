@@ -1332,6 +1332,9 @@ struct DeepGradArgs {
 #ifndef G2048_DEEP_RAW_BARRIER
 #define G2048_DEEP_RAW_BARRIER 1
 #endif
+#ifndef G2048_DEEP_SCALAR_W
+#define G2048_DEEP_SCALAR_W 1   // deep_grad_kernel's wave index as a scalar (0: per-lane, A/B)
+#endif
 __device__ __forceinline__ void lds_barrier() {
 #if G2048_DEEP_RAW_BARRIER
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -1352,7 +1355,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     extern __shared__ float dyn[];
     const DeepNet& net = a.net;
     const int L = net.L;
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31, w = tid >> 6;
+    // w through readfirstlane: the wave index and everything derived from it (tile ranges, LDS bases) live in
+    // SGPRs -- as a per-lane value hipcc kept them in VGPRs and the 4 x 10 instantiation spilled 41 of them
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31,
+              w = G2048_DEEP_SCALAR_W ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     // LDS: the hidden layers' activations (deltas overwrite them top down; layer l at aoff[l]), the output
     // partials, g, the boards and each thread's bias-gradient sums
     const auto actl = [&](int l) { return dyn + a.aoff[l]; };
