@@ -1332,6 +1332,9 @@ struct DeepGradArgs {
 #ifndef G2048_DEEP_RAW_BARRIER
 #define G2048_DEEP_RAW_BARRIER 1
 #endif
+#ifndef G2048_DEEP_STASH
+#define G2048_DEEP_STASH 1   // deep_grad_kernel's per-sample inputs and db_out sums in LDS (0: registers, A/B)
+#endif
 #ifndef G2048_DEEP_SCALAR_W
 #define G2048_DEEP_SCALAR_W 1   // deep_grad_kernel's wave index as a scalar (0: per-lane, A/B)
 #endif
@@ -1368,8 +1371,13 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     uint64_t* bds = reinterpret_cast<uint64_t*>(lds_end + 8 * 32 * 4 + 32 * 4);  // [32]
     float* dbs = lds_end + 8 * 32 * 4 + 32 * 4 + 64;                             // [kMaxHidden][256]: db_l of unit tid
     float* wol = dbs + kMaxHidden * 256;                                         // [HL][4] output weights, then [4] bias
+    // G2048_DEEP_STASH: the group's per-sample inputs (coef, action, target / TD row: [7][32]) and the db_out sums
+    // ([32][4]) in LDS instead of registers across the forward and delta chains
+    float* smp_in = wol + 256 * 4 + 4;
+    float* dbo_l = smp_in + 7 * 32;
     if (tid < 256)
         for (int l = 0; l < kMaxHidden; l++) dbs[l * 256 + tid] = 0.0f;
+    if (G2048_DEEP_STASH && tid < 128) dbo_l[tid] = 0.0f;
     const float* P = a.packed;
     {   // the output layer's weights and bias in LDS for the whole launch (its phases read them every group)
         const int HLw = 32 * net.nt[L - 1] * 4;
@@ -1445,7 +1453,16 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 tg = a.target[jc];
             }
         }
-        __syncthreads();
+        __syncthreads();   // (a fence: vmcnt(0) -- the loads above have arrived)
+        if (G2048_DEEP_STASH && tid < 32) {   // read back at the logits: their registers are free until then
+            smp_in[tid] = cf;
+            smp_in[32 + tid] = __uint_as_float(act_j);
+            smp_in[64 + tid] = tg;
+            smp_in[96 + tid] = td_r;
+            smp_in[128 + tid] = td_h;
+            smp_in[160 + tid] = __uint_as_float((uint32_t)td_l);
+            smp_in[192 + tid] = __uint_as_float((uint32_t)((uint64_t)td_l >> 32));
+        }
         DEEP_STAMP(0);
         // ---- forward: layer 0
         {
@@ -1492,7 +1509,12 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         }
         lds_barrier();
         DEEP_STAMP(1);
-        if (tid < 32 && a.critic && a.has_td) td_v = a.td.v_next[td_l];
+        if (tid < 32 && a.critic && a.has_td) {
+            const int64_t tl = G2048_DEEP_STASH ? (int64_t)((uint64_t)__float_as_uint(smp_in[160 + tid]) |
+                                                            ((uint64_t)__float_as_uint(smp_in[192 + tid]) << 32))
+                                                : td_l;
+            td_v = a.td.v_next[tl];
+        }
         // ---- forward: dense layers (each into its own region)
         for (int l = 1; l < L; l++) {
             const float* in = actl(l - 1);
@@ -1537,6 +1559,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         DEEP_STAMP(3);
         // ---- logits -> g (threads 0..31, one sample each)
         if (tid < 32) {
+            const float cf_ = G2048_DEEP_STASH ? smp_in[tid] : cf;
+            const uint32_t act_j_ = G2048_DEEP_STASH ? __float_as_uint(smp_in[32 + tid]) : act_j;
+            float tg_ = G2048_DEEP_STASH ? smp_in[64 + tid] : tg;
+            const float td_r_ = G2048_DEEP_STASH ? smp_in[96 + tid] : td_r, td_h_ = G2048_DEEP_STASH ? smp_in[128 + tid] : td_h;
             float lg[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -1549,7 +1575,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             if (!a.critic) {
                 // logits_to_probs (src/MLP.py:139-156) and the policy-gradient logits delta (:328-354)
                 const uint32_t mw = a.use_mask ? mask_word_of(bds[tid]) : 0x01010101u;
-                const uint32_t act = valid ? act_j : 0u;
+                const uint32_t act = valid ? act_j_ : 0u;
                 float l4[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) l4[k] = ((mw >> (8 * k)) & 0xFFu) ? lg[k] : -1e9f;
@@ -1559,15 +1585,15 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 for (int k = 0; k < 4; k++) e[k] = expf(l4[k] - mx);
                 const float es = ((e[0] + e[1]) + e[2]) + e[3];
 #pragma unroll
-                for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf;
+                for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf_;
             } else {
                 // the critic's value-loss gradient (update_batch :403-498, _get_grad_logits_critic :884-910)
-                if (a.has_td) tg = ((td_v * a.td.gamma) * td_h) + td_r;   // the host's fp32 operation order
-                const float diff = lg[0] - tg;
+                if (a.has_td) tg_ = ((td_v * a.td.gamma) * td_h_) + td_r_;   // the host's fp32 operation order
+                const float diff = lg[0] - tg_;
                 const float gd = (a.huber && fabsf(diff) > a.huber_delta) ? copysignf(a.huber_delta, diff) : diff;
-                g[0] = gd * cf;
+                g[0] = gd * cf_;
                 g[1] = g[2] = g[3] = 0.0f;
-                if (valid && a.delta_out) a.delta_out[j] = tg - lg[0];
+                if (valid && a.delta_out) a.delta_out[j] = tg_ - lg[0];
                 if (valid) {
                     if (a.has_td) a.td.v_out[a.td.lane[j]] = lg[0];
                     else if (a.v_out) a.v_out[j] = lg[0];
@@ -1576,7 +1602,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 gs[tid][k] = g[k];
-                dbo4[k] += g[k];
+                if (G2048_DEEP_STASH) dbo_l[tid * 4 + k] += g[k];
+                else dbo4[k] += g[k];
             }
         }
         lds_barrier();
@@ -1713,7 +1740,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         float* red = dyn;                                   // [oq][HL][5]
         if (tid < 32) {
 #pragma unroll
-            for (int k = 0; k < 4; k++) gs[tid][k] = dbo4[k];
+            for (int k = 0; k < 4; k++) gs[tid][k] = G2048_DEEP_STASH ? dbo_l[tid * 4 + k] : dbo4[k];
         }
         if (tid < oq * HL) {
 #pragma unroll
@@ -1849,7 +1876,8 @@ int64_t deep_grad_act_floats(const DeepNet& n, int nw) {
     return f;
 }
 int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, bias sums, output weights / bias
-    return (deep_grad_act_floats(n, nw) + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256 + 256 * 4 + 4) * 4;
+    return (deep_grad_act_floats(n, nw) + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256 + 256 * 4 + 4 +
+            (G2048_DEEP_STASH ? 7 * 32 + 32 * 4 : 0)) * 4;
 }
 
 // the instantiation that covers the net (nw = 0: none; see deep_grad_kernel).  The 4-wave and the 64-tile ones are
