@@ -18,6 +18,8 @@ ap.add_argument("--episodes", type=int, nargs="+", default=[65536, 1 << 20])
 ap.add_argument("--label", default="")
 ap.add_argument("--hidden", type=int, nargs="+", default=[256, 128, 64], help="hidden sizes (other nets, same env)")
 ap.add_argument("--no-fused-grad", action="store_true", help="update through the gather + hipBLASLt path (A/B)")
+ap.add_argument("--multi-launch", action="store_true",
+                help="deep_grad_multi_launch: nets past one launch's tile budget on g2048_deep_grad (A/B)")
 args = ap.parse_args()
 sys.path.insert(0, os.path.abspath(args.repo))
 if os.environ.get("G2048_LIB"):   # an A/B build of the library
@@ -43,6 +45,8 @@ dev = torch.device("cuda", 0)
 agent = ReinforceAgent(Game2048EnvConfig(**ENV), MLPConfig(**MLP), ReinforceAgentConfig(**AGENT), device=dev)
 if args.no_fused_grad:
     agent.use_fused_grad = False
+if args.multi_launch:
+    agent.deep_grad_multi_launch = True
 for si, E in enumerate(args.episodes):
     for rep in range(2):   # one warm-up iteration at every size, then the timed one (bench.py's definition)
         es = np.arange(3 + (rep + 10 * si) * E, 3 + (rep + 10 * si + 1) * E, dtype=np.int64)
