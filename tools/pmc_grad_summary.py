@@ -14,7 +14,7 @@ import sys
 
 D = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_grad"
 CLOCK_GHZ, SIMDS = 2.4, 1024
-KERNELS = ("grad_coop_kernel", "deep_grad_kernel", "deep_rollout_kernel", "deep_policy_kernel", "onehot_dw1_mfma_kernel", "onehot_dw1_kernel",
+KERNELS = ("grad_coop_kernel", "deep_grad_kernel", "deep_rollout_kernel", "deep_policy_kernel", "onehot_dw1_mfma_kernel", "onehot_dw1_ring_kernel", "onehot_dw1_kernel",
            "onehot_l0_mfma_kernel",
            "onehot_l1_kernel", "dw2_kernel", "fold_kernel", "grad_kernel", "policy_kernel", "rollout_kernel", "Cijk")
 
