@@ -1332,6 +1332,9 @@ struct DeepGradArgs {
 #ifndef G2048_DEEP_RAW_BARRIER
 #define G2048_DEEP_RAW_BARRIER 1
 #endif
+#ifndef G2048_DEEP_NO4
+#define G2048_DEEP_NO4 0   // A/B builds: one-hot nets of <= 40 tiles on the 8-wave instantiations instead of 4 x 10
+#endif
 #ifndef G2048_DEEP_STASH
 #define G2048_DEEP_STASH 1   // deep_grad_kernel's per-sample inputs and db_out sums in LDS (0: registers, A/B)
 #endif
@@ -1885,7 +1888,8 @@ int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, 
 // of 10 or 8 dense tiles per wave, hipcc spills whole accumulator tiles (~300-650 VGPRs).
 DeepGradVariant deep_grad_variant(const DeepNet& n) {
     const int tiles = deep_grad_layout(n).ntiles;
-    if (n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024) return {4, 10, G2048_DEEP_SPLIT4 ? 2 : 0, 2, 1};
+    if (!G2048_DEEP_NO4 && n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024)
+        return {4, 10, G2048_DEEP_SPLIT4 ? 2 : 0, 2, 1};
     if (tiles <= 48 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 6, 1, 1, 1};
     if ((n.onehot || G2048_DEEP_LOG2_64) && tiles <= 64 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 8, 1, 1, 1};
     // past one launch's accumulator budget (round 5; e.g. one-hot [256, 256, 256], log2 [256, 256]): the dense dW
