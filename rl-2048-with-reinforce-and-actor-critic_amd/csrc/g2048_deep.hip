@@ -432,6 +432,9 @@ __device__ __forceinline__ uint4 onehot_entry(uint32_t idx) {
 // a board never drains the previous group's stores.  Per 32-sample group and CU: 3,072 MFMA cycles per SIMD, 32 KiB
 // written.
 constexpr int kL0Waves = 8;
+#ifndef G2048_L0_SB
+#define G2048_L0_SB 1   // cells per scheduling region in onehot_l0_mfma_kernel (A/B builds)
+#endif
 #ifndef G2048_L0_PROBE
 #define G2048_L0_PROBE 0   // tools-only timing probes (1: no stores, 2: no MFMAs); 0 ships
 #endif
@@ -498,7 +501,7 @@ __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNe
             lv = lv1;
             bv1 = bn;
             lv1 = ln;
-            __builtin_amdgcn_sched_barrier(0);
+            if ((c + 1) % G2048_L0_SB == 0) __builtin_amdgcn_sched_barrier(0);
         }
     };
     float res[16];
