@@ -418,7 +418,8 @@ int64_t g2048_onehot_dw1_slab(int h1);
  * p of partials (nparts = ceil(m / per)) holds the sums over samples [p per, (p + 1) per) -- ABI 14: an fp32
  * accumulation on the bf16 MFMA of the exact products of the one-hot with each delta's three bf16 planes
  * (deterministic, one 8-wave workgroup per slab: pick per so that nparts ~ the CU count); fold them with
- * g2048_fold_partials. */
+ * g2048_fold_partials.  Rows on 16-byte boundaries (d1 16-byte aligned, ld % 4 == 0) stream through an LDS ring
+ * (round 5), any other stride through registers: the same bits either way. */
 int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m, int64_t ld, int64_t per,
                      float* partials, int64_t nparts, void* stream);
 
