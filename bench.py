@@ -16,9 +16,11 @@ Rank 0 prints ONE JSON line.  Extras: `roofline` of the step kernel (SURVEY.md s
 board-step / HIP-event kernel time vs 8 TB/s; the build's layout bytes beside them; `traffic` = HBM bytes per launch
 from rocprofv3 FETCH_SIZE/WRITE_SIZE passes when rocprofv3 is present), `cpu_baseline` (the reference's CPU step
 loop restated in Python -- oracle/pyref.py, pinned to the reference -- one process per host core, a bounded sample;
-the C port beside it), `train_iteration_dp` (configs[3]'s training iteration per GPU shard, every rank, with the
-gradient all-reduce inside the timed region) and, at N=1, `policy_rollout` (env steps/s with the [256,256] ReLU
-policy MLP + on-device sampling in the loop; the configs[1] / configs[2] training iterations).
+the C port beside it), `configs4_onehot_philox` (configs[4]'s per-GPU shard, every rank: the same step leg in Philox
+mode writing one-hot obs + int8 mask, 1,122 B / board-step, with its own roofline and PMC traffic),
+`train_iteration_dp` (configs[3]'s training iteration per GPU shard, every rank, with the gradient all-reduce inside
+the timed region) and, at N=1, `policy_rollout` (env steps/s with the [256,256] ReLU policy MLP + on-device sampling
+in the loop; the configs[1] / configs[2] training iterations; the reference runner's documented config).
 """
 from __future__ import annotations
 
@@ -63,7 +65,7 @@ def survey_bytes_per_step(rng: str, obs: str) -> int:
 def bytes_per_step(rng: str, obs: str) -> tuple[int, int]:
     """Layout bytes (reads, writes) per board-step."""
     r = CORE_R + RNG_BYTES[rng][0]
-    w = CORE_W + RNG_BYTES[rng][1] + OBS_BYTES[obs]
+    w = CORE_W + RNG_BYTES[rng][1] + OBS_BYTES[obs] + (3 if obs == "onehot" else 0)   # one-hot: int8[4] mask
     return r, w
 
 
@@ -82,6 +84,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"])
     ap.add_argument("--no-policy", action="store_true")
+    ap.add_argument("--no-configs4", action="store_true",
+                    help="skip configs[4]'s Philox + one-hot obs step leg (1,122 B / board-step)")
     ap.add_argument("--no-refconfig", action="store_true",
                     help="skip the reference runner-config training iterations (runner.py:10-47)")
     ap.add_argument("--no-auto-reset", action="store_true", help="diagnostic: finished lanes go inactive")
@@ -118,16 +122,21 @@ def synthetic_boards(torch, B: int, lane_offset: int, device, seed: int = 0x2048
     return out
 
 
-def make_env(torch, args, B, lane_offset, device):
+def make_env(torch, args, B, lane_offset, device, rng: str | None = None, obs: str | None = None):
+    """The bench env (rng / obs default to the headline's): max_steps 1024, auto-reset, per-lane seeds
+    seed0 + global lane, synthetic random-state boards.  The action mask is packed (bit a = action a) except with
+    one-hot obs, where it is the obs dict's int8[4] (configs[4]: SURVEY.md section 8(d)'s 1,092 B = obs + mask)."""
     from rl2048_amd import Game2048EnvConfig, VecGame2048Env
-    from rl2048_amd import _lib as L
 
-    cfg = Game2048EnvConfig(obs_mode="log2" if args.obs == "none" else args.obs, obs_log2_scale=0.0625,
+    rng = rng or args.rng
+    obs = obs or args.obs
+    packed_mask = obs != "onehot"
+    cfg = Game2048EnvConfig(obs_mode="log2" if obs == "none" else obs, obs_log2_scale=0.0625,
                             reward_mode="log2", base_reward_scale=0.5, max_steps=1024)
-    env = VecGame2048Env(B, cfg, device=device, rng=args.rng, auto_reset=not args.no_auto_reset,
+    env = VecGame2048Env(B, cfg, device=device, rng=rng, auto_reset=not args.no_auto_reset,
                          reset_stride=B * max(args.gpus, 1), lane_offset=lane_offset, track_score=False,
-                         packed_mask=True)
-    if args.obs == "none":
+                         packed_mask=packed_mask)
+    if obs == "none":
         env._out.obs = None
     # per-lane episode seeds (PCG64: default_rng(seed) streams) via g2048_reset, then the random-state boards
     env.reset(seed=torch.arange(B, dtype=torch.int64, device=device) + (1_000_003 + lane_offset))
@@ -137,10 +146,13 @@ def make_env(torch, args, B, lane_offset, device):
 
 
 # ---------------------------------------------------------------------------------------------- PMC traffic
-def pmc_traffic(args) -> dict | None:
-    """Run this benchmark twice under rocprofv3 (separate FETCH_SIZE and WRITE_SIZE passes, kernel-trace only,
-    per MI355X_MICROARCH.md 'HBM') and return HBM bytes per step-kernel launch.  FETCH_SIZE is doubled: on
-    gfx950 it reports half the bytes of coalesced streaming reads."""
+def pmc_traffic(args, rng: str | None = None, obs: str | None = None) -> dict | None:
+    """Run this benchmark's step leg twice under rocprofv3 (separate FETCH_SIZE and WRITE_SIZE passes, kernel-trace
+    only, per MI355X_MICROARCH.md 'HBM') and return HBM bytes per step-kernel launch (rng / obs: the leg's mode,
+    default the headline's).  FETCH_SIZE is doubled: on gfx950 it reports half the bytes of coalesced streaming
+    reads."""
+    rng = rng or args.rng
+    obs = obs or args.obs
     exe = shutil.which("rocprofv3")
     if exe is None:
         return None
@@ -153,10 +165,10 @@ def pmc_traffic(args) -> dict | None:
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                         "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT") and not k.startswith("TORCHELASTIC_")}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        out = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir=base)
+        out = tempfile.mkdtemp(prefix=f"pmc_{rng}_{obs}_{counter}_", dir=base)
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "pmc", "--", sys.executable,
                os.path.abspath(__file__), "--pmc-child", "--steps", "10", "--warmup", "3", "--boards",
-               str(args.boards), "--rng", args.rng, "--obs", args.obs]
+               str(args.boards), "--rng", rng, "--obs", obs]
         try:
             subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                            env=env)
@@ -436,6 +448,69 @@ def train_iteration_dp(torch, device, episodes_per_rank: int, rank: int, world: 
             "scaling": "weak"}
 
 
+def time_steps(torch, env, actions, K: int, W: int, world: int):
+    """W untimed launches, then EXACTLY K launches bracketed by a barrier + synchronize on both sides; HIP events on
+    the launch stream around launches 2..K of the same K (kernel ms per launch = their span / (K - 1)): the GPU is
+    idle when the first launch is enqueued, so an event recorded before it would also time the first launch's host
+    enqueue latency (~12 us; profiles/round6/r7a/trace_window.json: events 29.3 us against a 28.6 us dispatch span).
+    Returns (wall seconds, kernel ms per launch), each the MAX over ranks."""
+    import torch.distributed as dist
+
+    for k in range(W):
+        env.step_into(actions[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    if K == 1:
+        ev0.record()
+    for k in range(K):
+        env.step_into(actions[W + k])
+        if k == 0 and K > 1:
+            ev0.record()   # fires when launch 1 ends; launches 2..K are queued back to back behind it
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / max(K - 1, 1)
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=env.board.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    return elapsed, kern_ms
+
+
+def onehot_philox_leg(torch, args, B, rank, world, device, actions, K, W, traffic) -> dict:
+    """configs[4]'s per-GPU shard (BASELINE.json configs[4]: 8,388,608 boards = 8 x 1,048,576, fused step + one-hot
+    obs + Philox per-lane RNG): the same synthetic boards, actions and timing as the headline leg, on
+    g2048_step in Philox mode writing the one-hot obs (float32[272], src/env.py:131-150 / src/MLP.py:22-43) and
+    the int8[4] action mask every step -- 1,122 algorithmic B per board-step, 92 %
+    writes, a 1.1 GB launch: beyond the 256 MB MALL, so its HBM fraction is HBM's."""
+    env = make_env(torch, args, B, rank * B, device, rng="philox", obs="onehot")
+    elapsed, kern_ms = time_steps(torch, env, actions, K, W, world)
+    del env
+    torch.cuda.empty_cache()
+    sb = survey_bytes_per_step("philox", "onehot")
+    rb, wb = bytes_per_step("philox", "onehot")
+    alg = sb * B
+    achieved = alg / (kern_ms * 1e-3) / 1e9
+    out = {"config": f"configs[4] per-GPU shard: {B:,} boards x {world} GPU(s), Philox spawn + one-hot obs + int8 mask",
+           "boards_per_gpu": B, "rng": "philox", "obs": "onehot", "steps": K, "warmup": W,
+           "value": K * B * world / elapsed, "unit": "env steps/s", "ms_per_step": elapsed / K * 1e3,
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "bytes_per_board_step": sb,
+                        "algorithmic_bytes_per_launch": alg, "layout_bytes_per_board_step": rb + wb,
+                        "traffic": traffic["bytes"] if traffic else None,
+                        "traffic_over_algorithmic": traffic["bytes"] / alg if traffic else None,
+                        "kernel_ms": kern_ms, "kernel": "step_kernel (g2048_step, Philox + one-hot obs)"}}
+    if traffic:
+        out["roofline"]["traffic_detail"] = traffic
+    return out
+
+
 # ---------------------------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -447,9 +522,12 @@ def main():
     # The profiler passes and the CPU baseline run on rank 0 before this process touches the GPU, at every N: under
     # torchrun the other ranks meanwhile wait in init_process_group (well inside its timeout), so the CPU loop is
     # timed on the same box's host cores in the same run and the roofline carries PMC traffic at N > 1 too.
-    traffic = None
+    traffic = traffic4 = None
+    run_c4 = not args.pmc_child and not args.no_configs4
     if rank == 0 and not args.pmc_child and args.traffic == "auto":
         traffic = pmc_traffic(args)
+        if run_c4:
+            traffic4 = pmc_traffic(args, rng="philox", obs="onehot")
     cpu = None
     if rank == 0 and not args.pmc_child and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.cpu_baseline_seconds)
@@ -510,6 +588,12 @@ def main():
     g = torch.Generator(device=device)
     g.manual_seed(1 + rank)
     actions = torch.randint(0, 4, (K + W, B), dtype=torch.uint8, device=device, generator=g)
+    configs4 = None
+    if run_c4:   # every rank (weak scaling), before the headline leg: its K launches stay the run's last
+        try:
+            configs4 = onehot_philox_leg(torch, args, B, rank, world, device, actions, K, W, traffic4)
+        except Exception as e:  # noqa: BLE001 -- an extra, never the headline
+            configs4 = {"error": repr(e)}
     # Chip warm-up, explicit and independent of the extra legs above: untimed step launches for
     # --chip-warmup-seconds on a separate env of the same shape (on a cold chip the first ~20 launches of the step
     # kernel run 10-30 % slower, profiles/round3/step_cold_trace.log); the headline env below starts from the
@@ -545,31 +629,11 @@ def main():
                               "active_frac": round(act, 4), "invalid_frac": round(inv, 4),
                               "tiles_per_board": round(tiles, 2)}), flush=True)
         return
-    for k in range(W):
-        env.step_into(actions[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     # timed region (the reported value): K launches, nothing else on the stream.  HIP events on the launch stream
-    # bracket the same K launches: kernel_ms (the roofline's duration) is their average, back to back.
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    for k in range(K):
-        env.step_into(actions[W + k])
-    ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / K
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    # bracket the same K launches: kernel_ms (the roofline's duration) is their average, back to back -- the last K
+    # step_kernel dispatches of the run (tools/trace_window.py reads them back from a rocprofv3 kernel trace of this
+    # command: profiles/round6/)
+    elapsed, kern_ms = time_steps(torch, env, actions, K, W, world)
     if args.pmc_child:
         return
     del actions
@@ -603,11 +667,14 @@ def main():
                      "layout_bytes_per_board_step": rb + wb, "layout_achieved": layout_achieved,
                      "layout_frac": layout_achieved / HBM_PEAK_GBS,
                      "traffic_over_algorithmic": (traffic["bytes"] / alg_bytes) if traffic else None,
-                     "kernel_ms": kern_ms, "kernel": "step_kernel (g2048_step)"},
+                     "kernel_ms": kern_ms, "kernel_ms_basis": "HIP events around launches 2..K of the timed K",
+                     "kernel": "step_kernel (g2048_step)"},
         "cpu_baseline": cpu,
     }
     if traffic:
         line["roofline"]["traffic_detail"] = traffic
+    if configs4 is not None:
+        line["configs4_onehot_philox"] = configs4
     if train is not None:
         line["train_iteration_dp"] = train
     if policy is not None:

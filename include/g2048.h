@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 15
+#define G2048_ABI_VERSION 16
 
 /* status codes */
 #define G2048_OK 0
@@ -386,9 +386,11 @@ int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, 
                       void* stream);
 /* update_batch's actor or critic gradient (src/reinforce_agent.py:403-555, _backpropagation :639-678) fused for a
  * packed deep net (forward + loss gradient + backward in one kernel, 32 samples per workgroup step), covered when
- * g2048_deep_grad_slab() >= 0 (at most 64 dense 32x32 weight-gradient tiles: [256, 256], [256, 128, 64] and
- * smaller).  ABI 14: nets of at most 40 tiles run two 4-wave workgroups per CU -- pass nparts =
- * g2048_deep_grad_parts() (any nparts >= 1 is correct; that one fills the chip).
+ * g2048_deep_grad_slab() >= 0 (1..4 hidden layers of 1..256 units).  Nets of at most 64 dense 32x32 weight-gradient
+ * tiles on one-hot obs (48 on log2 / raw: [256, 256], [256, 128, 64] and smaller) take one launch; larger ones one
+ * launch per range of tiles, each redoing the forward and delta chains (g2048_deep_grad_passes()).  ABI 14: nets of
+ * at most 40 tiles run two 4-wave workgroups per CU -- pass nparts = g2048_deep_grad_parts() (any nparts >= 1 is
+ * correct; that one fills the chip).
  * grad_packed: g2048_deep_grad_pack (the dense layers' weights in backward-fragment order; re-pack after every
  * update).  Actor: coef = advantage x step weight, actions; critic (critic = 1): coef = step weight, target =
  * r + gamma V(s') m, loss 0 MSE / 1 Huber, delta_out = target - V, value_out = V (NULL ok).  partials [nparts][slab]
@@ -400,6 +402,9 @@ int64_t g2048_deep_grad_pack_size(int obs_mode, int n_hidden, const int32_t* hid
 int64_t g2048_deep_grad_slab(int obs_mode, int n_hidden, const int32_t* hidden);
 /* the workgroup count that fills the current device for this net (ABI 14; -1 when g2048_deep_grad_slab() < 0) */
 int g2048_deep_grad_parts(int obs_mode, int n_hidden, const int32_t* hidden);
+/* launches per g2048_deep_grad call for this net: 1 within one launch's accumulator budget, more past it (ABI 16;
+ * -1 when g2048_deep_grad_slab() < 0) */
+int g2048_deep_grad_passes(int obs_mode, int n_hidden, const int32_t* hidden);
 int g2048_deep_grad_pack(const float* const* W, int obs_mode, int n_hidden, const int32_t* hidden, float* packed,
                          int64_t packed_len, void* stream);
 int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden, const int32_t* hidden,
@@ -418,7 +423,7 @@ int64_t g2048_onehot_dw1_slab(int h1);
  * p of partials (nparts = ceil(m / per)) holds the sums over samples [p per, (p + 1) per) -- ABI 14: an fp32
  * accumulation on the bf16 MFMA of the exact products of the one-hot with each delta's three bf16 planes
  * (deterministic, one 8-wave workgroup per slab: pick per so that nparts ~ the CU count); fold them with
- * g2048_fold_partials.  Rows on 16-byte boundaries (d1 16-byte aligned, ld % 4 == 0) stream through an LDS ring
+ * g2048_fold_partials.  Rows on 16-byte boundaries (d1 16-byte aligned, ld % 4 == 0, h1 % 4 == 0) stream through an LDS ring
  * (round 5), any other stride through registers: the same bits either way. */
 int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m, int64_t ld, int64_t per,
                      float* partials, int64_t nparts, void* stream);

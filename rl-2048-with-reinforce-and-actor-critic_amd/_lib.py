@@ -21,7 +21,7 @@ SRC = os.path.join(PKG_DIR, "csrc", "g2048.hip")
 SOURCES = [SRC, os.path.join(PKG_DIR, "csrc", "g2048_policy.hip"), os.path.join(PKG_DIR, "csrc", "g2048_dw2.hip"),
            os.path.join(PKG_DIR, "csrc", "g2048_deep.hip")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
-ABI_VERSION = 15
+ABI_VERSION = 16
 DEEP_MAX_HIDDEN = 4
 
 # include/g2048.h constants
@@ -196,6 +196,8 @@ def _declare(L):
     L.g2048_deep_grad_slab.restype = i64
     L.g2048_deep_grad_parts.argtypes = [i32, i32, vp]
     L.g2048_deep_grad_parts.restype = i32
+    L.g2048_deep_grad_passes.argtypes = [i32, i32, vp]
+    L.g2048_deep_grad_passes.restype = i32
     L.g2048_deep_grad_pack.argtypes = [vp, i32, i32, vp, vp, i64, vp]
     L.g2048_deep_grad.argtypes = [vp, vp, i32, vp, i32, i32, f, i32, vp, vp, vp, i32, i32, f, vp, vp, vp, vp, i64, vp,
                                   i64, P(TdRows), vp]
@@ -219,7 +221,7 @@ EXPORTED_SYMBOLS = ("g2048_abi_version", "g2048_last_error", "g2048_init", "g204
                     "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2", "g2048_fold_partials",
                     "g2048_dw2_factored", "g2048_dw2_actor", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
                     "g2048_deep_rollout", "g2048_deep_hidden", "g2048_deep_grad_pack_size", "g2048_deep_grad_slab",
-                    "g2048_deep_grad_parts",
+                    "g2048_deep_grad_parts", "g2048_deep_grad_passes",
                     "g2048_deep_grad_pack", "g2048_deep_grad", "g2048_onehot_layer1", "g2048_onehot_dw1_slab",
                     "g2048_onehot_dw1")
 

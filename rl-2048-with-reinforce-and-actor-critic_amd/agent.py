@@ -561,19 +561,18 @@ class ReinforceAgent:
         self._fold(part, acc)
 
     def _deep_grad_spec(self, params, out_dim: int):
-        """_deep_spec when g2048_deep_grad covers the net in one launch per chunk (at most 64 dense 32x32
-        weight-gradient tiles on one-hot obs, 48 on log2 / raw), else None.  Larger nets run it as one launch per
-        range of tiles (each redoing the forward and delta chains) only with deep_grad_multi_launch: measured slower
-        than the gather + hipBLASLt path for one-hot [256, 256, 256] (update 1.37 s against 1.15 s at 262,144
-        episodes, profiles/round5/r6e/)."""
+        """_deep_spec when g2048_deep_grad covers the net in one launch per chunk (g2048_deep_grad_passes() == 1:
+        at most 64 dense 32x32 weight-gradient tiles on one-hot obs, 48 on log2 / raw), else None.  Larger nets run
+        it as one launch per range of tiles (each redoing the forward and delta chains) only with
+        deep_grad_multi_launch: measured slower than the gather + hipBLASLt path for one-hot [256, 256, 256] (update
+        1.31 s against 1.14 s at 262,144 episodes, profiles/round5/r6w/)."""
         if not self.use_fused_grad:
             return None
         d = self._deep_spec(params, out_dim)
-        if d is None or int(self._lib.g2048_deep_grad_slab(d[0], len(d[1]), d[3])) < 0:
+        if d is None:
             return None
-        t = [(h + 31) // 32 for h in d[1]]
-        tiles = sum(t[l - 1] * t[l] for l in range(1, len(t)))
-        if tiles > (64 if d[0] == L.OBS_ONEHOT else 48) and not self.deep_grad_multi_launch:
+        passes = int(self._lib.g2048_deep_grad_passes(d[0], len(d[1]), d[3]))
+        if passes < 1 or (passes > 1 and not self.deep_grad_multi_launch):
             return None
         return d
 
@@ -1358,13 +1357,18 @@ class ReinforceAgent:
             # reference itself would loop forever) must not run the device out of memory: refuse past the rows the
             # free memory holds, or past deep_rollout_max_rows.
             row_bytes = n * (8 + 1 + 8 + 1 + (16 if probs is not None else 0))
-            free_b = torch.cuda.mem_get_info(dev)[0] if dev.type == "cuda" else 1 << 62
+            free_b = 1 << 62
+            if dev.type == "cuda":
+                # free device memory plus what torch's caching allocator holds reserved but unused (torch.cat below
+                # reuses or releases that cache before it would fail)
+                free_b = (torch.cuda.mem_get_info(dev)[0] + torch.cuda.memory_reserved(dev) -
+                          torch.cuda.memory_allocated(dev))
             if cap + grow > self.deep_rollout_max_rows or (cap + grow) * row_bytes > free_b + cap * row_bytes // 2:
+                hint = "set max_steps" + ("" if self.env_config.use_action_mask else " or use_action_mask=True")
                 raise RuntimeError(
                     f"rollout_batch (max_steps=None): {k} episode(s) still running after {cap} steps; growing the "
                     f"[T, n] trajectory buffer to {cap + grow} rows needs {(cap + grow) * row_bytes / 2**30:.1f} GiB "
-                    f"(free: {free_b / 2**30:.1f} GiB, row limit {self.deep_rollout_max_rows}) -- set max_steps or "
-                    f"use_action_mask=True")
+                    f"(free: {free_b / 2**30:.1f} GiB, row limit {self.deep_rollout_max_rows}) -- {hint}")
             boards = torch.cat([boards, torch.empty(grow, n, dtype=torch.int64, device=dev)])
             actions = torch.cat([actions, torch.zeros(grow, n, dtype=torch.uint8, device=dev)])
             rewards = torch.cat([rewards, torch.zeros(grow, n, dtype=torch.float64, device=dev)])

@@ -2532,6 +2532,13 @@ int g2048_deep_grad_parts(int obs_mode, int n_hidden, const int32_t* hidden) {
     return deep_grad_variant(n).per_cu * device_cus();
 }
 
+int g2048_deep_grad_passes(int obs_mode, int n_hidden, const int32_t* hidden) {
+    DeepNet n;
+    if (g2048_deep_grad_slab(obs_mode, n_hidden, hidden) < 0) return -1;
+    deep_layout(n_hidden, hidden, obs_mode == G2048_OBS_ONEHOT, n);
+    return deep_grad_variant(n).passes;
+}
+
 int g2048_deep_grad_pack(const float* const* W, int obs_mode, int n_hidden, const int32_t* hidden, float* packed,
                          int64_t packed_len, void* stream) {
     DeepNet n;
@@ -2616,8 +2623,8 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
     if (activation != G2048_ACT_RELU && activation != G2048_ACT_SIGMOID)
         return dfail(G2048_EINVAL, "Unsupported activation");
     if (g2048_deep_grad_slab(obs_mode, n_hidden, hidden) < 0)
-        return dfail(G2048_EINVAL, "deep gradient: net not covered (obs mode, 1..4 layers of 1..256 units, at most "
-                                   "64 dense 32x32 weight-gradient tiles)");
+        return dfail(G2048_EINVAL, "deep gradient: net not covered (obs mode one-hot / log2 / raw, 1..4 hidden "
+                                   "layers of 1..256 units)");
     if (critic && loss != 0 && loss != 1) return dfail(G2048_EINVAL, "Unknown critic loss type");
     if (!packed || !partials || (n > 0 && (!boards || !coef)) || (n > 0 && !critic && !actions) ||
         (n > 0 && critic && !target && !td) || (n > 0 && obs_mode == G2048_OBS_ONEHOT && !d0_out))
@@ -2714,7 +2721,9 @@ int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m,
     hipLaunchKernelGGL(onehot_dw1_kernel, dim3((h1 + 63) / 64, (unsigned)nparts), dim3(64 * kDw1Waves), 0, (hipStream_t)stream,
                        boards, d1, h1, m, ld, per, partials);
 #else
-    if (G2048_DW1_RING && ld % 4 == 0 && ((uintptr_t)d1 & 15u) == 0)   // 16-byte rows for the LDS-DMA ring
+    // 16-byte rows for the LDS-DMA ring, whose whole 16-byte chunks end exactly at unit h1 (h1 % 4 == 0: a row's
+    // last chunk never reads past s * ld + h1 - 1, which the header promises is valid memory)
+    if (G2048_DW1_RING && ld % 4 == 0 && h1 % 4 == 0 && ((uintptr_t)d1 & 15u) == 0)
         hipLaunchKernelGGL(onehot_dw1_ring_kernel, dim3((unsigned)nparts), dim3(64 * kDw1MaxWaves), 0,
                            (hipStream_t)stream, boards, d1, h1, m, ld, per, partials);
     else

@@ -144,13 +144,14 @@ def reduce_gradients_(tensors: list[torch.Tensor], n_local: int, group=None) -> 
     critic) plus this rank's episode count (as exact base-2^16 digits) is all-reduced, the global count is rebuilt
     exactly in fp64 on the device, and every gradient is multiplied by fp32(1 / count) -- the 1 / n_traj of
     src/reinforce_agent.py:467, :533 (n_traj = 8 n with augmentation).  No host synchronisation.  Without a process
-    group: the same multiply by 1 / n_local rounded to the gradients' dtype."""
+    group: the same multiply by 1 / n_local, the Python scalar rounded to each tensor's own dtype (no host-to-device
+    copy, no host sync)."""
     if not tensors:
         return
     if not active(group):
-        inv = torch.tensor(1.0 / max(int(n_local), 1), dtype=torch.float64).to(tensors[0].dtype)
+        inv = 1.0 / max(int(n_local), 1)
         for t in tensors:
-            t.mul_(inv.to(t.device))
+            t.mul_(inv)
         return
     dev, dt = tensors[0].device, tensors[0].dtype
     flat = torch.cat([t.reshape(-1) for t in tensors] +

@@ -33,6 +33,7 @@ def test_header_declares_expected_api():
         "g2048_grad_pack", "g2048_actor_grad_waves", "g2048_actor_grad", "g2048_critic_grad", "g2048_dw2",
         "g2048_fold_partials", "g2048_dw2_factored", "g2048_dw2_actor", "g2048_deep_packed_size", "g2048_deep_pack", "g2048_deep_policy",
         "g2048_deep_rollout", "g2048_deep_hidden", "g2048_deep_grad_pack_size", "g2048_deep_grad_slab", "g2048_deep_grad_parts",
+        "g2048_deep_grad_passes",
         "g2048_deep_grad_pack", "g2048_deep_grad", "g2048_onehot_layer1", "g2048_onehot_dw1_slab", "g2048_onehot_dw1"])
 
 
@@ -188,10 +189,15 @@ def test_deep_sizes_and_validation_without_gpu(L):
         pw, pb = ReinforceAgent._deep_slab_layout(hs, obs == L.OBS_ONEHOT)
         assert lib.g2048_deep_grad_slab(obs, len(hs), arr(hs)) == pb[-1] + 4, (obs, hs)
         assert lib.g2048_deep_grad_parts(obs, len(hs), arr(hs)) > 0, (obs, hs)
+        assert lib.g2048_deep_grad_passes(obs, len(hs), arr(hs)) > 1, (obs, hs)
+    # within one launch's budget: one pass (what ReinforceAgent._deep_grad_spec gates on)
+    for obs, hs in ((L.OBS_ONEHOT, [256, 128, 64]), (L.OBS_ONEHOT, [256, 256]), (L.OBS_LOG2, [64, 48, 32])):
+        assert lib.g2048_deep_grad_passes(obs, len(hs), arr(hs)) == 1, (obs, hs)
     # not a net of the any-depth kernels at all (5 hidden layers)
     for obs, hs in ((L.OBS_LOG2, [32] * 5),):
         assert lib.g2048_deep_grad_slab(obs, len(hs), arr(hs)) == -1, (obs, hs)
         assert lib.g2048_deep_grad_parts(obs, len(hs), arr(hs)) == -1, (obs, hs)
+        assert lib.g2048_deep_grad_passes(obs, len(hs), arr(hs)) == -1, (obs, hs)
     # workgroups that fill the chip: two 4-wave workgroups per CU for one-hot nets of <= 40 tiles, else one
     cus = lib.g2048_deep_grad_parts(L.OBS_LOG2, 3, arr([64, 48, 32]))
     assert cus > 0

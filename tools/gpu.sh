@@ -9,6 +9,10 @@
 #   smoke               __graft_entry__.smoke()
 #   bench               the driver's bench command (bench.py --gpus 1 --steps 20 --warmup 5)
 #   prof_step           rocprofv3 kernel stats of 200 step-kernel launches (bench.py step leg only)
+#   trace_bench         the driver's bench command under a rocprofv3 kernel trace; tools/trace_window.py reads the
+#                       timed launches back (headline + configs[4] legs) beside the line's kernel_ms
+#   rehearse8           bench.py under torchrun with 8 ranks sharing the one GPU (gloo): the N = 8 flow end to end
+#   prof_c4             rocprofv3 kernel stats of 200 launches of configs[4]'s Philox + one-hot step leg
 #   refconf[:EPISODES]  tools/bench_refconfig.py under rocprofv3 --kernel-trace --stats; the top kernels printed
 #   pmc_refconf[:E]     PMC passes over the runner config at E episodes (default 262144): SQ busy / LDS, SQ waits,
 #                       FETCH_SIZE, WRITE_SIZE, TCC hit / miss -- one counter group per run; tools/pmc_grad_summary.py
@@ -70,9 +74,37 @@ for step in "$@"; do
             { tail -20 "$O/bench_driver_cmd.log"; exit 1; }
         grep '^{' "$O/bench_driver_cmd.log" | cut -c1-400
         ;;
+    trace_bench)
+        # the driver's bench command itself under a rocprofv3 kernel trace: its timed launches read back
+        # (tools/trace_window.py) beside the line's HIP-event kernel_ms; then the per-kernel stats of the same run
+        timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_bench" -o tb -- \
+            python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$O/trace_bench.log" 2>&1 ||
+            { tail -20 "$O/trace_bench.log"; exit 1; }
+        grep '^{' "$O/trace_bench.log" | cut -c1-300
+        python3 tools/trace_window.py "$O/trace_bench" "$O/trace_bench.log" --keep "$O/trace_bench_step_rows.csv" \
+            > "$O/trace_window.json" && cat "$O/trace_window.json"
+        top_kernels "$O/trace_bench/tb_kernel_stats.csv"
+        find "$O/trace_bench" -name '*_kernel_trace.csv' -size +4M -delete
+        ;;
+    prof_c4)
+        # rocprofv3 kernel stats of configs[4]'s step leg alone (Philox + one-hot obs + int8 mask, 1M boards)
+        timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c4" -o c4 -- \
+            python3 bench.py --rng philox --obs onehot --no-cpu-baseline --no-policy --no-train --no-configs4 \
+            --traffic off --steps 200 --warmup 20 > "$O/prof_c4.log" 2>&1 || { tail -20 "$O/prof_c4.log"; exit 1; }
+        grep '^{' "$O/prof_c4.log" | cut -c1-300
+        top_kernels "$O/prof_c4/c4_kernel_stats.csv"
+        ;;
+    rehearse8)
+        # bench.py's N = 8 flow on ONE GPU (8 ranks share it: the gloo fallback) -- rank 0's PMC children and CPU
+        # baseline before init_process_group, every leg's barriers and max-over-ranks reduce; value is not scaling
+        HSA_ENABLE_IPC_MODE_LEGACY=0 timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+            --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 8 --steps 20 --warmup 5 --boards 65536 \
+            --train-episodes 4096 > "$O/rehearse8.log" 2>&1 || { tail -30 "$O/rehearse8.log"; exit 1; }
+        grep '^{' "$O/rehearse8.log" | cut -c1-400
+        ;;
     prof_step)
         timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_step" -o step -- \
-            python3 bench.py --no-cpu-baseline --no-policy --no-train --no-refconfig --traffic off --steps 200 --warmup 20 \
+            python3 bench.py --no-cpu-baseline --no-policy --no-train --no-refconfig --no-configs4 --traffic off --steps 200 --warmup 20 \
             > "$O/prof_step.log" 2>&1 || { tail -20 "$O/prof_step.log"; exit 1; }
         grep '^{' "$O/prof_step.log" | cut -c1-300
         top_kernels "$O/prof_step/step_kernel_stats.csv"
