@@ -56,17 +56,6 @@ int fail(int code, const std::string& msg) {
 #ifndef G2048_DIAG
 #define G2048_DIAG 0
 #endif
-#ifndef G2048_LEAN
-#define G2048_LEAN 1
-#endif
-// 1: a lane whose episode ends stores its step outputs in the sweep before the deferred reset rewrites them (whole
-// lines); 0 (A/B builds only): it leaves them to the reset pass
-#ifndef G2048_RESET_FULL_STORES
-#define G2048_RESET_FULL_STORES 1
-#endif
-
-
-
 #if G2048_DIAG
 // per-workgroup phase timestamps of the last step launch (s_memrealtime, 100 MHz): entry, tables filled,
 // main loop done, reset list built, end
@@ -106,17 +95,10 @@ __device__ __forceinline__ void st(T* p, uint32_t idx, T v) {
 }
 
 // observation stores are non-temporal (streaming): measured on MI355X, onehot obs (1,088 B/board) 260 -> 241 us at
-// 1M boards and 1050 -> 908 us at 4M; log2 obs unchanged (tools/ab_nt.sh, profiles/round1/ab_nt.log)
-#ifndef G2048_OBS_NT
-#define G2048_OBS_NT 1   // 0: plain stores (A/B builds only)
-#endif
+// 1M boards and 1050 -> 908 us at 4M; log2 obs unchanged (round 1, profiles/round1/ab_nt.log)
 __device__ __forceinline__ void st_obs(float4* base, int q, float4 v) {
-#if G2048_OBS_NT
     typedef float f4v __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(base + q));
-#else
-    base[q] = v;
-#endif
 }
 
 struct LineFn {
@@ -144,24 +126,35 @@ __device__ inline void write_obs_wave(float* __restrict__ obs, uint32_t w0, uint
                                       float scale) {
     if constexpr (OBS == G2048_OBS_ONEHOT) {
         float4* dst = reinterpret_cast<float4*>(obs) + (size_t)w0 * 68;
+        // float4 q of the wave's region: board src = q / 68, floats j..j+3 of its 272 -- they touch at most two
+        // cells, and each cell's one-hot 1 sits at 17 cell + e
+        const auto value = [&](int q, int src, uint64_t bb) {
+            const int j = (q - src * 68) * 4;
+            const int c0 = j / 17;
+            const int c1 = c0 + 1 < 16 ? c0 + 1 : 15;
+            const int p0 = 17 * c0 + (int)nib(bb, c0);
+            const int p1 = 17 * c1 + (int)nib(bb, c1);
+            float4 v;
+            v.x = (j == p0 || j == p1) ? 1.0f : 0.0f;
+            v.y = (j + 1 == p0 || j + 1 == p1) ? 1.0f : 0.0f;
+            v.z = (j + 2 == p0 || j + 2 == p1) ? 1.0f : 0.0f;
+            v.w = (j + 3 == p0 || j + 3 == p1) ? 1.0f : 0.0f;
+            return v;
+        };
+        if (wmask == ~0ull) {   // wave-uniform: every board of the chunk writes (no per-store lane test)
 #pragma unroll 4
-        for (int k = 0; k < 68; k++) {
-            const int q = k * 64 + lane;         // float4 index in the wave's region
-            const int src = q / 68;              // owning board (lane)
-            const int j = (q - src * 68) * 4;    // first float index inside the board's 272 (a multiple of 4)
-            const uint64_t bb = shfl64(b, src);
-            if ((wmask >> src) & 1ull) {
-                // the four floats j..j+3 touch at most two cells; each cell's one-hot 1 sits at 17*cell + e
-                const int c0 = j / 17;
-                const int c1 = c0 + 1 < 16 ? c0 + 1 : 15;
-                const int p0 = 17 * c0 + (int)nib(bb, c0);
-                const int p1 = 17 * c1 + (int)nib(bb, c1);
-                float4 v;
-                v.x = (j == p0 || j == p1) ? 1.0f : 0.0f;
-                v.y = (j + 1 == p0 || j + 1 == p1) ? 1.0f : 0.0f;
-                v.z = (j + 2 == p0 || j + 2 == p1) ? 1.0f : 0.0f;
-                v.w = (j + 3 == p0 || j + 3 == p1) ? 1.0f : 0.0f;
-                st_obs(dst, q, v);
+            for (int k = 0; k < 68; k++) {
+                const int q = k * 64 + lane;
+                const int src = q / 68;
+                st_obs(dst, q, value(q, src, shfl64(b, src)));
+            }
+        } else {
+#pragma unroll 4
+            for (int k = 0; k < 68; k++) {
+                const int q = k * 64 + lane;
+                const int src = q / 68;
+                const uint64_t bb = shfl64(b, src);
+                if ((wmask >> src) & 1ull) st_obs(dst, q, value(q, src, bb));
             }
         }
     } else if constexpr (OBS == G2048_OBS_LOG2 || OBS == G2048_OBS_RAW) {
@@ -411,12 +404,6 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     if (LIST && a.out.merged) st(a.out.merged, i, s.list);
     if (EXTRA && a.out.score_add) st(a.out.score_add, i, s.score);
     reset = (done || trunc) && a.auto_reset;   // board / lane state / obs are rewritten by reset_lane after the loop
-#if !G2048_RESET_FULL_STORES
-    if (reset) {
-        st(a.out.flags, i, (uint8_t)(fl | G2048_F_RESET));
-        return m;
-    }
-#endif
     // A resetting lane stores this step's board / state / stream / mask / obs like any other lane (reset_lane
     // overwrites them after the loop): the sweep's stores then cover whole lines.  A hole left for the reset pass
     // is written back as a partial line, and filled later by another partial write; HBM3E has no byte mask, so
@@ -433,12 +420,6 @@ __device__ inline uint64_t step_lane(const StepArgs& a, uint32_t i, LaneIn& x, c
     return m;
 }
 
-// G2048_STEP_SEED (tools/ A/B builds only): 0 = a lane's first pending reset reads its seed inside the sweep, behind
-// the lane's reset test (shipped); 1 = every lane issues that read (lanes without a new reset re-read lane w0's seed),
-// so the sweep's vector-memory count is the same on every path
-#ifndef G2048_STEP_SEED
-#define G2048_STEP_SEED 0
-#endif
 // One sweep of one wave: the step of board w0 + lane (inputs already in registers), its mask, the wave's obs.
 // A lane's first pending reset has its seed read here (`pseed`), so the read is long complete at the tail.
 template <int OBS, int RNG, int XO, int RK>
@@ -449,20 +430,6 @@ __device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, 
     uint32_t mbits = 0;
     uint64_t b = 0;
     if (i < a.n) b = step_lane<RNG, XO, RK>(a, i, x, lut, code, wobs, reset, mbits);
-#if G2048_STEP_SEED == 1   // A/B: the seed read issued by every lane (non-resetting lanes re-read lane w0's line)
-    if constexpr (RNG == G2048_RNG_PCG64) {
-        const uint64_t sd = ld(a.L.seed, (reset && !pending) ? i : (w0 < a.n ? w0 : a.n - 1u));
-        if (reset) {
-            if (!pending) pseed = sd;
-            pending |= 1ull << k;
-        }
-    } else {
-        if (reset) {
-            if (!pending) pseed = x.seed;
-            pending |= 1ull << k;
-        }
-    }
-#else
     if (reset) {
         if (!pending) {
             if constexpr (RNG == G2048_RNG_PCG64) pseed = ld(a.L.seed, i);
@@ -470,7 +437,6 @@ __device__ __forceinline__ void sweep(const StepArgs& a, uint32_t w0, int lane, 
         }
         pending |= 1ull << k;
     }
-#endif
     if constexpr (XO == 3) {
         if (wobs) st(a.out.mask_bits, i, (uint8_t)mbits);
     } else {
@@ -506,43 +472,17 @@ static_assert(kTabVec % kBlock == 0, "table fill: whole chunks per thread");
 // of a 1M-board step per CU cost one pass of one wave instead of one divergent pass in most of the 16 waves.
 // (A dynamic schedule -- chunks claimed with device-scope atomics -- measured slower on MI355X: under this
 // kernel's streaming load an atomic's return takes microseconds, and same-address atomics serialize.)
-// G2048_STEP_XCD = d > 0 (tools/ A/B builds only): an XCD-aware static partition instead
-// of the strided one -- block b takes a contiguous range of 64-board chunks, base + d of them when its XCD group
-// (b % 8) is one of the early-dispatched 0..3 and base - d for 4..7 (profiles/round3/step_diag: groups 4..7 enter
-// up to 1.9 us later), its waves taking the range's chunks w, w + 16, ...  Falls back to equal ranges when the
-// chunk count does not divide evenly.
-#ifndef G2048_STEP_XCD
-#define G2048_STEP_XCD 0
-#endif
+// (Round 4: an XCD-aware static partition -- contiguous chunk ranges, larger for the early-dispatched XCD groups --
+// measured no gain against this strided one, profiles/round4/r4c10/ab_xcd.log.)
 template <int OBS, int RNG, bool LDS, int XO, int U, int RK>
 __global__ void __launch_bounds__(kBlock) step_kernel(StepArgs a) {
     static_assert(U == 1, "one board per lane per sweep");
     __shared__ uint4 tab_lds[LDS ? kStepLdsVec : 1];
     const int lane = threadIdx.x & 63;
-#if G2048_STEP_XCD
-    uint32_t w_first, wend;
-    const uint32_t wstride = kBlock;
-    {
-        const uint32_t nc = (a.n + 63u) >> 6, G = gridDim.x, base = nc / G, d = G2048_STEP_XCD;
-        uint32_t cs, ce;
-        if ((G & 7u) == 0u && nc % G == 0u && base > 2u * d && base + d <= 64u * (kBlock / 64)) {
-            const uint32_t x = blockIdx.x & 7u, i = blockIdx.x >> 3;
-            cs = i * 8u * base + (x < 4u ? x * (base + d) : 4u * (base + d) + (x - 4u) * (base - d));
-            ce = cs + (x < 4u ? base + d : base - d);
-        } else {
-            cs = (uint32_t)(((uint64_t)nc * blockIdx.x) / G);
-            ce = (uint32_t)(((uint64_t)nc * (blockIdx.x + 1u)) / G);
-        }
-        w_first = (cs + (threadIdx.x >> 6)) * 64u;
-        wend = ce * 64u < a.n ? ce * 64u : a.n;
-    }
-    const uint32_t last = (wend > 0u ? wend : 1u) - 1u;
-#else
     const uint32_t w_first = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
     const uint32_t wstride = gridDim.x * kBlock;
     const uint32_t wend = a.n;
     const uint32_t last = a.n - 1u;           // n >= 1 (the launcher never launches n == 0)
-#endif
     const auto lane_at = [&](uint32_t w) { return w + lane < last ? w + lane : last; };
     G2048_TS(0);
     LaneIn A, B, C;
@@ -907,9 +847,8 @@ void launch_step_u(const StepArgs& a, int cus, hipStream_t s) {
     if (G2048_DIAG && (a.diag & 8)) grid = grid_for(a.n, kBlock, 1 << 30);
     int xo = a.out.merged ? 2 : (a.out.prev_board || a.out.reward64 || a.out.score_add) ? 1 : 0;
     if (xo == 0 && a.out.mask_bits && !a.out.mask) xo = 3;
-    // the lean summary path: log2 rewards, no score / merged-list outputs (G2048_LEAN=0 builds keep the general
-    // path for every config -- tools/ A/B only)
-    const int rk = G2048_LEAN && a.rc.reward_mode == 1 && (xo == 0 || xo == 3) ? 1 : 0;
+    // the lean summary path: log2 rewards, no score / merged-list outputs
+    const int rk = a.rc.reward_mode == 1 && (xo == 0 || xo == 3) ? 1 : 0;
     if (lds) launch_step3<OBS, RNG, true, kU>(a, grid, xo, rk, s);
     else launch_step3<OBS, RNG, false, kU>(a, grid, xo, rk, s);
 }

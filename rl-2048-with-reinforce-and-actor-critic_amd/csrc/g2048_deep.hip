@@ -221,16 +221,12 @@ struct DeepSmem {
 // load exceeded the one k-tile of round 4's double buffer.  Past the end the window reloads the last k-tile
 // (harmless, an L1 hit).  (Without a barrier hipcc sank every fragment load next to its MFMA and waited for it there:
 // four L2 round trips per k-tile.)  Same MFMAs in the same order as a plain loop.
-#ifndef G2048_DEEP_CHAIN_WINDOW
-#define G2048_DEEP_CHAIN_WINDOW 1
-#endif
 template <int STRIDE = kActStride>
 __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, const float* in, int t0, int t1, int h,
                                                int col) {
     floatx16 c = {};
     if (t0 >= t1) return c;
     float4 fa[4], fb[4];
-#if G2048_DEEP_CHAIN_WINDOW
     const auto seg = [&](float4& f, int t, int q, int tn) {
         const float* ib = in + (32 * t + 4 * h) * STRIDE + col + 8 * q * STRIDE;   // k-step 4 q + u: row 8 q + u + 4 h
         c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, ib[0 * STRIDE], c, 0, 0, 0);
@@ -258,33 +254,6 @@ __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, co
 #pragma unroll
         for (int q = 0; q < 4; q++) seg(fa[q], t, q, last);
     }
-#else   // round 4's double buffer (A/B builds)
-    const auto tile = [&](const float4 (&f)[4], int t) {
-        const float* ib = in + (32 * t + 4 * h) * STRIDE + col;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].x, ib[(8 * q + 0) * STRIDE], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].y, ib[(8 * q + 1) * STRIDE], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].z, ib[(8 * q + 2) * STRIDE], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(f[q].w, ib[(8 * q + 3) * STRIDE], c, 0, 0, 0);
-        }
-    };
-#pragma unroll
-    for (int q = 0; q < 4; q++) fa[q] = fo[t0 * 256 + q * 64];
-    int t = t0;
-    for (; t + 1 < t1; t += 2) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) fb[q] = fo[(t + 1) * 256 + q * 64];
-        __builtin_amdgcn_sched_barrier(0);
-        tile(fa, t);
-        const int tn = t + 2 < t1 ? t + 2 : t + 1;   // past the end: a harmless reload of the last k-tile
-#pragma unroll
-        for (int q = 0; q < 4; q++) fa[q] = fo[tn * 256 + q * 64];
-        __builtin_amdgcn_sched_barrier(0);
-        tile(fb, t + 1);
-    }
-    if (t < t1) tile(fa, t);
-#endif
     return c;
 }
 
@@ -353,58 +322,6 @@ __device__ __forceinline__ void dense_fwd_split(const float* in, float* out, con
 // The forward of the group's 32 boards (S.board) through every hidden layer, leaving the output layer's 8 partial
 // sums per board in S.part (the caller adds them in order p = 0..7 plus the output bias).  Every thread of the
 // workgroup calls it; it ends with a barrier.
-// cells of the one-hot gather unrolled per batch of loads (16 / this L2 round trips per group when every tile is
-// present; x 4 tiles for the gradient kernel, x 8 / 2 for deep_forward)
-#ifndef G2048_DEEP_GATHER_UNROLL
-#define G2048_DEEP_GATHER_UNROLL 4
-#endif
-// the one-hot rollout on 64-slot 8-wave workgroups (deep_forward64): 1 on, 0 off = 32-slot 4-wave ones (A/B builds)
-#ifndef G2048_ROLL64
-#define G2048_ROLL64 1
-#endif
-// deep_forward64's layer-0 fragment window in cells: 1 (2 measured 0.2606-0.2615 s against 0.2595-0.2599 s,
-// `profiles/round5/r6a/`; 3 spills)
-#ifndef G2048_ROLL64_L0_AHEAD
-#define G2048_ROLL64_L0_AHEAD 1
-#endif
-// deep_forward's one-hot layer 0: 0 = the bf16-plane MFMA form (round 5), 1 = round 4's W1-row gather (A/B builds)
-#ifndef G2048_DEEP_L0_GATHER
-#define G2048_DEEP_L0_GATHER 0
-#endif
-
-// One-hot layer-0 gather of one board: acc[m] += W1 row (17 c + e_c), units 32 (m0 + m) + 4 k .. + 3 (`tab` points
-// at unit 32 m0 + 4 k of row 0), summed over the 16 cells in cell order, for the tiles m < mcount (wave-uniform).
-// With all NM tiles present the loads carry no guard, so a batch of cells issues back to back: a per-load guard
-// made the compiler wait for every load before the next (one L2 round trip per load).  Same adds, same order
-// either way, so every kernel that gathers (rollout, policy, probe, gradient) computes the same bits.
-template <int NM, int UNROLL = (NM == 4 ? G2048_DEEP_GATHER_UNROLL : (G2048_DEEP_GATHER_UNROLL + 1) / 2)>
-__device__ __forceinline__ void onehot_gather(const float* tab, uint64_t b, int H, int mcount, float4 (&acc)[NM]) {
-    const auto add = [](float4& s, const float4 v) {
-        s.x += v.x;
-        s.y += v.y;
-        s.z += v.z;
-        s.w += v.w;
-    };
-    if (mcount >= NM) {
-#pragma unroll UNROLL
-        for (int c = 0; c < 16; c++) {
-            const float* row = tab + (int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * H;
-            float4 v[NM];
-#pragma unroll
-            for (int m = 0; m < NM; m++) v[m] = *reinterpret_cast<const float4*>(row + 32 * m);
-#pragma unroll
-            for (int m = 0; m < NM; m++) add(acc[m], v[m]);
-        }
-    } else {
-#pragma unroll 4
-        for (int c = 0; c < 16; c++) {
-            const float* row = tab + (int64_t)(17 * c + (int)((b >> (4 * c)) & 15u)) * H;
-#pragma unroll
-            for (int m = 0; m < NM; m++)
-                if (m < mcount) add(acc[m], *reinterpret_cast<const float4*>(row + 32 * m));
-        }
-    }
-}
 
 // Entry 2 e + hh of the one-hot B-operand table: exponent e as 8 bf16 (1.0 at k = e, else 0) for the lane half hh
 // (k = 8 hh .. 8 hh + 7).  Looked up per cell from LDS by the layer-0 kernels: built by compares and selects it was
@@ -432,12 +349,6 @@ __device__ __forceinline__ uint4 onehot_entry(uint32_t idx) {
 // a board never drains the previous group's stores.  Per 32-sample group and CU: 3,072 MFMA cycles per SIMD, 32 KiB
 // written.
 constexpr int kL0Waves = 8;
-#ifndef G2048_L0_SB
-#define G2048_L0_SB 1   // cells per scheduling region in onehot_l0_mfma_kernel (A/B builds)
-#endif
-#ifndef G2048_L0_PROBE
-#define G2048_L0_PROBE 0   // tools-only timing probes (1: no stores, 2: no MFMAs); 0 ships
-#endif
 template <int ACT>
 __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNet net, const float* __restrict__ P,
                                                                           const uint64_t* __restrict__ boards,
@@ -489,19 +400,14 @@ __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNe
 #pragma unroll
         for (int c = 0; c < 16; c++) {
             const bf16x8 bn = onehot(c < 14 ? c + 2 : 15), ln = wlo[w][c < 14 ? c + 2 : 15][lane];
-#if G2048_L0_PROBE == 2   // tools-only timing probe: no MFMAs (wrong results)
-            hi[c] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, bv)[0]);
-            lo[c] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, lv)[0] ^ __builtin_bit_cast(u32x4, wp[c][0])[1]);
-#else
             hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][0], bv, hi, 0, 0, 0);
             lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][1], bv, lo, 0, 0, 0);
             lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lv, bv, lo, 0, 0, 0);
-#endif
             bv = bv1;
             lv = lv1;
             bv1 = bn;
             lv1 = ln;
-            if ((c + 1) % G2048_L0_SB == 0) __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
     float res[16];
@@ -512,9 +418,6 @@ __global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNe
     const uint32_t wu = (uint32_t)__builtin_amdgcn_readfirstlane(w);   // the row offset is scalar (soffset)
     // buffer stores, issued by every lane (a lane past `left` stores past num_records: dropped): no branch
     const auto store = [&](uint32_t g) {
-#if G2048_L0_PROBE == 1   // tools-only timing probe: no stores (wrong results)
-        if (n != 0xFFFFFFFFu) return;
-#endif
         const uint32_t left = n - g * 32u < 32u ? n - g * 32u : 32u;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             out + (size_t)g * 32u * (uint32_t)H, 0, (int)(left * (uint32_t)H * 4u), 0x00020000);
@@ -604,7 +507,7 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
         const int nt0 = net.nt[0];
         if constexpr (A0IN) {
             load_l0_block<kDeepBlock>(a0, n, gi, 32 * nt0, out);
-        } else if constexpr (OBS == G2048_OBS_ONEHOT && !G2048_DEEP_L0_GATHER) {
+        } else if constexpr (OBS == G2048_OBS_ONEHOT) {
             // the update's layer-0 arithmetic (onehot_l0_mfma_kernel), W1's plane fragments streamed from the
             // packed net: wave w, unit tiles w, w + 4; per cell one exact one-hot B operand and 3 MFMAs (hi plane
             // into `hi`, the mid and lo planes into `lo`), cell by cell; act((hi + lo) + b1) -- the same bits in
@@ -645,31 +548,6 @@ __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, De
 #pragma unroll
                 for (int i = 0; i < 16; i++)
                     out[(32 * t + tile_row(i, h)) * kActStride + col] = activate<ACT>((hi[i] + lo[i]) + bv[i]);
-            }
-        } else if constexpr (OBS == G2048_OBS_ONEHOT) {
-            // (A/B builds, G2048_DEEP_L0_GATHER=1: round 4's gather)
-            // wave w: boards 8 w .. 8 w + 7, 8 lanes per board; lane k of a board: units 4 k + 32 m (m < nt0)
-            const int bb = 8 * w + (lane >> 3), k = lane & 7;
-            const uint64_t b = S.board[bb];
-            const int H = 32 * nt0;
-            const float* tab = P + net.w[0] + 4 * k;
-            float4 acc[8];
-#pragma unroll
-            for (int m = 0; m < 8; m++) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
-            onehot_gather<8>(tab, b, H, nt0, acc);
-            float4 bv[8];   // bias loads issued together (clamped index: always a valid address)
-#pragma unroll
-            for (int m = 0; m < 8; m++)
-                bv[m] = *reinterpret_cast<const float4*>(P + net.b[0] + 32 * (m < nt0 ? m : nt0 - 1) + 4 * k);
-#pragma unroll
-            for (int m = 0; m < 8; m++) {
-                if (m < nt0) {
-                    const int u = 32 * m + 4 * k;
-                    out[(u + 0) * kActStride + bb] = activate<ACT>(acc[m].x + bv[m].x);
-                    out[(u + 1) * kActStride + bb] = activate<ACT>(acc[m].y + bv[m].y);
-                    out[(u + 2) * kActStride + bb] = activate<ACT>(acc[m].z + bv[m].z);
-                    out[(u + 3) * kActStride + bb] = activate<ACT>(acc[m].w + bv[m].w);
-                }
             }
         } else {
             const uint64_t b = S.board[col];
@@ -760,7 +638,7 @@ __device__ void deep_forward64(const DeepNet& net, const float* __restrict__ P, 
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     // ---- layer 0: wave w owns unit tile w for both 32-board column tiles (one fragment stream, two B operands;
-    //      fragments G2048_ROLL64_L0_AHEAD cells ahead; the bias is loaded after the chain, beside which the four
+    //      fragments one cell ahead; the bias is loaded after the chain, beside which the four
     //      accumulator tiles are live)
     {
         float* out = S.act[0];
@@ -769,7 +647,7 @@ __device__ void deep_forward64(const DeepNet& net, const float* __restrict__ P, 
             const int t = w;
             const uint64_t b0 = S.board[col], b1 = S.board[32 + col];
             const u32x4* ft = reinterpret_cast<const u32x4*>(P + net.wpl) + lane + (int64_t)t * (kOneHotPlaneFloats / 4);
-            constexpr int kAhead = G2048_ROLL64_L0_AHEAD;   // cells of fragments in flight ahead of the MFMAs
+            constexpr int kAhead = 1;   // cells of fragments in flight ahead of the MFMAs
             u32x4 f[kAhead + 1][3];
 #pragma unroll
             for (int q = 0; q < kAhead; q++)
@@ -1086,12 +964,6 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
         if (need && idx < a.n_order) start(a.order ? (uint32_t)a.order[idx] : idx);
         drained = __ballot(need && idx >= a.n_order) != 0ull;
     };
-#if G2048_ROLL_STAGGER   // A/B builds: delay one of each pair of workgroups by G2048_ROLL_STAGGER x 10 ns
-    if (G2048_DEEP_STAGGER_SEL == 0 ? blockIdx.x >= gridDim.x / 2 : (blockIdx.x & 1u) != 0u) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)G2048_ROLL_STAGGER) __builtin_amdgcn_s_sleep(4);
-    }
-#endif
 #if G2048_DEEP_DIAG
     DiagClock dclk{};
     dclk.last = __builtin_amdgcn_s_memtime();
@@ -1215,66 +1087,14 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
 //     accumulator registers per wave.
 // (A 4-wave workgroup alone per CU with 12 tiles per wave took the whole register file, one wave per SIMD.)
 constexpr int kDeepGradMaxBlock = 512;
-// the 4-wave instantiation's k-split of its 64-unit layer (dense_fwd_split MODE 2): 1 on, 0 off (A/B builds)
-#ifndef G2048_DEEP_SPLIT4
-#define G2048_DEEP_SPLIT4 0
-#endif
-// log2 / raw nets of 49..64 dense tiles (configs[2]'s [256, 256]) on the 8 x 8 instantiation too: 1 = on (A/B builds
-// only -- it spills ~300 VGPRs; the shipped path is the two-layer cooperative kernel)
-#ifndef G2048_DEEP_LOG2_64
-#define G2048_DEEP_LOG2_64 0
-#endif
-// the one-hot gradient kernel's layer 0 computed in the kernel from W1's packed planes (1) instead of read back
-// from onehot_l0_mfma_kernel's blocks (0, with the next-group LDS-DMA prefetch below) -- A/B builds.  Fused measured
-// 1.363-1.365 s against 1.355-1.359 s (`profiles/round5/r6b/`): the separate kernel's 0.126 s go, but the group
-// grows 105.7 k -> 118.3 k cycles (the plane stream one cell ahead is latency-bound beside 10 accumulator tiles)
-#ifndef G2048_DEEP_L0_FUSED
-#define G2048_DEEP_L0_FUSED 0
-#endif
-// the one-hot gradient kernel's next-group layer-0 prefetch (unfused layer 0 only): 1 on, 0 off (A/B builds)
-#ifndef G2048_DEEP_L0_PREFETCH
-#define G2048_DEEP_L0_PREFETCH 1
-#endif
-#ifndef G2048_DEEP_D0_UNROLL   // the delta_0 row stores per batch
-#define G2048_DEEP_D0_UNROLL 32
-#endif
-// One unit tile t of a one-hot layer 0 for 32 boards (lane col: board b) by the exact bf16-plane MFMAs of
-// onehot_l0_mfma_kernel (same bits), W1's plane fragments streamed from the packed net one cell ahead, the bias
-// loaded after the chain; writes act((hi + lo) + b1) to out[unit * stride + col].  The gradient kernel's fused
-// layer 0 (G2048_DEEP_L0_FUSED).
-template <int ACT>
-__device__ __forceinline__ void onehot_l0_tile(const float* __restrict__ P, const DeepNet& net, int t, uint64_t b,
-                                               float* out, int stride) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
-    const u32x4* ft = reinterpret_cast<const u32x4*>(P + net.wpl) + lane + (int64_t)t * (kOneHotPlaneFloats / 4);
-    u32x4 f[2][3];
-#pragma unroll
-    for (int pl = 0; pl < 3; pl++) f[0][pl] = ft[pl * 64];
-    floatx16 hi = {}, lo = {};
-#pragma unroll
-    for (int c = 0; c < 16; c++) {
-        if (c + 1 < 16) {
-#pragma unroll
-            for (int pl = 0; pl < 3; pl++) f[(c + 1) & 1][pl] = ft[((c + 1) * 3 + pl) * 64];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
-        u32x4 dv;
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++)
-            dv[jj] = (nib == (uint32_t)(8 * h + 2 * jj) ? 0x3F80u : 0u) | (nib == (uint32_t)(8 * h + 2 * jj + 1) ? 0x3F800000u : 0u);
-        const bf16x8 bvv = __builtin_bit_cast(bf16x8, dv);
-        hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][0]), bvv, hi, 0, 0, 0);
-        lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][1]), bvv, lo, 0, 0, 0);
-        lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][2]), bvv, lo, 0, 0, 0);
-    }
-    float bv[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) bv[i] = P[net.b[0] + 32 * t + tile_row(i, h)];
-#pragma unroll
-    for (int i = 0; i < 16; i++) out[(32 * t + tile_row(i, h)) * stride + col] = activate<ACT>((hi[i] + lo[i]) + bv[i]);
-}
+// Tried, not kept (measured on the runner config; the A/B switches are gone from the source): the 4-wave
+// instantiation's 64-unit layer as a 4-way k split (no change); log2 / raw nets of 49..64 dense tiles on the 8 x 8
+// instantiation (spills ~300 VGPRs; the two-layer cooperative kernel runs them); the one-hot layer 0 computed in the
+// kernel from W1's packed planes instead of read back from onehot_l0_mfma_kernel's blocks -- its 0.126 s go, but the
+// group grows 105.7 k -> 118.3 k cycles (the plane stream is latency-bound beside 10 accumulator tiles): update
+// 1.278-1.281 s against 1.251 s (round 6, profiles/round6/r7a/l0fused_*; round 5: profiles/round5/r6b/); the
+// delta_0 rows by 16-byte stores (a quarter of the store instructions): 1.2535-1.2542 s against 1.2499-1.2517 s
+// (profiles/round6/r7b/d0b128_*).
 
 struct DeepGradVariant {
     int nw, tpw, ksplit, per_cu, passes;   // passes > 1: the dense dW tiles in ranges of nw x tpw, one launch each
@@ -1331,25 +1151,9 @@ struct DeepGradArgs {
 // __syncthreads() adds a workgroup release fence, i.e. vmcnt(0): every barrier would wait for the wave's global
 // stores (the V(s) / delta_0 rows) and for the weight-fragment loads a chain's window left in flight, none of which
 // another wave reads (loaded values are waited for at their use, as always).  The group's first barrier keeps
-// __syncthreads(): it retires the layer-0 LDS-DMA.  G2048_DEEP_RAW_BARRIER=0: __syncthreads() everywhere (A/B).
-#ifndef G2048_DEEP_RAW_BARRIER
-#define G2048_DEEP_RAW_BARRIER 1
-#endif
-#ifndef G2048_DEEP_NO4
-#define G2048_DEEP_NO4 0   // A/B builds: one-hot nets of <= 40 tiles on the 8-wave instantiations instead of 4 x 10
-#endif
-#ifndef G2048_DEEP_STASH
-#define G2048_DEEP_STASH 1   // deep_grad_kernel's per-sample inputs and db_out sums in LDS (0: registers, A/B)
-#endif
-#ifndef G2048_DEEP_SCALAR_W
-#define G2048_DEEP_SCALAR_W 1   // deep_grad_kernel's wave index as a scalar (0: per-lane, A/B)
-#endif
+// __syncthreads(): it retires the layer-0 LDS-DMA.  (__syncthreads() everywhere measured the same, round 5.)
 __device__ __forceinline__ void lds_barrier() {
-#if G2048_DEEP_RAW_BARRIER
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
-    __syncthreads();
-#endif
 }
 
 template <int ACT>
@@ -1367,7 +1171,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     // w through readfirstlane: the wave index and everything derived from it (tile ranges, LDS bases) live in
     // SGPRs -- as a per-lane value hipcc kept them in VGPRs and the 4 x 10 instantiation spilled 41 of them
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31,
-              w = G2048_DEEP_SCALAR_W ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
+              w = __builtin_amdgcn_readfirstlane(tid >> 6);
     // LDS: the hidden layers' activations (deltas overwrite them top down; layer l at aoff[l]), the output
     // partials, g, the boards and each thread's bias-gradient sums
     const auto actl = [&](int l) { return dyn + a.aoff[l]; };
@@ -1377,13 +1181,13 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     uint64_t* bds = reinterpret_cast<uint64_t*>(lds_end + 8 * 32 * 4 + 32 * 4);  // [32]
     float* dbs = lds_end + 8 * 32 * 4 + 32 * 4 + 64;                             // [kMaxHidden][256]: db_l of unit tid
     float* wol = dbs + kMaxHidden * 256;                                         // [HL][4] output weights, then [4] bias
-    // G2048_DEEP_STASH: the group's per-sample inputs (coef, action, target / TD row: [7][32]) and the db_out sums
-    // ([32][4]) in LDS instead of registers across the forward and delta chains
+    // the group's per-sample inputs (coef, action, target / TD row: [7][32]) and the db_out sums ([32][4]) in LDS
+    // instead of registers across the forward and delta chains (round 5: 29 -> 16 spilled VGPRs)
     float* smp_in = wol + 256 * 4 + 4;
     float* dbo_l = smp_in + 7 * 32;
     if (tid < 256)
         for (int l = 0; l < kMaxHidden; l++) dbs[l * 256 + tid] = 0.0f;
-    if (G2048_DEEP_STASH && tid < 128) dbo_l[tid] = 0.0f;
+    if (tid < 128) dbo_l[tid] = 0.0f;
     const float* P = a.packed;
     {   // the output layer's weights and bias in LDS for the whole launch (its phases read them every group)
         const int HLw = 32 * net.nt[L - 1] * 4;
@@ -1398,18 +1202,12 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     for (int i = 0; i < kA0; i++) acc0[i] = floatx16{};
     // dW_out / db_{L-1} partials of this thread's (unit, sample range); db_out: threads 0..31 sum their sample slot's
     // g over the groups (the slots are added in order at the end)
-    float dwo[4] = {0.f, 0.f, 0.f, 0.f}, dbl = 0.f, dbo4[4] = {0.f, 0.f, 0.f, 0.f};
+    float dwo[4] = {0.f, 0.f, 0.f, 0.f}, dbl = 0.f;
     const int HL = 32 * net.nt[L - 1];
     const int oq = kBlock / HL, oper = (32 + oq - 1) / oq;   // sample ranges of the output layer
     const float4* wout = reinterpret_cast<const float4*>(wol);
     const float* bo = wol + 4 * HL;
     const uint32_t groups = (a.n + 31u) >> 5;
-#if G2048_DEEP_STAGGER   // A/B builds: delay one of each pair of workgroups by G2048_DEEP_STAGGER x 10 ns
-    if (G2048_DEEP_STAGGER_SEL == 0 ? blockIdx.x >= gridDim.x / 2 : (blockIdx.x & 1u) != 0u) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)G2048_DEEP_STAGGER) __builtin_amdgcn_s_sleep(4);
-    }
-#endif
 #if G2048_DEEP_DIAG
     uint64_t dph[kDiagSlots] = {};
     uint64_t dlast = __builtin_amdgcn_s_memtime();
@@ -1421,7 +1219,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     // would drain the DMA there), and the next group's first barrier retires it.  Its forward then only re-strides
     // the block from LDS (the load had been 10 % of the group).  Whole groups only; the launch's last, ragged group
     // reads its block in place.
-    constexpr bool kPrefetch = OBS == G2048_OBS_ONEHOT && G2048_DEEP_L0_PREFETCH && !G2048_DEEP_L0_FUSED;
+    constexpr bool kPrefetch = OBS == G2048_OBS_ONEHOT;
     const int H0a = 32 * net.nt[0];
     float* stage = dyn + a.aoff[0] + H0a * kActStride;   // [unit][32]: deep_grad_act_floats leaves room
     const auto whole = [&](uint32_t g) { return g < groups && a.n - g * 32u >= 32u; };
@@ -1460,7 +1258,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             }
         }
         __syncthreads();   // (a fence: vmcnt(0) -- the loads above have arrived)
-        if (G2048_DEEP_STASH && tid < 32) {   // read back at the logits: their registers are free until then
+        if (tid < 32) {   // read back at the logits: their registers are free until then
             smp_in[tid] = cf;
             smp_in[32 + tid] = __uint_as_float(act_j);
             smp_in[64 + tid] = tg;
@@ -1477,9 +1275,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             if constexpr (OBS == G2048_OBS_ONEHOT) {
                 // the group's block from onehot_l0_mfma_kernel (in d0_out: this workgroup overwrites the same rows
                 // with the group's layer-0 deltas at its end)
-                if constexpr (G2048_DEEP_L0_FUSED) {
-                    for (int t = w; t < nt0; t += NW) onehot_l0_tile<ACT>(P, net, t, bds[col], out, kActStride);
-                } else if (kPrefetch && whole(gi)) {   // the staged block (its DMA retired by the barrier above)
+                if (whole(gi)) {   // the staged block (its DMA retired by the barrier above)
                     const float4* st4 = reinterpret_cast<const float4*>(stage);
 #pragma unroll 4
                     for (int e4 = tid; e4 < 8 * H0a; e4 += kBlock) {
@@ -1516,9 +1312,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         lds_barrier();
         DEEP_STAMP(1);
         if (tid < 32 && a.critic && a.has_td) {
-            const int64_t tl = G2048_DEEP_STASH ? (int64_t)((uint64_t)__float_as_uint(smp_in[160 + tid]) |
-                                                            ((uint64_t)__float_as_uint(smp_in[192 + tid]) << 32))
-                                                : td_l;
+            const int64_t tl = (int64_t)((uint64_t)__float_as_uint(smp_in[160 + tid]) |
+                                         ((uint64_t)__float_as_uint(smp_in[192 + tid]) << 32));
             td_v = a.td.v_next[tl];
         }
         // ---- forward: dense layers (each into its own region)
@@ -1565,10 +1360,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         DEEP_STAMP(3);
         // ---- logits -> g (threads 0..31, one sample each)
         if (tid < 32) {
-            const float cf_ = G2048_DEEP_STASH ? smp_in[tid] : cf;
-            const uint32_t act_j_ = G2048_DEEP_STASH ? __float_as_uint(smp_in[32 + tid]) : act_j;
-            float tg_ = G2048_DEEP_STASH ? smp_in[64 + tid] : tg;
-            const float td_r_ = G2048_DEEP_STASH ? smp_in[96 + tid] : td_r, td_h_ = G2048_DEEP_STASH ? smp_in[128 + tid] : td_h;
+            const float cf_ = smp_in[tid];
+            const uint32_t act_j_ = __float_as_uint(smp_in[32 + tid]);
+            float tg_ = smp_in[64 + tid];
+            const float td_r_ = smp_in[96 + tid], td_h_ = smp_in[128 + tid];
             float lg[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -1608,8 +1403,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 gs[tid][k] = g[k];
-                if (G2048_DEEP_STASH) dbo_l[tid * 4 + k] += g[k];
-                else dbo4[k] += g[k];
+                dbo_l[tid * 4 + k] += g[k];
             }
         }
         lds_barrier();
@@ -1699,7 +1493,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 const uint32_t left = a.n - gi * 32u < 32u ? a.n - gi * 32u : 32u;
                 const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
                     a.d0_out + (size_t)gi * 32u * (uint32_t)H0, 0, (int)(left * (uint32_t)H0 * 4u), 0x00020000);
-#pragma unroll G2048_DEEP_D0_UNROLL
+#pragma unroll
                 for (int n2 = 0; n2 < 32; n2++)
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(drow[n2]), rd, tid * 4, n2 * H0 * 4, 0);
             }
@@ -1746,7 +1540,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         float* red = dyn;                                   // [oq][HL][5]
         if (tid < 32) {
 #pragma unroll
-            for (int k = 0; k < 4; k++) gs[tid][k] = G2048_DEEP_STASH ? dbo_l[tid * 4 + k] : dbo4[k];
+            for (int k = 0; k < 4; k++) gs[tid][k] = dbo_l[tid * 4 + k];
         }
         if (tid < oq * HL) {
 #pragma unroll
@@ -1875,7 +1669,7 @@ int64_t deep_grad_act_floats(const DeepNet& n, int nw) {
     int64_t f = units * kActStride;
     const int64_t red = 5 * 64 * nw;
     if (red > f) f = red;
-    if (n.onehot && G2048_DEEP_L0_PREFETCH && !G2048_DEEP_L0_FUSED) {
+    if (n.onehot) {
         const int64_t st = 32 * n.nt[0] * (kActStride + 32);
         if (st > f) f = st;
     }
@@ -1883,7 +1677,7 @@ int64_t deep_grad_act_floats(const DeepNet& n, int nw) {
 }
 int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, bias sums, output weights / bias
     return (deep_grad_act_floats(n, nw) + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256 + 256 * 4 + 4 +
-            (G2048_DEEP_STASH ? 7 * 32 + 32 * 4 : 0)) * 4;
+            7 * 32 + 32 * 4) * 4;
 }
 
 // the instantiation that covers the net (nw = 0: none; see deep_grad_kernel).  The 4-wave and the 64-tile ones are
@@ -1891,10 +1685,10 @@ int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, 
 // of 10 or 8 dense tiles per wave, hipcc spills whole accumulator tiles (~300-650 VGPRs).
 DeepGradVariant deep_grad_variant(const DeepNet& n) {
     const int tiles = deep_grad_layout(n).ntiles;
-    if (!G2048_DEEP_NO4 && n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024)
-        return {4, 10, G2048_DEEP_SPLIT4 ? 2 : 0, 2, 1};
+    if (n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024)
+        return {4, 10, 0, 2, 1};
     if (tiles <= 48 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 6, 1, 1, 1};
-    if ((n.onehot || G2048_DEEP_LOG2_64) && tiles <= 64 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 8, 1, 1, 1};
+    if (n.onehot && tiles <= 64 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 8, 1, 1, 1};
     // past one launch's accumulator budget (round 5; e.g. one-hot [256, 256, 256], log2 [256, 256]): the dense dW
     // tiles in ranges, one launch per range, each redoing the forward and the delta chains (the dW MFMAs, a third
     // of the work, are split); 64 tiles per launch on one-hot nets, 48 on log2 / raw (whose 8 x 8 instantiation
@@ -1930,73 +1724,6 @@ __global__ void __launch_bounds__(256) onehot_l1_kernel(const float* __restrict_
     }
 }
 
-// dW1 / db1 partials of a one-hot first layer: block (slice, part) owns units [64 slice, 64 slice + 64) and
-// samples [part * per, ...): dW1[17 c + e_c(s)][j] += d1[s][j] in sample order, then slab rows 0..271 = dW1 and row
-// 272 = db1 of its columns.  Accumulated in registers: wave k of the 4 owns cells 4k .. 4k + 3, lane = unit, one
-// 16-float array per cell indexed by the cell's nibble -- the board is the same for the whole wave, so the index
-// is scalar and `acc[e] += v` is a register-relative move, an add and a move back (no memory round trip; row
-// 17 c + 16, exponent 16, never occurs on a bitboard and stays zero).  Each row's adds run in sample order:
-// deterministic.  (Round 4 before this: a [272][64] LDS accumulator, each add a read-modify-write that waited for
-// its read -- latency-bound at ~1.5 ms per 2^20 samples against ~0.3 ms for this form.)
-constexpr int kDw1Rows = kOneHotRows + 1;
-constexpr int kDw1Waves = 4;
-__global__ void __launch_bounds__(64 * kDw1Waves) onehot_dw1_kernel(const uint64_t* __restrict__ boards,
-                                                                   const float* __restrict__ d1, int h1, int64_t m,
-                                                                   int64_t ld, int64_t per, float* __restrict__ part) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int slice = blockIdx.x, p = blockIdx.y;
-    const int j = 64 * slice + lane;
-    float a0[16], a1[16], a2[16], a3[16];           // cells 4w .. 4w + 3
-#pragma unroll
-    for (int r = 0; r < 16; r++) a0[r] = a1[r] = a2[r] = a3[r] = 0.0f;
-    float db = 0.0f;
-    const int64_t s0 = (int64_t)p * per, s1 = s0 + per < m ? s0 + per : m;
-    const bool live = j < h1;
-    const int jc = live ? j : 0;
-    const uint32_t sh = 16u * (uint32_t)__builtin_amdgcn_readfirstlane(w);   // the four cells' nibbles
-    const auto add = [&](uint64_t b, float v) {
-        if (w == 0) db += v;
-        const uint32_t e = (uint32_t)(b >> sh);
-        a0[e & 15u] += v;
-        a1[(e >> 4) & 15u] += v;
-        a2[(e >> 8) & 15u] += v;
-        a3[(e >> 12) & 15u] += v;
-    };
-    // the boards by one vector load per 64 samples (lane l: sample c0 + l), read out per sample with v_readlane
-    const auto board_of = [](uint64_t bl, int k) -> uint64_t {
-        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)bl, k), hi = __builtin_amdgcn_readlane((uint32_t)(bl >> 32), k);
-        return ((uint64_t)hi << 32) | lo;
-    };
-    for (int64_t c0 = s0; c0 < s1; c0 += 64) {
-        const int64_t cl = c0 + lane < s1 ? c0 + lane : s1 - 1;
-        const uint64_t bl = boards[cl];
-        const int cnt = s1 - c0 < 64 ? (int)(s1 - c0) : 64;
-        int k = 0;
-        for (; k + 8 <= cnt; k += 8) {
-            float v[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) v[q] = d1[(c0 + k + q) * ld + jc];
-#pragma unroll
-            for (int q = 0; q < 8; q++) add(board_of(bl, k + q), live ? v[q] : 0.0f);
-        }
-        for (; k < cnt; k++) add(board_of(bl, k), live ? d1[(c0 + k) * ld + jc] : 0.0f);
-    }
-    float* slab = part + (int64_t)p * kDw1Rows * h1;
-    if (live) {
-        const int64_t r0 = 17 * 4 * w;
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            slab[(r0 + r) * h1 + j] = a0[r];
-            slab[(r0 + 17 + r) * h1 + j] = a1[r];
-            slab[(r0 + 34 + r) * h1 + j] = a2[r];
-            slab[(r0 + 51 + r) * h1 + j] = a3[r];
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++) slab[(r0 + 17 * q + 16) * h1 + j] = 0.0f;
-        if (w == 0) slab[(int64_t)kOneHotRows * h1 + j] = db;
-    }
-}
-
 // dW1 / db1 of a one-hot first layer on the bf16 MFMA (round 5; replaces onehot_dw1_kernel's register scatter on
 // the update path).  dW1 = X^T D1 with X the [samples][272] one-hot of the boards is a GEMM whose A operand is exact
 // in bf16 (0 / 1): v_mfma_f32_32x32x16_bf16 with A = X^T of two cells (row 16 q + e: cell 2 p + q, exponent e; k = 16
@@ -2011,6 +1738,7 @@ __global__ void __launch_bounds__(64 * kDw1Waves) onehot_dw1_kernel(const uint64
 // two lane halves added at the end.  Deltas and boards are loaded three steps ahead (a four-slot register ring)
 // through buffer resources.
 // Rows 17 c + 16 (exponent 16, never on a bitboard) are written as zeros.
+constexpr int kDw1Rows = kOneHotRows + 1;   // a dW1 partial slab: 272 rows of dW1, then db1
 constexpr int kDw1Step = 16;        // samples per MFMA k-step
 constexpr int kDw1MaxWaves = 8;     // 32 units per wave
 
@@ -2116,7 +1844,7 @@ __global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_mfma_kernel(
 }
 
 // onehot_dw1_mfma_kernel with its deltas and boards staged through an LDS ring by LDS-DMA (round 5; the shipped
-// dW1 path when d1 rows are 16-byte aligned, G2048_DW1_RING=0 for the register form).  The register form kept three
+// dW1 path when d1 rows are 16-byte aligned; any other stride takes the register form).  The register form kept three
 // steps of loads in flight on paper, but the register allocator reused in-flight load destinations as temporaries,
 // so the wait-count pass drained every load each step (vmcnt(0) in the loop): 2.9 TB/s, MFMA busy 0.40.  Here a
 // step's 16 rows (16 KiB at h1 = 256) and 16 boards go straight to LDS (global_load_lds_dwordx4: no registers) in
@@ -2124,9 +1852,6 @@ __global__ void __launch_bounds__(64 * kDw1MaxWaves, 1) onehot_dw1_mfma_kernel(
 // instructions per wave).  Row r's 16-byte chunks are stored XOR-swizzled by 8 chunks when r >= 8 so the two lane
 // halves (rows 8 h + k) read disjoint banks.  Rows past the range are clamped loads (valid memory) masked to 0 at
 // the read, and their boards to 0: the same operands, MFMAs and order as onehot_dw1_mfma_kernel, the same bits.
-#ifndef G2048_DW1_RING
-#define G2048_DW1_RING 1
-#endif
 constexpr int kDw1Slots = 8;
 #define G2048_DW1_STEP_WAIT "s_waitcnt vmcnt(15)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier"
 static_assert((kDw1Slots - 3) * 3 == 15, "G2048_DW1_STEP_WAIT: (slots - 3) steps x 3 DMA instructions in flight");
@@ -2442,7 +2167,7 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
     a.cap = (uint32_t)cap;
     hipStream_t s = (hipStream_t)stream;
     const int obs = cfg->obs_mode;
-    if (obs == G2048_OBS_ONEHOT && G2048_ROLL64) {   // persistent: one workgroup per CU, 64 slots each
+    if (obs == G2048_OBS_ONEHOT) {   // persistent: one workgroup per CU, 64 slots each
         int64_t grid = (n_order + 63) / 64;
         if (grid > (int64_t)cus) grid = cus;
         return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_ONEHOT, 0, 64>(a, (int)grid, s)
@@ -2588,9 +2313,7 @@ int launch_deep_grad_v(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t
 template <int OBS, int ACT>
 int launch_deep_grad_pass(const DeepGradArgs& a, const DeepGradVariant& v, int grid, int64_t lds, hipStream_t s) {
     if constexpr (OBS == G2048_OBS_ONEHOT) {
-        if (v.nw == 4) return launch_deep_grad_v<OBS, ACT, 4, 10, G2048_DEEP_SPLIT4 ? 2 : 0>(a, grid, lds, s);
-        if (v.tpw == 8) return launch_deep_grad_v<OBS, ACT, 8, 8, 1>(a, grid, lds, s);
-    } else if constexpr (G2048_DEEP_LOG2_64 != 0) {
+        if (v.nw == 4) return launch_deep_grad_v<OBS, ACT, 4, 10, 0>(a, grid, lds, s);
         if (v.tpw == 8) return launch_deep_grad_v<OBS, ACT, 8, 8, 1>(a, grid, lds, s);
     }
     return launch_deep_grad_v<OBS, ACT, 8, 6, 1>(a, grid, lds, s);
@@ -2677,7 +2400,7 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
     const int64_t lds = deep_grad_lds_bytes(net, v.nw);
     hipStream_t s = (hipStream_t)stream;
     const int grid = (int)nparts;   // every workgroup writes its slab (zeros when it gets no group)
-    if (obs_mode == G2048_OBS_ONEHOT && n > 0 && !G2048_DEEP_L0_FUSED) {   // layer 0 on the bf16 MFMA, into d0_out
+    if (obs_mode == G2048_OBS_ONEHOT && n > 0) {   // layer 0 on the bf16 MFMA, into d0_out
         const int rc = launch_onehot_l0(net, packed, boards, (uint32_t)n, activation, d0_out, s);
         if (rc) return rc;
     }
@@ -2717,19 +2440,14 @@ int g2048_onehot_dw1(const uint64_t* boards, const float* d1, int h1, int64_t m,
     if (per * ld * 4 >= ((int64_t)1 << 31)) return dfail(G2048_EINVAL, "one-hot dW1: per x ld too large (2 GiB per slab range)");
     if (m > 0 && (!boards || !d1 || !partials)) return dfail(G2048_EINVAL, "one-hot dW1: NULL buffer");
     if (m == 0) return G2048_OK;
-#if G2048_DW1_SCATTER   // A/B build only: round 4's register scatter
-    hipLaunchKernelGGL(onehot_dw1_kernel, dim3((h1 + 63) / 64, (unsigned)nparts), dim3(64 * kDw1Waves), 0, (hipStream_t)stream,
-                       boards, d1, h1, m, ld, per, partials);
-#else
     // 16-byte rows for the LDS-DMA ring, whose whole 16-byte chunks end exactly at unit h1 (h1 % 4 == 0: a row's
     // last chunk never reads past s * ld + h1 - 1, which the header promises is valid memory)
-    if (G2048_DW1_RING && ld % 4 == 0 && h1 % 4 == 0 && ((uintptr_t)d1 & 15u) == 0)
+    if (ld % 4 == 0 && h1 % 4 == 0 && ((uintptr_t)d1 & 15u) == 0)
         hipLaunchKernelGGL(onehot_dw1_ring_kernel, dim3((unsigned)nparts), dim3(64 * kDw1MaxWaves), 0,
                            (hipStream_t)stream, boards, d1, h1, m, ld, per, partials);
     else
         hipLaunchKernelGGL(onehot_dw1_mfma_kernel, dim3((unsigned)nparts), dim3(64 * kDw1MaxWaves), 0,
                            (hipStream_t)stream, boards, d1, h1, m, ld, per, partials);
-#endif
     return check_hip();
 }
 

@@ -60,21 +60,10 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
 #endif
 }
 
-// 256-wide second layers: G2048_DW2_WIDE 1 (default) -- one 8-wave workgroup per column range (2 waves per SIMD,
-// 8 accumulator tiles each, one register set of planes); 0 -- the 4-wave kernel with the output columns split over
-// two workgroups (each re-reads the a1 rows); the 4-wave kernel with all 256 columns spills (tools/ A/B builds:
-// G2048_DW2_WIDE=0, and G2048_DW2_SPLIT=0 for the spilling form)
-#ifndef G2048_DW2_WIDE
-#define G2048_DW2_WIDE 1
-#endif
-#ifndef G2048_DW2_SPLIT
-#define G2048_DW2_SPLIT 1
-#endif
-#ifndef G2048_DW2_WIDEPIPE
-#define G2048_DW2_WIDEPIPE 0   // 1: the wide kernel's tile-pipelined loop (measured 3-5 % slower; tools/ A/B build)
-#endif
-
-__host__ __device__ constexpr int dw2_threads(int nt2) { return G2048_DW2_WIDE && nt2 >= 8 ? 512 : 256; }
+// 256-wide second layers: one 8-wave workgroup per column range (2 waves per SIMD, 8 accumulator tiles each, one
+// register set of planes).  (Round 4: the 4-wave kernel with all 256 output columns spilled ~145 VGPRs; with the
+// columns split over two workgroups each re-read the a1 rows -- both slower, profiles/round4/r4c10/.)
+__host__ __device__ constexpr int dw2_threads(int nt2) { return nt2 >= 8 ? 512 : 256; }
 
 // MODE: 0 = d2 columns; 1 = the ReLU critic's factored records (mask words + scalar g); 2 = the ReLU actor's
 // records (mask words + the 4 values of g per sample; d2 rebuilt here)
@@ -83,11 +72,8 @@ struct Dw2 {
     static constexpr bool FAC = MODE != 0;             // a record per block instead of d2 rows
     static constexpr int H1 = 32 * NT1, H2 = 32 * NT2;
     static constexpr int RB = H1 > H2 ? H1 : H2;        // rows per 16-column block of both column buffers
-    // output column halves: a 256-wide second layer is split over two workgroups (blockIdx.y), each owning 128
-    // output columns -- with all 256 in one workgroup every wave holds 16 tiles = 256 accumulators, the whole AGPR
-    // file, and the register allocator spilled them to scratch inside the loop (~145 VGPRs)
-    static constexpr bool WIDE = G2048_DW2_WIDE && NT2 >= 8;
-    static constexpr int CS = !WIDE && G2048_DW2_SPLIT && NT2 >= 8 ? 2 : 1;
+    static constexpr bool WIDE = NT2 >= 8;
+    static constexpr int CS = 1;                        // output column ranges per column range (blockIdx.y)
     static constexpr int kW = WIDE ? 8 : 4;             // waves: a WR x WC grid over the output tiles
     static constexpr int WR = 2, WC = kW / 2;
     static constexpr int kThr = 64 * kW;
@@ -335,111 +321,6 @@ __global__ void __launch_bounds__(dw2_threads(NT2), 1) dw2_kernel(Dw2Args a) {
                 }
         }
     };
-    // the wide kernel's per-tile pieces of `load` / `mfma` (same values, same order): A tile i, the B tiles + db2
-    const auto load_a = [&](const float* st, Planes& p, int i) {
-        if (!(rows_mine && cols_mine)) return;
-        float v[8];
-        read_frag(st, 32 * (wr * G::TR + i) + r, h, v);
-        if constexpr (MODE == 1) {
-            const float* gv = st + G::kRows * kBK + 128;
-            const float4 g0 = *reinterpret_cast<const float4*>(gv + 8 * h);
-            const float4 g1 = *reinterpret_cast<const float4*>(gv + 8 * h + 4);
-            const float gk[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-#pragma unroll
-            for (int e = 0; e < 8; e++) v[e] *= gk[e];
-        }
-        split3(v, p.a0[i], p.a1[i], p.a2[i]);
-    };
-    const auto load_b = [&](const float* st, Planes& p) {
-        if constexpr (MODE == 2) {
-            const float* rec = st + G::kRows * kBK;
-            const uint16_t* mw = reinterpret_cast<const uint16_t*>(rec);
-            const float4* gv = reinterpret_cast<const float4*>(rec + 128);
-            {
-                const uint32_t m = mw[dunit];
-#pragma unroll
-                for (int e = 0; e < 16; e++) dsum += d2_of(gv[e], w3d, (m >> e) & 1u);
-            }
-            if (rows_mine && cols_mine) {
-                float4 gk[8];
-#pragma unroll
-                for (int e = 0; e < 8; e++) gk[e] = gv[8 * h + e];
-#pragma unroll
-                for (int j = 0; j < G::TC; j++) {
-                    const uint32_t m = (uint32_t)mw[c0 + 32 * (wc * G::TC + j) + r] >> (8 * h);
-                    float v[8];
-#pragma unroll
-                    for (int e = 0; e < 8; e++) v[e] = d2_of(gk[e], w3c[j], (m >> e) & 1u);
-                    split3(v, p.b0[j], p.b1[j], p.b2[j]);
-                }
-            }
-        } else if constexpr (MODE == 1) {
-            const float* rec = st + G::kRows * kBK;
-            const uint16_t* mw = reinterpret_cast<const uint16_t*>(rec);
-            const float* gv = rec + 128;
-            {
-                const uint32_t m = mw[dunit];
-#pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    const float4 x = *reinterpret_cast<const float4*>(gv + 4 * c);
-                    dsum += ((m >> (4 * c + 0)) & 1u) ? x.x : 0.0f;
-                    dsum += ((m >> (4 * c + 1)) & 1u) ? x.y : 0.0f;
-                    dsum += ((m >> (4 * c + 2)) & 1u) ? x.z : 0.0f;
-                    dsum += ((m >> (4 * c + 3)) & 1u) ? x.w : 0.0f;
-                }
-            }
-            if (rows_mine && cols_mine) {
-#pragma unroll
-                for (int j = 0; j < G::TC; j++) {
-                    const uint32_t m = (uint32_t)mw[c0 + 32 * (wc * G::TC + j) + r] >> (8 * h);
-                    u32x4 q;
-#pragma unroll
-                    for (int e = 0; e < 4; e++)
-                        q[e] = (((m >> (2 * e)) & 1u) * 0x3F80u) | (((m >> (2 * e + 1)) & 1u) * 0x3F800000u);
-                    p.b0[j] = __builtin_bit_cast(bf16x8, q);
-                }
-            }
-        } else {
-            const float* rowp = st + drow * kBK;
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const float4 x = *reinterpret_cast<const float4*>(rowp + 4 * c);
-                dsum += x.x;
-                dsum += x.y;
-                dsum += x.z;
-                dsum += x.w;
-            }
-            if (rows_mine && cols_mine) {
-#pragma unroll
-                for (int j = 0; j < G::TC; j++) {
-                    float v[8];
-                    read_frag(st, G::H1 + 32 * (wc * G::TC + j) + r, h, v);
-                    split3(v, p.b0[j], p.b1[j], p.b2[j]);
-                }
-            }
-        }
-    };
-    const auto mfma_row = [&](const Planes& p, int i) {
-        if (!(rows_mine && cols_mine)) return;
-#pragma unroll
-        for (int j = 0; j < G::TC; j++) {
-            floatx16 c = acc[i][j];
-            if constexpr (MODE == 1) {
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a2[i], p.b0[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a1[i], p.b0[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a0[i], p.b0[j], c, 0, 0, 0);
-            } else {
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a2[i], p.b0[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a1[i], p.b1[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a0[i], p.b2[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a1[i], p.b0[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a0[i], p.b1[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p.a0[i], p.b0[j], c, 0, 0, 0);
-            }
-            acc[i][j] = c;
-        }
-    };
-
     // one loop step: refill the slot of stage it + 1 + kAhead (past the end: stage iters - 1 again into a slot
     // nobody reads, so the wait count stays uniform), wait for stage it + 1, then split it into `nxt` while the
     // MFMAs of stage it (`cur`) run; the interleave is pinned (1 MFMA, then up to 4 VALU) since hipcc otherwise
@@ -462,39 +343,7 @@ __global__ void __launch_bounds__(dw2_threads(NT2), 1) dw2_kernel(Dw2Args a) {
         }
     };
 
-    if constexpr (G::WIDE && G2048_DW2_WIDEPIPE) {
-        // (A/B build G2048_DW2_WIDEPIPE=1) two waves per SIMD and one register set of planes, pipelined by tile: in
-        // step it the MFMAs of stage it run row tile by row tile, and as each A tile's MFMAs are issued its
-        // registers are refilled with stage it + 1's split (then the B tiles).  Measured 3-5 % slower than the
-        // stage-by-stage loop below (profiles/round4/r4c16/dw2_ab.log), configs[2] update equal.
-        Planes pa;
-        if (iters > 0) {
-#pragma unroll
-            for (int q = 0; q <= kAhead; q++) issue_to(q, q < iters ? q : iters - 1);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kAhead * G::kGldsPerWave) : "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            load_b(S, pa);
-#pragma unroll
-            for (int i = 0; i < G::TR; i++) load_a(S, pa, i);
-            for (int it = 0; it < iters; it++) {
-                const bool nxt = it + 1 < iters;            // uniform
-                const int q = it + 1 + kAhead;
-                issue_to(q % kStages, q < iters ? q : iters - 1);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kAhead * G::kGldsPerWave) : "memory");
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-                const float* st = S + ((it + 1) % kStages) * G::kStageFloats;
-#pragma unroll
-                for (int i = 0; i < G::TR; i++) {
-                    mfma_row(pa, i);
-                    if (nxt) load_a(st, pa, i);
-                }
-                if (nxt) load_b(st, pa);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    } else if constexpr (G::WIDE) {
+    if constexpr (G::WIDE) {
         // two waves per SIMD, one register set of planes (a second set does not fit 256 registers): each step waits
         // for stage it, splits it and runs its MFMAs; the SIMD's other wave fills the gaps
         Planes pa;

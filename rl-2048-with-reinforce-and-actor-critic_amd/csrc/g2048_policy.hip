@@ -1494,15 +1494,6 @@ __global__ void __launch_bounds__(kPolBlock, 2) grad_coop_kernel(GradArgs a) {
     }
 }
 
-// G2048_GRAD_COOP=0 in the environment selects grad_kernel for 256 x 256 nets too (tools/ A/B only)
-bool grad_coop_enabled() {
-    static const int v = [] {
-        const char* e = std::getenv("G2048_GRAD_COOP");
-        return e ? std::atoi(e) : 1;
-    }();
-    return v != 0;
-}
-
 template <int ACT, int OBS, int FAC>
 void launch_coop(const GradArgs& a, int grid, hipStream_t s) {
     constexpr int kBytes = CoopLds<8, 8>::kBytes;
@@ -1532,16 +1523,13 @@ void launch_coop_obs(const GradArgs& a, int obs, int grid, hipStream_t s) {
 // with two rows per workgroup, the same row count
 template <int NT1, int NT2>
 void launch_grad(const GradArgs& a, int act, int obs, int grid, hipStream_t s) {
-    if constexpr (NT1 == 8 && NT2 == 8) {
-        if (grad_coop_enabled()) {
-            if (act == G2048_ACT_RELU && a.d2_form == 1) launch_coop_obs<0, 1>(a, obs, 2 * grid, s);
-            else if (act == G2048_ACT_RELU && a.d2_form == 2) launch_coop_obs<0, 2>(a, obs, 2 * grid, s);
-            else if (act == G2048_ACT_RELU) launch_coop_obs<0, 0>(a, obs, 2 * grid, s);
-            else launch_coop_obs<1, 0>(a, obs, 2 * grid, s);
-            return;
-        }
-    }
-    if (act == G2048_ACT_RELU && a.d2_form == 1) {
+    if constexpr (NT1 == 8 && NT2 == 8) {   // 256 x 256: the cooperative kernel (round 4: 0.78 of the fp32 MFMA peak
+                                            // against grad_kernel's 0.68, profiles/round4/r4c6/)
+        if (act == G2048_ACT_RELU && a.d2_form == 1) launch_coop_obs<0, 1>(a, obs, 2 * grid, s);
+        else if (act == G2048_ACT_RELU && a.d2_form == 2) launch_coop_obs<0, 2>(a, obs, 2 * grid, s);
+        else if (act == G2048_ACT_RELU) launch_coop_obs<0, 0>(a, obs, 2 * grid, s);
+        else launch_coop_obs<1, 0>(a, obs, 2 * grid, s);
+    } else if (act == G2048_ACT_RELU && a.d2_form == 1) {
         if (obs == G2048_OBS_LOG2) hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_LOG2, 1>), dim3(grid), dim3(kPolBlock), 0, s, a);
         else hipLaunchKernelGGL((grad_kernel<NT1, NT2, 0, G2048_OBS_RAW, 1>), dim3(grid), dim3(kPolBlock), 0, s, a);
     } else if (act == G2048_ACT_RELU && a.d2_form == 2) {

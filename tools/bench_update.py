@@ -28,8 +28,8 @@ def main():
     ap.add_argument("--lib", default=None, help="another build of libg2048 (A/B scripts)")
     ap.add_argument("--repo", default=None, help="import rl2048_amd from this checkout")
     ap.add_argument("--deep-grad", action="store_true",
-                    help="the two-layer net through g2048_deep_grad (use_two_layer_grad = False; a --lib build with "
-                         "G2048_DEEP_LOG2_64=1 covers log2 [256, 256])")
+                    help="the two-layer net through g2048_deep_grad (use_two_layer_grad = False; log2 [256, 256] is "
+                         "past its one-launch budget, so this is the multi-launch form)")
     ap.add_argument("--no-actor-records", action="store_true",
                     help="actor d2 as columns + g2048_dw2 instead of d2_form 2 records + g2048_dw2_actor (A/B)")
     args = ap.parse_args()

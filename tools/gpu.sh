@@ -18,6 +18,7 @@
 #                       FETCH_SIZE, WRITE_SIZE, TCC hit / miss -- one counter group per run; tools/pmc_grad_summary.py
 #   pmc_configs2        the same passes over one configs[2] update (tools/bench_update.py, 1,048,576 episodes)
 #   abref:LIB[:N]       N (default 2) interleaved runner-config iterations: the shipped library, then LIB
+#   abstep:LIB[:N[:ARGS]] N interleaved rounds of bench.py's step leg alone, shipped then LIB (ARGS: e.g. --rng philox --obs onehot)
 #   cmd:'...'           any other command (its own timeout inside)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -134,6 +135,28 @@ for step in "$@"; do
             G2048_LIB=$lib timeout -k 10 300 python3 tools/bench_refconfig.py --label "$(basename "$lib")" > "$O/ab_var_$r.log" 2>&1 || exit 1
         done
         grep -h '^{' "$O"/ab_*.log | cut -c1-220
+        ;;
+    abstep)
+        # abstep:LIB[:N[:BENCH ARGS]] -- N interleaved rounds of the step leg alone (200 launches), shipped then LIB
+        lib=${arg%%:*}
+        rest=""
+        [[ "$arg" == *:* ]] && rest=${arg#*:}
+        n=${rest%%:*}
+        n=${n:-3}
+        extra=""
+        [[ "$rest" == *:* ]] && extra=${rest#*:}
+        tag=abstep$SECONDS
+        for r in $(seq "$n"); do
+            # shellcheck disable=SC2086
+            timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-policy --no-train --no-configs4 --traffic off \
+                --steps 200 --warmup 20 $extra > "$O/${tag}_shipped_$r.log" 2>&1 || exit 1
+            # shellcheck disable=SC2086
+            timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-policy --no-train --no-configs4 --traffic off \
+                --steps 200 --warmup 20 $extra --lib "$lib" > "$O/${tag}_var_$r.log" 2>&1 || exit 1
+        done
+        for f in "$O"/"$tag"_*.log; do
+            python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[1].split('/')[-1], round(d['roofline']['kernel_ms']*1e3, 2), 'us', round(d['roofline']['frac'], 4))" "$f"
+        done
         ;;
     cmd)
         bash -o pipefail -c "$arg" || exit 1
