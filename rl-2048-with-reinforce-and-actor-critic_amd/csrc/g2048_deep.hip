@@ -1096,6 +1096,49 @@ constexpr int kDeepGradMaxBlock = 512;
 // delta_0 rows by 16-byte stores (a quarter of the store instructions): 1.2535-1.2542 s against 1.2499-1.2517 s
 // (profiles/round6/r7b/d0b128_*).
 
+#ifndef G2048_L0_FUSED
+#define G2048_L0_FUSED 0
+#endif
+// One unit tile t of a one-hot layer 0 for 32 boards (lane col: board b) by the exact bf16-plane MFMAs of
+// onehot_l0_mfma_kernel (same bits), W1's plane fragments streamed from the packed net one cell ahead, the bias
+// loaded after the chain; writes act((hi + lo) + b1) to out[unit * stride + col].  The gradient kernel's fused
+// layer 0 (G2048_DEEP_L0_FUSED).
+template <int ACT>
+__device__ __forceinline__ void onehot_l0_tile(const float* __restrict__ P, const DeepNet& net, int t, uint64_t b,
+                                               float* out, int stride) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    int tq = (int)threadIdx.x;
+    asm volatile("" : "+v"(tq));   // lane ids derived here, not hoisted out of the caller's group loop
+    const int lane = tq & 63, h = lane >> 5, col = lane & 31;
+    const u32x4* ft = reinterpret_cast<const u32x4*>(P + net.wpl) + lane + (int64_t)t * (kOneHotPlaneFloats / 4);
+    u32x4 f[2][3];
+#pragma unroll
+    for (int pl = 0; pl < 3; pl++) f[0][pl] = ft[pl * 64];
+    floatx16 hi = {}, lo = {};
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        if (c + 1 < 16) {
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++) f[(c + 1) & 1][pl] = ft[((c + 1) * 3 + pl) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
+        u32x4 dv;
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++)
+            dv[jj] = (nib == (uint32_t)(8 * h + 2 * jj) ? 0x3F80u : 0u) | (nib == (uint32_t)(8 * h + 2 * jj + 1) ? 0x3F800000u : 0u);
+        const bf16x8 bvv = __builtin_bit_cast(bf16x8, dv);
+        hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][0]), bvv, hi, 0, 0, 0);
+        lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][1]), bvv, lo, 0, 0, 0);
+        lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][2]), bvv, lo, 0, 0, 0);
+    }
+    float bv[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) bv[i] = P[net.b[0] + 32 * t + tile_row(i, h)];
+#pragma unroll
+    for (int i = 0; i < 16; i++) out[(32 * t + tile_row(i, h)) * stride + col] = activate<ACT>((hi[i] + lo[i]) + bv[i]);
+}
+
 struct DeepGradVariant {
     int nw, tpw, ksplit, per_cu, passes;   // passes > 1: the dense dW tiles in ranges of nw x tpw, one launch each
 };
@@ -1162,6 +1205,21 @@ __device__ __forceinline__ float act_deriv(float a) {   // from the activation (
     else return a * (1.0f - a);
 }
 
+// threadIdx.x through an empty asm: every call is a new value to the compiler, so the per-lane LDS / global
+// addresses a phase derives from it are computed in that phase -- derived once from threadIdx.x, hipcc hoisted them
+// out of the group loop and kept them live across all of it, and the 4 x 10 instantiation spilled them to scratch
+// (whose reloads, vector-memory ops, then waited behind the in-order vmcnt of the phase's stores / LDS-DMA)
+__device__ __forceinline__ int fresh_tid() {
+    int t = (int)threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+#define DEEP_LANE_IDS                                                                    \
+    const int tid = fresh_tid(), lane = tid & 63, h = lane >> 5, col = lane & 31; \
+    (void)lane;                                                                          \
+    (void)h;                                                                             \
+    (void)col
+
 template <int OBS, int ACT, int NW, int TPW, int KSPLIT>
 __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs a) {
     constexpr int kBlock = 64 * NW;
@@ -1219,7 +1277,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     // would drain the DMA there), and the next group's first barrier retires it.  Its forward then only re-strides
     // the block from LDS (the load had been 10 % of the group).  Whole groups only; the launch's last, ragged group
     // reads its block in place.
-    constexpr bool kPrefetch = OBS == G2048_OBS_ONEHOT;
+    constexpr bool kPrefetch = OBS == G2048_OBS_ONEHOT && !G2048_L0_FUSED;
     const int H0a = 32 * net.nt[0];
     float* stage = dyn + a.aoff[0] + H0a * kActStride;   // [unit][32]: deep_grad_act_floats leaves room
     const auto whole = [&](uint32_t g) { return g < groups && a.n - g * 32u >= 32u; };
@@ -1237,45 +1295,52 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         if (whole(blockIdx.x)) prefetch(blockIdx.x);   // retired by the first group's first barrier
     }
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
-        const uint32_t j = gi * 32u + (uint32_t)(tid & 31);
-        const bool valid = j < a.n;
-        const uint32_t jc = valid ? j : a.n - 1u;
-        if (tid < 32) bds[tid] = valid ? a.boards[j] : 0ull;
-        // the sample's coefficient / action / target, loaded now so that the forward covers their latency
-        const float cf = (tid < 32 && valid) ? a.coef[jc] : 0.0f;
-        const uint32_t act_j = (tid < 32 && !a.critic) ? a.actions[jc] : 0u;
-        // the critic's target, or (TD rows) its reward / has-next / lane now and V(s') once layer 0 is done (the
-        // lane index has arrived by then: no dependent load in front of the first barrier)
-        float tg = 0.0f, td_r = 0.0f, td_h = 0.0f, td_v = 0.0f;
-        int64_t td_l = 0;
-        if (tid < 32 && a.critic) {
-            if (a.has_td) {
-                td_l = a.td.lane[jc];
-                td_r = a.td.reward[jc];
-                td_h = a.td.has_next[jc];
-            } else {
-                tg = a.target[jc];
+        float td_v = 0.0f;   // V(s') of the critic's TD row (loaded after layer 0, used at the logits)
+        {
+            DEEP_LANE_IDS;
+            const uint32_t j = gi * 32u + (uint32_t)(tid & 31);
+            const bool valid = j < a.n;
+            const uint32_t jc = valid ? j : a.n - 1u;
+            if (tid < 32) bds[tid] = valid ? a.boards[j] : 0ull;
+            // the sample's coefficient / action / target, loaded now so that the forward covers their latency
+            const float cf = (tid < 32 && valid) ? a.coef[jc] : 0.0f;
+            const uint32_t act_j = (tid < 32 && !a.critic) ? a.actions[jc] : 0u;
+            // the critic's target, or (TD rows) its reward / has-next / lane now and V(s') once layer 0 is done (the
+            // lane index has arrived by then: no dependent load in front of the first barrier)
+            float tg = 0.0f, td_r = 0.0f, td_h = 0.0f;
+            int64_t td_l = 0;
+            if (tid < 32 && a.critic) {
+                if (a.has_td) {
+                    td_l = a.td.lane[jc];
+                    td_r = a.td.reward[jc];
+                    td_h = a.td.has_next[jc];
+                } else {
+                    tg = a.target[jc];
+                }
             }
-        }
-        __syncthreads();   // (a fence: vmcnt(0) -- the loads above have arrived)
-        if (tid < 32) {   // read back at the logits: their registers are free until then
-            smp_in[tid] = cf;
-            smp_in[32 + tid] = __uint_as_float(act_j);
-            smp_in[64 + tid] = tg;
-            smp_in[96 + tid] = td_r;
-            smp_in[128 + tid] = td_h;
-            smp_in[160 + tid] = __uint_as_float((uint32_t)td_l);
-            smp_in[192 + tid] = __uint_as_float((uint32_t)((uint64_t)td_l >> 32));
+            __syncthreads();   // (a fence: vmcnt(0) -- the loads above have arrived)
+            if (tid < 32) {   // read back at the logits: their registers are free until then
+                smp_in[tid] = cf;
+                smp_in[32 + tid] = __uint_as_float(act_j);
+                smp_in[64 + tid] = tg;
+                smp_in[96 + tid] = td_r;
+                smp_in[128 + tid] = td_h;
+                smp_in[160 + tid] = __uint_as_float((uint32_t)td_l);
+                smp_in[192 + tid] = __uint_as_float((uint32_t)((uint64_t)td_l >> 32));
+            }
         }
         DEEP_STAMP(0);
         // ---- forward: layer 0
         {
+            DEEP_LANE_IDS;
             float* out = actl(0);
             const int nt0 = net.nt[0];
             if constexpr (OBS == G2048_OBS_ONEHOT) {
                 // the group's block from onehot_l0_mfma_kernel (in d0_out: this workgroup overwrites the same rows
                 // with the group's layer-0 deltas at its end)
-                if (whole(gi)) {   // the staged block (its DMA retired by the barrier above)
+                if constexpr (G2048_L0_FUSED) {
+                    for (int t = w; t < nt0; t += NW) onehot_l0_tile<ACT>(P, net, t, bds[col], out, kActStride);
+                } else if (whole(gi)) {   // the staged block (its DMA retired by the barrier above)
                     const float4* st4 = reinterpret_cast<const float4*>(stage);
 #pragma unroll 4
                     for (int e4 = tid; e4 < 8 * H0a; e4 += kBlock) {
@@ -1311,13 +1376,17 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         }
         lds_barrier();
         DEEP_STAMP(1);
-        if (tid < 32 && a.critic && a.has_td) {
-            const int64_t tl = (int64_t)((uint64_t)__float_as_uint(smp_in[160 + tid]) |
-                                         ((uint64_t)__float_as_uint(smp_in[192 + tid]) << 32));
-            td_v = a.td.v_next[tl];
+        {
+            DEEP_LANE_IDS;
+            if (tid < 32 && a.critic && a.has_td) {
+                const int64_t tl = (int64_t)((uint64_t)__float_as_uint(smp_in[160 + tid]) |
+                                             ((uint64_t)__float_as_uint(smp_in[192 + tid]) << 32));
+                td_v = a.td.v_next[tl];
+            }
         }
         // ---- forward: dense layers (each into its own region)
         for (int l = 1; l < L; l++) {
+            DEEP_LANE_IDS;
             const float* in = actl(l - 1);
             float* out = actl(l);
             const int ntin = net.nt[l - 1], ntout = net.nt[l];
@@ -1338,105 +1407,120 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             lds_barrier();
         }
         DEEP_STAMP(2);
-        // ---- output layer partials (as deep_forward; threads 0..255)
-        if (tid < 256) {
-            const float* in = actl(L - 1);
-            const int pp = tid >> 5, bb = tid & 31, per = HL >> 3;
-            float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-            for (int u = pp * per; u < (pp + 1) * per; u++) {
-                const float x = in[u * kActStride + bb];
-                const float4 wv = wout[u];
-                s0 = fmaf(x, wv.x, s0);
-                s1 = fmaf(x, wv.y, s1);
-                s2 = fmaf(x, wv.z, s2);
-                s3 = fmaf(x, wv.w, s3);
+        // ---- output layer partials (as deep_forward; threads 0..255).  (Round 6: the same sums from the last dense
+        //      layer's epilogue registers, the chain handed across the lane halves -- same bits, no pass and barrier
+        //      here -- measured 0.4 % slower: the epilogue lengthens the 2-tile layer's waves while the pass here
+        //      uses all four; profiles/round6/r7c/, r7d/)
+        {
+            DEEP_LANE_IDS;
+            if (tid < 256) {
+                const float* in = actl(L - 1);
+                const int pp = tid >> 5, bb = tid & 31, per = HL >> 3;
+                float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+                for (int u = pp * per; u < (pp + 1) * per; u++) {
+                    const float x = in[u * kActStride + bb];
+                    const float4 wv = wout[u];
+                    s0 = fmaf(x, wv.x, s0);
+                    s1 = fmaf(x, wv.y, s1);
+                    s2 = fmaf(x, wv.z, s2);
+                    s3 = fmaf(x, wv.w, s3);
+                }
+                part[pp][bb][0] = s0;
+                part[pp][bb][1] = s1;
+                part[pp][bb][2] = s2;
+                part[pp][bb][3] = s3;
             }
-            part[pp][bb][0] = s0;
-            part[pp][bb][1] = s1;
-            part[pp][bb][2] = s2;
-            part[pp][bb][3] = s3;
+            lds_barrier();
         }
-        lds_barrier();
         DEEP_STAMP(3);
         // ---- logits -> g (threads 0..31, one sample each)
-        if (tid < 32) {
-            const float cf_ = smp_in[tid];
-            const uint32_t act_j_ = __float_as_uint(smp_in[32 + tid]);
-            float tg_ = smp_in[64 + tid];
-            const float td_r_ = smp_in[96 + tid], td_h_ = smp_in[128 + tid];
-            float lg[4];
+        {
+            DEEP_LANE_IDS;
+                const uint32_t j = gi * 32u + (uint32_t)(tid & 31);
+                const bool valid = j < a.n;
+            if (tid < 32) {
+                const float cf_ = smp_in[tid];
+                const uint32_t act_j_ = __float_as_uint(smp_in[32 + tid]);
+                float tg_ = smp_in[64 + tid];
+                const float td_r_ = smp_in[96 + tid], td_h_ = smp_in[128 + tid];
+                float lg[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                float v = part[0][tid][k];
+                for (int k = 0; k < 4; k++) {
+                    float v = part[0][tid][k];
 #pragma unroll
-                for (int q = 1; q < 8; q++) v += part[q][tid][k];
-                lg[k] = v + bo[k];
-            }
-            float g[4];
-            if (!a.critic) {
-                // logits_to_probs (src/MLP.py:139-156) and the policy-gradient logits delta (:328-354)
-                const uint32_t mw = a.use_mask ? mask_word_of(bds[tid]) : 0x01010101u;
-                const uint32_t act = valid ? act_j_ : 0u;
-                float l4[4];
+                    for (int q = 1; q < 8; q++) v += part[q][tid][k];
+                    lg[k] = v + bo[k];
+                }
+                float g[4];
+                if (!a.critic) {
+                    // logits_to_probs (src/MLP.py:139-156) and the policy-gradient logits delta (:328-354)
+                    const uint32_t mw = a.use_mask ? mask_word_of(bds[tid]) : 0x01010101u;
+                    const uint32_t act = valid ? act_j_ : 0u;
+                    float l4[4];
 #pragma unroll
-                for (int k = 0; k < 4; k++) l4[k] = ((mw >> (8 * k)) & 0xFFu) ? lg[k] : -1e9f;
-                const float mx = fmaxf(fmaxf(l4[0], l4[1]), fmaxf(l4[2], l4[3]));
-                float e[4];
+                    for (int k = 0; k < 4; k++) l4[k] = ((mw >> (8 * k)) & 0xFFu) ? lg[k] : -1e9f;
+                    const float mx = fmaxf(fmaxf(l4[0], l4[1]), fmaxf(l4[2], l4[3]));
+                    float e[4];
 #pragma unroll
-                for (int k = 0; k < 4; k++) e[k] = expf(l4[k] - mx);
-                const float es = ((e[0] + e[1]) + e[2]) + e[3];
+                    for (int k = 0; k < 4; k++) e[k] = expf(l4[k] - mx);
+                    const float es = ((e[0] + e[1]) + e[2]) + e[3];
 #pragma unroll
-                for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf_;
-            } else {
-                // the critic's value-loss gradient (update_batch :403-498, _get_grad_logits_critic :884-910)
-                if (a.has_td) tg_ = ((td_v * a.td.gamma) * td_h_) + td_r_;   // the host's fp32 operation order
-                const float diff = lg[0] - tg_;
-                const float gd = (a.huber && fabsf(diff) > a.huber_delta) ? copysignf(a.huber_delta, diff) : diff;
-                g[0] = gd * cf_;
-                g[1] = g[2] = g[3] = 0.0f;
-                if (valid && a.delta_out) a.delta_out[j] = tg_ - lg[0];
-                if (valid) {
-                    if (a.has_td) a.td.v_out[a.td.lane[j]] = lg[0];
-                    else if (a.v_out) a.v_out[j] = lg[0];
+                    for (int k = 0; k < 4; k++) g[k] = (((uint32_t)k == act ? 1.0f : 0.0f) - e[k] / es) * cf_;
+                } else {
+                    // the critic's value-loss gradient (update_batch :403-498, _get_grad_logits_critic :884-910)
+                    if (a.has_td) tg_ = ((td_v * a.td.gamma) * td_h_) + td_r_;   // the host's fp32 operation order
+                    const float diff = lg[0] - tg_;
+                    const float gd = (a.huber && fabsf(diff) > a.huber_delta) ? copysignf(a.huber_delta, diff) : diff;
+                    g[0] = gd * cf_;
+                    g[1] = g[2] = g[3] = 0.0f;
+                    if (valid && a.delta_out) a.delta_out[j] = tg_ - lg[0];
+                    if (valid) {
+                        if (a.has_td) a.td.v_out[a.td.lane[j]] = lg[0];
+                        else if (a.v_out) a.v_out[j] = lg[0];
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    gs[tid][k] = g[k];
+                    dbo_l[tid * 4 + k] += g[k];
                 }
             }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                gs[tid][k] = g[k];
-                dbo_l[tid * 4 + k] += g[k];
-            }
+            lds_barrier();
         }
-        lds_barrier();
         DEEP_STAMP(4);
-        // ---- output layer backward: dW_out, db_{L-1}, delta_{L-1} in place; thread (unit u, sample range q) of
-        //      oq ranges, so every thread works (one thread per unit ran 32 serial steps on one or two waves)
-        if (tid < oq * HL) {
-            const int u = tid % HL, q = tid / HL, n0 = q * oper, n1 = n0 + oper < 32 ? n0 + oper : 32;
-            float* arow = actl(L - 1) + u * kActStride;
-            const float4 wv = wout[u];
-            float d0 = dwo[0], d1 = dwo[1], d2 = dwo[2], d3 = dwo[3], db = dbl;
-            for (int n2 = n0; n2 < n1; n2++) {
-                const float x = arow[n2];
-                const float4 g4 = *reinterpret_cast<const float4*>(gs[n2]);
-                d0 = fmaf(x, g4.x, d0);
-                d1 = fmaf(x, g4.y, d1);
-                d2 = fmaf(x, g4.z, d2);
-                d3 = fmaf(x, g4.w, d3);
-                float dh = g4.x * wv.x;
-                dh = fmaf(g4.y, wv.y, dh);
-                dh = fmaf(g4.z, wv.z, dh);
-                dh = fmaf(g4.w, wv.w, dh);
-                const float dl = dh * act_deriv<ACT>(x);
-                db += dl;
-                arow[n2] = dl;
+        {
+            DEEP_LANE_IDS;
+            // ---- output layer backward: dW_out, db_{L-1}, delta_{L-1} in place; thread (unit u, sample range q) of
+            //      oq ranges, so every thread works (one thread per unit ran 32 serial steps on one or two waves)
+            if (tid < oq * HL) {
+                const int u = tid % HL, q = tid / HL, n0 = q * oper, n1 = n0 + oper < 32 ? n0 + oper : 32;
+                float* arow = actl(L - 1) + u * kActStride;
+                const float4 wv = wout[u];
+                float d0 = dwo[0], d1 = dwo[1], d2 = dwo[2], d3 = dwo[3], db = dbl;
+                for (int n2 = n0; n2 < n1; n2++) {
+                    const float x = arow[n2];
+                    const float4 g4 = *reinterpret_cast<const float4*>(gs[n2]);
+                    d0 = fmaf(x, g4.x, d0);
+                    d1 = fmaf(x, g4.y, d1);
+                    d2 = fmaf(x, g4.z, d2);
+                    d3 = fmaf(x, g4.w, d3);
+                    float dh = g4.x * wv.x;
+                    dh = fmaf(g4.y, wv.y, dh);
+                    dh = fmaf(g4.z, wv.z, dh);
+                    dh = fmaf(g4.w, wv.w, dh);
+                    const float dl = dh * act_deriv<ACT>(x);
+                    db += dl;
+                    arow[n2] = dl;
+                }
+                dwo[0] = d0; dwo[1] = d1; dwo[2] = d2; dwo[3] = d3;
+                dbl = db;
             }
-            dwo[0] = d0; dwo[1] = d1; dwo[2] = d2; dwo[3] = d3;
-            dbl = db;
+            lds_barrier();
         }
-        lds_barrier();
         DEEP_STAMP(5);
         // ---- dense layers top down: dW_l (MFMA over the 32 samples), then delta_{l-1} (MFMA chain) in place
         for (int l = L - 1; l >= 1; l--) {
+            DEEP_LANE_IDS;
             const float* A = actl(l - 1);
             const float* D = actl(l);
             const int ntin = net.nt[l - 1], ntout = net.nt[l];
@@ -1479,47 +1563,67 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             DEEP_STAMP(7);
         }
         // ---- first layer's weight gradient
-        if constexpr (kPrefetch) {
-            if (whole(gi + gridDim.x)) prefetch(gi + gridDim.x);   // the deeper layers' LDS is dead from here on
-        }
-        if constexpr (OBS == G2048_OBS_ONEHOT) {
-            // delta_0 out for the one-hot scatter (g2048_onehot_dw1): row j, unit tid (coalesced rows) -- by the last
-            // launch only (the earlier ones still read the layer-0 blocks these rows overwrite)
-            const int H0 = 32 * net.nt[0];
-            if (tid < H0 && a.last_pass) {
-                // through a buffer resource over the group's rows (base and row offsets in SGPRs, no 64-bit
-                // per-lane address to keep live; the rows past a ragged group's end fall outside num_records)
-                const float* drow = actl(0) + tid * kActStride;
-                const uint32_t left = a.n - gi * 32u < 32u ? a.n - gi * 32u : 32u;
-                const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-                    a.d0_out + (size_t)gi * 32u * (uint32_t)H0, 0, (int)(left * (uint32_t)H0 * 4u), 0x00020000);
-#pragma unroll
-                for (int n2 = 0; n2 < 32; n2++)
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(drow[n2]), rd, tid * 4, n2 * H0 * 4, 0);
+        {
+            DEEP_LANE_IDS;
+            if constexpr (kPrefetch) {
+                if (whole(gi + gridDim.x)) prefetch(gi + gridDim.x);   // the deeper layers' LDS is dead from here on
             }
-        } else {
-            // dW_0^T tile t (32 units x 32 features, features >= 16 zero): A = delta_0 [unit][sample], B = x [sample][feature]
-            const float* D0 = actl(0);
+            if constexpr (OBS == G2048_OBS_ONEHOT) {
+                // delta_0 out for the one-hot scatter (g2048_onehot_dw1): row j, unit tid (coalesced rows) -- by the last
+                // launch only (the earlier ones still read the layer-0 blocks these rows overwrite)
+                const int H0 = 32 * net.nt[0];
+                if (tid < H0 && a.last_pass) {
+                    // through a buffer resource over the group's rows (base and row offsets in SGPRs, no 64-bit
+                    // per-lane address to keep live; the rows past a ragged group's end fall outside num_records)
+                    const float* drow = actl(0) + tid * kActStride;
+                    const uint32_t left = a.n - gi * 32u < 32u ? a.n - gi * 32u : 32u;
+                    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                        a.d0_out + (size_t)gi * 32u * (uint32_t)H0, 0, (int)(left * (uint32_t)H0 * 4u), 0x00020000);
+                    // in batches of 8: the batch's LDS reads issued together, one wait, then its stores (hipcc otherwise
+                    // alternated one ds_read2 / one wait / two stores, 16 LDS round trips in series)
+                    // the row offset advances by one scalar add per store (as 32 distinct offsets hipcc hoisted them out of
+                    // the group loop and spilled them to VGPR lanes)
+                    const int rowb = __builtin_amdgcn_readfirstlane(H0 * 4);
+                    int so = 0;
 #pragma unroll
-            for (int i = 0; i < kA0; i++) {
-                const int t = w + NW * i;
-                if (t < net.nt[0]) {
-                    floatx16 c = acc0[i];
-                    const float* dp = D0 + (32 * t + col) * kActStride + h;
+                    for (int n0 = 0; n0 < 32; n0 += 8) {
+                        float v[8];
 #pragma unroll
-                    for (int s2 = 0; s2 < 16; s2++) {
-                        const float xv = col < 16 ? obs_value<OBS>(bds[2 * s2 + h], col, a.obs_scale) : 0.0f;
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(dp[2 * s2], xv, c, 0, 0, 0);
+                        for (int i = 0; i < 8; i++) v[i] = drow[n0 + i];
+                        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);   // the 4 ds_read2 first
+                        __builtin_amdgcn_sched_group_barrier(0x040, 8, 0);   // then the 8 stores
+#pragma unroll
+                        for (int i = 0; i < 8; i++) {
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), rd, tid * 4, so, 0);
+                            so += rowb;
+                            asm volatile("" : "+s"(so));   // one running offset, not 32 hoisted constants
+                        }
                     }
-                    acc0[i] = c;
+                }
+            } else {
+                // dW_0^T tile t (32 units x 32 features, features >= 16 zero): A = delta_0 [unit][sample], B = x [sample][feature]
+                const float* D0 = actl(0);
+#pragma unroll
+                for (int i = 0; i < kA0; i++) {
+                    const int t = w + NW * i;
+                    if (t < net.nt[0]) {
+                        floatx16 c = acc0[i];
+                        const float* dp = D0 + (32 * t + col) * kActStride + h;
+#pragma unroll
+                        for (int s2 = 0; s2 < 16; s2++) {
+                            const float xv = col < 16 ? obs_value<OBS>(bds[2 * s2 + h], col, a.obs_scale) : 0.0f;
+                            c = __builtin_amdgcn_mfma_f32_32x32x2f32(dp[2 * s2], xv, c, 0, 0, 0);
+                        }
+                        acc0[i] = c;
+                    }
                 }
             }
-        }
-        // the next group rewrites the boards and layer 0: every LDS access done (raw: keeps the DMA in flight)
-        if constexpr (kPrefetch) {
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        } else {
-            lds_barrier();
+            // the next group rewrites the boards and layer 0: every LDS access done (raw: keeps the DMA in flight)
+            if constexpr (kPrefetch) {
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            } else {
+                lds_barrier();
+            }
         }
         DEEP_STAMP(8);
 #if G2048_DEEP_DIAG
@@ -1669,7 +1773,7 @@ int64_t deep_grad_act_floats(const DeepNet& n, int nw) {
     int64_t f = units * kActStride;
     const int64_t red = 5 * 64 * nw;
     if (red > f) f = red;
-    if (n.onehot) {
+    if (n.onehot && !G2048_L0_FUSED) {
         const int64_t st = 32 * n.nt[0] * (kActStride + 32);
         if (st > f) f = st;
     }
@@ -2400,7 +2504,7 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
     const int64_t lds = deep_grad_lds_bytes(net, v.nw);
     hipStream_t s = (hipStream_t)stream;
     const int grid = (int)nparts;   // every workgroup writes its slab (zeros when it gets no group)
-    if (obs_mode == G2048_OBS_ONEHOT && n > 0) {   // layer 0 on the bf16 MFMA, into d0_out
+    if (obs_mode == G2048_OBS_ONEHOT && n > 0 && !G2048_L0_FUSED) {   // layer 0 on the bf16 MFMA, into d0_out
         const int rc = launch_onehot_l0(net, packed, boards, (uint32_t)n, activation, d0_out, s);
         if (rc) return rc;
     }

@@ -18,6 +18,7 @@
 #                       FETCH_SIZE, WRITE_SIZE, TCC hit / miss -- one counter group per run; tools/pmc_grad_summary.py
 #   pmc_configs2        the same passes over one configs[2] update (tools/bench_update.py, 1,048,576 episodes)
 #   abref:LIB[:N]       N (default 2) interleaved runner-config iterations: the shipped library, then LIB
+#   abmulti:L1,L2,..[:N] N interleaved runner-config rounds: shipped, then each library
 #   abstep:LIB[:N[:ARGS]] N interleaved rounds of bench.py's step leg alone, shipped then LIB (ARGS: e.g. --rng philox --obs onehot)
 #   cmd:'...'           any other command (its own timeout inside)
 set -o pipefail
@@ -130,11 +131,32 @@ for step in "$@"; do
         lib=${arg%%:*}
         n=2
         [[ "$arg" == *:* ]] && n=${arg#*:}
+        tag=ab$SECONDS
         for r in $(seq "$n"); do
-            timeout -k 10 300 python3 tools/bench_refconfig.py --label shipped > "$O/ab_shipped_$r.log" 2>&1 || exit 1
-            G2048_LIB=$lib timeout -k 10 300 python3 tools/bench_refconfig.py --label "$(basename "$lib")" > "$O/ab_var_$r.log" 2>&1 || exit 1
+            timeout -k 10 300 python3 tools/bench_refconfig.py --label shipped > "$O/${tag}_shipped_$r.log" 2>&1 || exit 1
+            G2048_LIB=$lib timeout -k 10 300 python3 tools/bench_refconfig.py --label "$(basename "$lib")" > "$O/${tag}_var_$r.log" 2>&1 || exit 1
         done
-        grep -h '^{' "$O"/ab_*.log | cut -c1-220
+        grep -h '^{' "$O"/"$tag"_*.log | cut -c1-220
+        ;;
+    abmulti)
+        # abmulti:LIB1,LIB2,...[:N] -- N interleaved rounds of the runner config: the shipped library, then each LIB
+        libs=${arg%%:*}
+        n=2
+        [[ "$arg" == *:* ]] && n=${arg#*:}
+        tag=abm$SECONDS
+        for r in $(seq "$n"); do
+            timeout -k 10 300 python3 tools/bench_refconfig.py --label shipped > "$O/${tag}_shipped_$r.log" 2>&1 || exit 1
+            for lib in ${libs//,/ }; do
+                G2048_LIB=$lib timeout -k 10 300 python3 tools/bench_refconfig.py --label "$(basename "$lib")" \
+                    > "$O/${tag}_$(basename "$lib" .so)_$r.log" 2>&1 || exit 1
+            done
+        done
+        grep -h '^{' "$O"/"$tag"_*.log | python3 -c "
+import json, sys
+for l in sys.stdin:
+    d = json.loads(l)
+    if d['episodes'] > 100000:
+        print(f\"{d['label'][:24]:24s} rep {d['rep']} update {d['update_s']:.4f} rollout {d['rollout_s']:.4f}\")"
         ;;
     abstep)
         # abstep:LIB[:N[:BENCH ARGS]] -- N interleaved rounds of the step leg alone (200 launches), shipped then LIB
