@@ -137,7 +137,7 @@ struct DeepPackArgs {
 __global__ void __launch_bounds__(256) deep_pack_kernel(DeepPackArgs a) {
     const DeepNet& n = a.net;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n.total; q += (int64_t)gridDim.x * blockDim.x) {
-        if (n.onehot && q >= n.wpl) {   // W1 plane fragment dword: the same split as onehot_l0_mfma_kernel's
+        if (n.onehot && q >= n.wpl) {   // W1 plane fragment dword (split3_bf16: w = p0 + p1 + p2 exactly)
             const int64_t x = q - n.wpl;
             const int d = (int)(x & 3), lane = (int)((x >> 2) & 63);
             const int64_t r = x >> 8;
@@ -324,8 +324,8 @@ __device__ __forceinline__ void dense_fwd_split(const float* in, float* out, con
 // workgroup calls it; it ends with a barrier.
 
 // Entry 2 e + hh of the one-hot B-operand table: exponent e as 8 bf16 (1.0 at k = e, else 0) for the lane half hh
-// (k = 8 hh .. 8 hh + 7).  Looked up per cell from LDS by the layer-0 kernels: built by compares and selects it was
-// ~21 VALU per cell and operand, which made onehot_l0_mfma_kernel VALU-bound.
+// (k = 8 hh .. 8 hh + 7).  Looked up per cell from LDS by the 64-slot rollout's layer 0: built by compares and
+// selects it was ~21 VALU per cell and operand (round 5, the then layer-0 kernel of the update was VALU-bound).
 __device__ __forceinline__ uint4 onehot_entry(uint32_t idx) {
     const uint32_t e = idx >> 1, hh = idx & 1;
     uint32_t d[4];
@@ -335,141 +335,6 @@ __device__ __forceinline__ uint4 onehot_entry(uint32_t idx) {
     return make_uint4(d[0], d[1], d[2], d[3]);
 }
 
-// One-hot first layer on the bf16 MFMA for the update (round 5): a0[u][s] = act(sum_c W1[17 c + e_c(s)][u] + b1[u])
-// per 32-sample group, written as a group block [unit][left] (left = the group's valid samples, 32 but for the last
-// group) -- the layout g2048_deep_grad reads back into its LDS activations (in the d0_out buffer, whose rows the
-// same workgroup later overwrites with the group's layer-0 deltas).  x W1 of a one-hot x is a GEMM whose B operand
-// (one-hot: cell c's 16 exponents as one k-step of v_mfma_f32_32x32x16_bf16, k = 8 h .. 8 h + 7 per lane half) is
-// exact in bf16; W1 is split exactly into three bf16 planes (w = hi + mid + lo), so every product is exact: each
-// MFMA adds exactly one nonzero term per output (the cell's exponent), hi terms into one accumulator and mid + lo
-// into another (their sum as accurate as the gather's 16-term fp32 sum).  Wave w owns unit tile w for the whole
-// launch: its hi / mid plane fragments (16 cells, from the packed net's plane section) in registers (128 VGPRs), the
-// lo plane in LDS (re-read per cell), the one-hot B operands from a 512-byte LDS table; 48 MFMAs per wave per group.
-// A group's results are stored at the top of the next group's iteration (buffer stores, no branch), so the wait for
-// a board never drains the previous group's stores.  Per 32-sample group and CU: 3,072 MFMA cycles per SIMD, 32 KiB
-// written.
-constexpr int kL0Waves = 8;
-template <int ACT>
-__global__ void __launch_bounds__(64 * kL0Waves, 1) onehot_l0_mfma_kernel(DeepNet net, const float* __restrict__ P,
-                                                                          const uint64_t* __restrict__ boards,
-                                                                          uint32_t n, float* __restrict__ out) {
-    __shared__ float bias[256];
-    __shared__ bf16x8 wlo[kL0Waves][16][64];   // the lo plane (wave, cell, lane): 128 KiB, read once per cell
-    __shared__ uint4 ohtab[32];                 // [2 exponent + lane half]: the one-hot B operand (k = 8 h .. 8 h + 7)
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, col = lane & 31;
-    const int nt0 = net.nt[0], H = 32 * nt0;
-    for (int u = threadIdx.x; u < H; u += blockDim.x) bias[u] = P[net.b[0] + u];
-    if (threadIdx.x < 32) ohtab[threadIdx.x] = onehot_entry(threadIdx.x);
-    __syncthreads();
-    if (w >= nt0) return;   // wave-uniform; no barrier below (each wave reads only its own wlo rows)
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    bf16x8 wp[16][2];   // hi, mid planes in registers (128 VGPRs)
-    {   // the packed net's plane section (g2048_deep_pack: the same split3_bf16 of W1), coalesced 16-byte loads --
-        // splitting W1 here took 128 strided loads per lane at every launch
-        const u32x4* ft = reinterpret_cast<const u32x4*>(P + net.wpl) + lane + (int64_t)w * (kOneHotPlaneFloats / 4);
-#pragma unroll
-        for (int c = 0; c < 16; c++) {
-            wp[c][0] = __builtin_bit_cast(bf16x8, ft[(c * 3 + 0) * 64]);
-            wp[c][1] = __builtin_bit_cast(bf16x8, ft[(c * 3 + 1) * 64]);
-            wlo[w][c][lane] = __builtin_bit_cast(bf16x8, ft[(c * 3 + 2) * 64]);
-        }
-    }
-    const uint32_t groups = (n + 31u) >> 5;
-    const auto board_of = [&](uint32_t g) {   // lane col's board of group g (clamped: always a valid address)
-        const uint32_t j = g * 32u + (uint32_t)col;
-        return boards[j < n ? j : n - 1u];
-    };
-    // Software-pipelined by one group: group g's 16 results are stored at the top of the next group's iteration,
-    // before that group's board prefetch and MFMAs.  vmcnt counts stores and loads in one queue, and the wait-count
-    // pass makes a store's data registers wait for the store before they are rewritten: stored at the end of their
-    // own iteration (round 5 as first shipped), the next group's first VALU waited for the previous group's stores
-    // (vmcnt(1) at the loop top, the HBM write latency once per group); now the results are rewritten a whole
-    // MFMA phase after their stores issue, and the board a group needs was loaded before the stores ahead of it.
-    floatx16 hi, lo;
-    const auto layer0 = [&](const uint64_t b) {
-        hi = floatx16{};
-        lo = floatx16{};
-        asm volatile("" ::: "memory");   // wlo is re-read per group: hoisted out of the loop it would be 64 VGPRs
-        const auto onehot = [&](int c) {   // cell c's exponent as the B operand, from the LDS table
-            const uint32_t nib = (uint32_t)(b >> (4 * c)) & 15u;
-            return __builtin_bit_cast(bf16x8, ohtab[(nib << 1) | (uint32_t)h]);
-        };
-        // two cells ahead (B operand, lo-plane fragment: LDS reads), a scheduling barrier per cell: left free, the
-        // scheduler built all 16 B operands first and the kernel spilled; one cell ahead exposed the LDS latency
-        bf16x8 bv = onehot(0), lv = wlo[w][0][lane], bv1 = onehot(1), lv1 = wlo[w][1][lane];
-#pragma unroll
-        for (int c = 0; c < 16; c++) {
-            const bf16x8 bn = onehot(c < 14 ? c + 2 : 15), ln = wlo[w][c < 14 ? c + 2 : 15][lane];
-            hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][0], bv, hi, 0, 0, 0);
-            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[c][1], bv, lo, 0, 0, 0);
-            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lv, bv, lo, 0, 0, 0);
-            bv = bv1;
-            lv = lv1;
-            bv1 = bn;
-            lv1 = ln;
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    float res[16];
-    const auto finish = [&]() {
-#pragma unroll
-        for (int i = 0; i < 16; i++) res[i] = activate<ACT>((hi[i] + lo[i]) + bias[32 * w + tile_row(i, h)]);
-    };
-    const uint32_t wu = (uint32_t)__builtin_amdgcn_readfirstlane(w);   // the row offset is scalar (soffset)
-    // buffer stores, issued by every lane (a lane past `left` stores past num_records: dropped): no branch
-    const auto store = [&](uint32_t g) {
-        const uint32_t left = n - g * 32u < 32u ? n - g * 32u : 32u;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            out + (size_t)g * 32u * (uint32_t)H, 0, (int)(left * (uint32_t)H * 4u), 0x00020000);
-        const uint32_t cofs = (uint32_t)col < left ? ((uint32_t)col + 4u * (uint32_t)h * left) * 4u : 0x80000000u;
-#pragma unroll
-        for (int i = 0; i < 16; i++)
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(res[i]), rs, (int)cofs,
-                                                  (int)((32u * wu + (uint32_t)tile_row(i, 0)) * left * 4u), 0);
-    };
-    uint32_t gi = blockIdx.x;   // < groups: the grid is at most one workgroup per group
-    uint64_t bnext = board_of(gi + gridDim.x < groups ? gi + gridDim.x : gi);
-    layer0(board_of(gi));
-    finish();
-    // the prefetched board retired before the loop (no store is in flight yet; an empty asm reading it makes the
-    // pass wait here): merged with the back edge, where it is ready, its pending load made the pass wait vmcnt(1) at
-    // the loop top -- i.e. for the previous group's stores
-    asm volatile("" ::"v"(bnext));
-    for (gi += gridDim.x; gi < groups; gi += gridDim.x) {
-        const uint64_t b = bnext;
-        bnext = board_of(gi + gridDim.x < groups ? gi + gridDim.x : gi);   // the next group's, one group ahead
-        store(gi - gridDim.x);   // after the board load: waiting for that board leaves these 16 stores in flight
-        layer0(b);
-        finish();
-    }
-    store(gi - gridDim.x);
-}
-
-// layer 0 of a one-hot net from its onehot_l0_mfma_kernel block (group gi, [unit][left]) into LDS [unit][sample]
-// (stride kActStride); samples past the batch read as 0.  Every thread of the block (NT threads) calls it.
-template <int NT>
-__device__ __forceinline__ void load_l0_block(const float* __restrict__ a0, uint32_t n, uint32_t gi, int H, float* out) {
-    const float* blk = a0 + (size_t)gi * 32u * (uint32_t)H;
-    const uint32_t left = n - gi * 32u < 32u ? n - gi * 32u : 32u;
-    const int tid = threadIdx.x;
-    if (left == 32u) {
-        const float4* b4 = reinterpret_cast<const float4*>(blk);
-#pragma unroll 8
-        for (int e4 = tid; e4 < 8 * H; e4 += NT) {   // all of a thread's loads issued before the LDS writes
-            const float4 v = b4[e4];
-            float* o = out + (e4 >> 3) * kActStride + ((e4 & 7) << 2);
-            o[0] = v.x;
-            o[1] = v.y;
-            o[2] = v.z;
-            o[3] = v.w;
-        }
-    } else {
-        for (int e = tid; e < 32 * H; e += NT) {
-            const uint32_t u = (uint32_t)e >> 5, sm = (uint32_t)e & 31u;
-            out[u * kActStride + sm] = sm < left ? blk[u * left + sm] : 0.0f;
-        }
-    }
-}
 
 // Tools-only phase clock (-DG2048_DEEP_DIAG=1 builds; see deep_grad_kernel's DEEP_STAMP): deep_forward stamps its
 // layer phases into it when the caller passes one (the rollout kernel), an empty type in the product.
@@ -495,20 +360,17 @@ struct DiagClock {};
     } while (0)
 #endif
 
-// KSPLIT: the dense layers by dense_fwd_split (the gradient kernel's forward, for the pattern probe).  A0IN (one-hot,
-// the probe): layer 0 from onehot_l0_mfma_kernel's block of group gi (a0) -- the update's layer-0 bits.
-template <int OBS, int ACT, int KSPLIT = 0, bool A0IN = false>
+// KSPLIT: the dense layers by dense_fwd_split (the gradient kernel's forward, for the pattern probe).
+template <int OBS, int ACT, int KSPLIT = 0>
 __device__ void deep_forward(const DeepNet& net, const float* __restrict__ P, DeepSmem& S, float obs_scale,
-                             const float* a0 = nullptr, uint32_t n = 0, uint32_t gi = 0, DiagClock* dc = nullptr) {
+                             DiagClock* dc = nullptr) {
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31, w = threadIdx.x >> 6;
     // ---- first hidden layer -> S.act[0]
     {
         float* out = S.act[0];
         const int nt0 = net.nt[0];
-        if constexpr (A0IN) {
-            load_l0_block<kDeepBlock>(a0, n, gi, 32 * nt0, out);
-        } else if constexpr (OBS == G2048_OBS_ONEHOT) {
-            // the update's layer-0 arithmetic (onehot_l0_mfma_kernel), W1's plane fragments streamed from the
+        if constexpr (OBS == G2048_OBS_ONEHOT) {
+            // the one-hot layer-0 arithmetic of every kernel (onehot_l0_tile), W1's plane fragments streamed from the
             // packed net: wave w, unit tiles w, w + 4; per cell one exact one-hot B operand and 3 MFMAs (hi plane
             // into `hi`, the mid and lo planes into `lo`), cell by cell; act((hi + lo) + b1) -- the same bits in
             // rollout, policy, probe and update, and 32 x 16 x 3 fragments of 1 KiB per tile instead of 16 KiB of
@@ -824,10 +686,10 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_policy_kernel(DeepPolArgs 
 // are unused): out[j * ld + u] for u < 32 nt[layer] -- bit for bit what deep_grad_kernel computes (dense layers by
 // dense_fwd_split when the net's gradient instantiation splits k, else deep_forward's chain), for tests that impose
 // the gradient kernel's own activation pattern on an fp64 evaluation.
-template <int OBS, int ACT, int KSPLIT, bool A0IN>
+template <int OBS, int ACT, int KSPLIT>
 __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net, const float* packed,
                                                                      const uint64_t* boards, uint32_t n, float obs_scale,
-                                                                     float* out, uint32_t ld, const float* a0) {
+                                                                     float* out, uint32_t ld) {
     __shared__ DeepSmem S;
     const uint32_t groups = (n + 31u) >> 5;
     const int tid = threadIdx.x, layer = net.L - 1, H = 32 * net.nt[layer];
@@ -837,7 +699,7 @@ __global__ void __launch_bounds__(kDeepBlock, 2) deep_hidden_kernel(DeepNet net,
             S.board[tid] = boards[j < n ? j : n - 1u];
         }
         __syncthreads();
-        deep_forward<OBS, ACT, KSPLIT, A0IN>(net, packed, S, obs_scale, a0, n, gi);
+        deep_forward<OBS, ACT, KSPLIT>(net, packed, S, obs_scale);
         const float* act = S.act[layer & 1];
         for (int e = tid; e < 32 * H; e += kDeepBlock) {
             const int b = e / H, u = e % H;
@@ -1006,7 +868,7 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
             gp.s_lo = get64(18); gp.s_hi = get64(20); gp.i_lo = get64(22); gp.i_hi = get64(24);
             gp.has_uint32 = get(26); gp.uinteger = get(27);
         } else {
-            deep_forward<OBS, ACT>(a.net, a.packed, S, a.obs_scale, nullptr, 0, 0, dc);
+            deep_forward<OBS, ACT>(a.net, a.packed, S, a.obs_scale, dc);
         }
         if (owner && ep != kNoEpisode) {
             float lg[4];
@@ -1089,20 +951,17 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
 constexpr int kDeepGradMaxBlock = 512;
 // Tried, not kept (measured on the runner config; the A/B switches are gone from the source): the 4-wave
 // instantiation's 64-unit layer as a 4-way k split (no change); log2 / raw nets of 49..64 dense tiles on the 8 x 8
-// instantiation (spills ~300 VGPRs; the two-layer cooperative kernel runs them); the one-hot layer 0 computed in the
-// kernel from W1's packed planes instead of read back from onehot_l0_mfma_kernel's blocks -- its 0.126 s go, but the
-// group grows 105.7 k -> 118.3 k cycles (the plane stream is latency-bound beside 10 accumulator tiles): update
-// 1.278-1.281 s against 1.251 s (round 6, profiles/round6/r7a/l0fused_*; round 5: profiles/round5/r6b/); the
-// delta_0 rows by 16-byte stores (a quarter of the store instructions): 1.2535-1.2542 s against 1.2499-1.2517 s
-// (profiles/round6/r7b/d0b128_*).
+// instantiation (spills ~300 VGPRs; the two-layer cooperative kernel runs them); the delta_0 rows by 16-byte stores
+// (a quarter of the store instructions): 1.2535-1.2542 s against 1.2499-1.2517 s (profiles/round6/r7b/d0b128_*).
+// The one-hot layer 0 is computed here (onehot_l0_tile) since round 6: with the per-phase lane ids below the kernel
+// no longer spills, and the fused form measured equal to reading back a separate layer-0 kernel's 1 KiB / sample
+// blocks (1.2167-1.2200 s against 1.2167-1.2181 s, profiles/round6/r7f/; it had been 2 % slower while it spilled 30
+// VGPRs, r7a/l0fused_*), so that kernel and its 2 KiB / sample-pass of HBM traffic are gone.
 
-#ifndef G2048_L0_FUSED
-#define G2048_L0_FUSED 0
-#endif
-// One unit tile t of a one-hot layer 0 for 32 boards (lane col: board b) by the exact bf16-plane MFMAs of
-// onehot_l0_mfma_kernel (same bits), W1's plane fragments streamed from the packed net one cell ahead, the bias
-// loaded after the chain; writes act((hi + lo) + b1) to out[unit * stride + col].  The gradient kernel's fused
-// layer 0 (G2048_DEEP_L0_FUSED).
+// One unit tile t of a one-hot layer 0 for 32 boards (lane col: board b) by the exact bf16-plane MFMAs: per cell one
+// exact one-hot B operand, hi plane into `hi`, mid and lo planes into `lo` (deep_forward's arithmetic, the same
+// bits), W1's plane fragments streamed from the packed net one cell ahead, the bias loaded after the chain; writes
+// act((hi + lo) + b1) to out[unit * stride + col].  The gradient kernel's layer 0.
 template <int ACT>
 __device__ __forceinline__ void onehot_l0_tile(const float* __restrict__ P, const DeepNet& net, int t, uint64_t b,
                                                float* out, int stride) {
@@ -1270,30 +1129,6 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     uint64_t dph[kDiagSlots] = {};
     uint64_t dlast = __builtin_amdgcn_s_memtime();
 #endif
-    // one-hot: the layer-0 block of the workgroup's next group (onehot_l0_mfma_kernel's output, [unit][32], 32 KiB at
-    // H0 = 256) copied by LDS-DMA (global_load_lds_dwordx4: no registers -- the register form spilled) into a linear
-    // staging area over the dead deeper layers as soon as the current group's last delta chain is done, so its HBM
-    // latency runs under the delta_0 stores; the group's end barrier is a raw s_barrier (a __syncthreads() fence
-    // would drain the DMA there), and the next group's first barrier retires it.  Its forward then only re-strides
-    // the block from LDS (the load had been 10 % of the group).  Whole groups only; the launch's last, ragged group
-    // reads its block in place.
-    constexpr bool kPrefetch = OBS == G2048_OBS_ONEHOT && !G2048_L0_FUSED;
-    const int H0a = 32 * net.nt[0];
-    float* stage = dyn + a.aoff[0] + H0a * kActStride;   // [unit][32]: deep_grad_act_floats leaves room
-    const auto whole = [&](uint32_t g) { return g < groups && a.n - g * 32u >= 32u; };
-    const auto prefetch = [&](uint32_t g) {   // wave w, piece k: float4s [k kBlock + 64 w, + 64) of the block
-        typedef __attribute__((address_space(1))) void gvoid;
-        typedef __attribute__((address_space(3))) void lvoid;
-        const float4* b4 = reinterpret_cast<const float4*>(a.d0_out + (size_t)g * 32u * (uint32_t)H0a);
-        for (int k = 0; k * kBlock < 8 * H0a; k++) {
-            const int e0 = k * kBlock + 64 * w;
-            if (e0 < 8 * H0a)   // wave-uniform (8 H0 is a multiple of 256)
-                __builtin_amdgcn_global_load_lds((gvoid*)(b4 + e0 + lane), (lvoid*)(stage + 4 * e0), 16, 0, 0);
-        }
-    };
-    if constexpr (kPrefetch) {
-        if (whole(blockIdx.x)) prefetch(blockIdx.x);   // retired by the first group's first barrier
-    }
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
         float td_v = 0.0f;   // V(s') of the critic's TD row (loaded after layer 0, used at the logits)
         {
@@ -1336,24 +1171,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             float* out = actl(0);
             const int nt0 = net.nt[0];
             if constexpr (OBS == G2048_OBS_ONEHOT) {
-                // the group's block from onehot_l0_mfma_kernel (in d0_out: this workgroup overwrites the same rows
-                // with the group's layer-0 deltas at its end)
-                if constexpr (G2048_L0_FUSED) {
-                    for (int t = w; t < nt0; t += NW) onehot_l0_tile<ACT>(P, net, t, bds[col], out, kActStride);
-                } else if (whole(gi)) {   // the staged block (its DMA retired by the barrier above)
-                    const float4* st4 = reinterpret_cast<const float4*>(stage);
-#pragma unroll 4
-                    for (int e4 = tid; e4 < 8 * H0a; e4 += kBlock) {
-                        const float4 v = st4[e4];
-                        float* o = out + (e4 >> 3) * kActStride + ((e4 & 7) << 2);
-                        o[0] = v.x;
-                        o[1] = v.y;
-                        o[2] = v.z;
-                        o[3] = v.w;
-                    }
-                } else {
-                    load_l0_block<kBlock>(a.d0_out, a.n, gi, 32 * nt0, out);
-                }
+                for (int t = w; t < nt0; t += NW) onehot_l0_tile<ACT>(P, net, t, bds[col], out, kActStride);
             } else {
                 const uint64_t b = bds[col];
                 float x[8];
@@ -1417,6 +1235,23 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 const float* in = actl(L - 1);
                 const int pp = tid >> 5, bb = tid & 31, per = HL >> 3;
                 float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+                if (per == 8) {   // a 64-unit last layer: the slice's 8 reads in flight, then the same chain
+                    float x[8];
+                    float4 wv[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        x[i] = in[(8 * pp + i) * kActStride + bb];
+                        wv[i] = wout[8 * pp + i];
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        s0 = fmaf(x[i], wv[i].x, s0);
+                        s1 = fmaf(x[i], wv[i].y, s1);
+                        s2 = fmaf(x[i], wv[i].z, s2);
+                        s3 = fmaf(x[i], wv[i].w, s3);
+                    }
+                } else
                 for (int u = pp * per; u < (pp + 1) * per; u++) {
                     const float x = in[u * kActStride + bb];
                     const float4 wv = wout[u];
@@ -1497,6 +1332,34 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 float* arow = actl(L - 1) + u * kActStride;
                 const float4 wv = wout[u];
                 float d0 = dwo[0], d1 = dwo[1], d2 = dwo[2], d3 = dwo[3], db = dbl;
+                const auto step = [&](int n2, float x, float4 g4) {
+                    d0 = fmaf(x, g4.x, d0);
+                    d1 = fmaf(x, g4.y, d1);
+                    d2 = fmaf(x, g4.z, d2);
+                    d3 = fmaf(x, g4.w, d3);
+                    float dh = g4.x * wv.x;
+                    dh = fmaf(g4.y, wv.y, dh);
+                    dh = fmaf(g4.z, wv.z, dh);
+                    dh = fmaf(g4.w, wv.w, dh);
+                    const float dl = dh * act_deriv<ACT>(x);
+                    db += dl;
+                    arow[n2] = dl;
+                };
+                if (n1 - n0 == 8) {   // the runner net's 64-unit layer on 4 waves: 4 samples' reads in flight per wait
+#pragma unroll
+                    for (int b0 = 0; b0 < 8; b0 += 4) {
+                        float x[4];
+                        float4 g4[4];
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            x[i] = arow[n0 + b0 + i];
+                            g4[i] = *reinterpret_cast<const float4*>(gs[n0 + b0 + i]);
+                        }
+                        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+                        for (int i = 0; i < 4; i++) step(n0 + b0 + i, x[i], g4[i]);
+                    }
+                } else
                 for (int n2 = n0; n2 < n1; n2++) {
                     const float x = arow[n2];
                     const float4 g4 = *reinterpret_cast<const float4*>(gs[n2]);
@@ -1557,7 +1420,16 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             if (tid < 32 * ntin) {
                 const float* drow = Aw + tid * kActStride;
                 float db = dbs[(l - 1) * 256 + tid];
-                for (int n2 = 0; n2 < 32; n2++) db += drow[n2];
+                // 8 rows' reads in flight per wait (the same adds in the same order)
+#pragma unroll
+                for (int n0 = 0; n0 < 32; n0 += 8) {
+                    float v[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) v[i] = drow[n0 + i];
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) db += v[i];
+                }
                 dbs[(l - 1) * 256 + tid] = db;
             }
             DEEP_STAMP(7);
@@ -1565,12 +1437,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         // ---- first layer's weight gradient
         {
             DEEP_LANE_IDS;
-            if constexpr (kPrefetch) {
-                if (whole(gi + gridDim.x)) prefetch(gi + gridDim.x);   // the deeper layers' LDS is dead from here on
-            }
             if constexpr (OBS == G2048_OBS_ONEHOT) {
                 // delta_0 out for the one-hot scatter (g2048_onehot_dw1): row j, unit tid (coalesced rows) -- by the last
-                // launch only (the earlier ones still read the layer-0 blocks these rows overwrite)
+                // launch of a multi-launch net only (each launch recomputes the same rows)
                 const int H0 = 32 * net.nt[0];
                 if (tid < H0 && a.last_pass) {
                     // through a buffer resource over the group's rows (base and row offsets in SGPRs, no 64-bit
@@ -1580,9 +1449,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
                         a.d0_out + (size_t)gi * 32u * (uint32_t)H0, 0, (int)(left * (uint32_t)H0 * 4u), 0x00020000);
                     // in batches of 8: the batch's LDS reads issued together, one wait, then its stores (hipcc otherwise
-                    // alternated one ds_read2 / one wait / two stores, 16 LDS round trips in series)
-                    // the row offset advances by one scalar add per store (as 32 distinct offsets hipcc hoisted them out of
-                    // the group loop and spilled them to VGPR lanes)
+                    // alternated one ds_read2 / one wait / two stores, 16 LDS round trips in series); the row offset
+                    // advances by one scalar add per store (as 32 distinct offsets hipcc hoisted them out of the group
+                    // loop and spilled them to VGPR lanes)
                     const int rowb = __builtin_amdgcn_readfirstlane(H0 * 4);
                     int so = 0;
 #pragma unroll
@@ -1618,12 +1487,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     }
                 }
             }
-            // the next group rewrites the boards and layer 0: every LDS access done (raw: keeps the DMA in flight)
-            if constexpr (kPrefetch) {
-                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            } else {
-                lds_barrier();
-            }
+            lds_barrier();   // the next group rewrites the boards and layer 0: every LDS access done
         }
         DEEP_STAMP(8);
 #if G2048_DEEP_DIAG
@@ -1765,18 +1629,14 @@ DeepGradLayout deep_grad_layout(const DeepNet& n) {
     return g;
 }
 
-// floats of the output layer's final reduction (deep_grad_kernel: [oq][HL][5], oq HL <= the block size)
-// (one-hot: and the next group's layer-0 staging block [H0][32] right after layer 0's rows)
+// floats of the hidden layers' activations, at least the output layer's final reduction (deep_grad_kernel:
+// [oq][HL][5], oq HL <= the block size)
 int64_t deep_grad_act_floats(const DeepNet& n, int nw) {
     int64_t units = 0;
     for (int l = 0; l < n.L; l++) units += 32 * n.nt[l];
     int64_t f = units * kActStride;
     const int64_t red = 5 * 64 * nw;
     if (red > f) f = red;
-    if (n.onehot && !G2048_L0_FUSED) {
-        const int64_t st = 32 * n.nt[0] * (kActStride + 32);
-        if (st > f) f = st;
-    }
     return f;
 }
 int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, bias sums, output weights / bias
@@ -2117,16 +1977,6 @@ int launch_deep_roll(const DeepRollArgs& a, int grid, hipStream_t s) {
     return check_hip();
 }
 
-int launch_onehot_l0(const DeepNet& net, const float* packed, const uint64_t* boards, uint32_t n, int activation,
-                     float* out, hipStream_t s) {
-    const int64_t groups = ((int64_t)n + 31) / 32, cap = device_cus();
-    const int grid = (int)(groups < cap ? groups : cap);   // one 8-wave workgroup per CU, W1 resident in registers
-    if (activation == G2048_ACT_RELU)
-        hipLaunchKernelGGL(onehot_l0_mfma_kernel<0>, dim3(grid), dim3(64 * kL0Waves), 0, s, net, packed, boards, n, out);
-    else
-        hipLaunchKernelGGL(onehot_l0_mfma_kernel<1>, dim3(grid), dim3(64 * kL0Waves), 0, s, net, packed, boards, n, out);
-    return check_hip();
-}
 }  // namespace
 
 #if G2048_DEEP_DIAG
@@ -2305,37 +2155,29 @@ int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, 
     if (n == 0) return G2048_OK;
     const int ksplit = deep_grad_variant(net).ksplit;   // the full net's gradient instantiation's k-split rule
     hipStream_t s = (hipStream_t)stream;
-    float* a0 = nullptr;   // one-hot: the update's layer 0 (onehot_l0_mfma_kernel) in a scratch buffer
-    if (obs_mode == G2048_OBS_ONEHOT) {
-        if (hipMallocAsync(reinterpret_cast<void**>(&a0), (size_t)n * 32 * net.nt[0] * sizeof(float), s) != hipSuccess)
-            return dfail(G2048_EHIP, "deep hidden: scratch allocation failed");
-        const int rc = launch_onehot_l0(net, packed, boards, (uint32_t)n, activation, a0, s);
-        if (rc) return rc;
-    }
     net.L = layer + 1;   // truncated: deep_forward stops after `layer` (offsets of the kept layers unchanged)
     const int64_t groups = (n + 31) / 32, cap = 2 * (int64_t)device_cus();
     const int grid = (int)(groups < cap ? groups : cap);
-#define G2048_HIDDEN(O, A, A0)                                                                                      \
+#define G2048_HIDDEN(O, A)                                                                                      \
     do {                                                                                                            \
         if (ksplit == 1)                                                                                            \
-            hipLaunchKernelGGL((deep_hidden_kernel<O, A, 1, A0>), dim3(grid), dim3(kDeepBlock), 0, s, net,          \
-                               packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld, a0);                      \
+            hipLaunchKernelGGL((deep_hidden_kernel<O, A, 1>), dim3(grid), dim3(kDeepBlock), 0, s, net,          \
+                               packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld);                      \
         else if (ksplit == 2)                                                                                       \
-            hipLaunchKernelGGL((deep_hidden_kernel<O, A, 2, A0>), dim3(grid), dim3(kDeepBlock), 0, s, net,          \
-                               packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld, a0);                      \
+            hipLaunchKernelGGL((deep_hidden_kernel<O, A, 2>), dim3(grid), dim3(kDeepBlock), 0, s, net,          \
+                               packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld);                      \
         else                                                                                                        \
-            hipLaunchKernelGGL((deep_hidden_kernel<O, A, 0, A0>), dim3(grid), dim3(kDeepBlock), 0, s, net,          \
-                               packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld, a0);                      \
+            hipLaunchKernelGGL((deep_hidden_kernel<O, A, 0>), dim3(grid), dim3(kDeepBlock), 0, s, net,          \
+                               packed, boards, (uint32_t)n, obs_scale, out, (uint32_t)ld);                      \
     } while (0)
     if (obs_mode == G2048_OBS_ONEHOT) {
-        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_ONEHOT, 0, true); else G2048_HIDDEN(G2048_OBS_ONEHOT, 1, true);
+        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_ONEHOT, 0); else G2048_HIDDEN(G2048_OBS_ONEHOT, 1);
     } else if (obs_mode == G2048_OBS_LOG2) {
-        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_LOG2, 0, false); else G2048_HIDDEN(G2048_OBS_LOG2, 1, false);
+        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_LOG2, 0); else G2048_HIDDEN(G2048_OBS_LOG2, 1);
     } else {
-        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_RAW, 0, false); else G2048_HIDDEN(G2048_OBS_RAW, 1, false);
+        if (activation == G2048_ACT_RELU) G2048_HIDDEN(G2048_OBS_RAW, 0); else G2048_HIDDEN(G2048_OBS_RAW, 1);
     }
 #undef G2048_HIDDEN
-    if (a0 && hipFreeAsync(a0, s) != hipSuccess) return dfail(G2048_EHIP, "deep hidden: scratch free failed");
     return check_hip();
 }
 
@@ -2504,10 +2346,6 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
     const int64_t lds = deep_grad_lds_bytes(net, v.nw);
     hipStream_t s = (hipStream_t)stream;
     const int grid = (int)nparts;   // every workgroup writes its slab (zeros when it gets no group)
-    if (obs_mode == G2048_OBS_ONEHOT && n > 0 && !G2048_L0_FUSED) {   // layer 0 on the bf16 MFMA, into d0_out
-        const int rc = launch_onehot_l0(net, packed, boards, (uint32_t)n, activation, d0_out, s);
-        if (rc) return rc;
-    }
     if (obs_mode == G2048_OBS_ONEHOT)
         return activation == G2048_ACT_RELU ? launch_deep_grad<G2048_OBS_ONEHOT, 0>(a, v, grid, lds, s)
                                             : launch_deep_grad<G2048_OBS_ONEHOT, 1>(a, v, grid, lds, s);
