@@ -11,16 +11,17 @@
 //     A-fragment order (one 16-B load per lane = four k-steps) and the activations as the B operand read from LDS;
 //     bias + activation in registers on the way back to LDS; the output layer (4 logits, or the value) on VALU.
 //   * the one-hot first layer (obs_mode "onehot": 16 cells x 17 one-hot features, src/env.py:131-150) is NOT a
-//     272-wide GEMM: x has exactly one 1 per cell, so x W1 = sum over the 16 cells of W1's row 17 c + e_c -- a gather
-//     of 16 rows of the (padded, row-major) W1 table, read straight from the bitboard's nibbles.  Each lane adds the
-//     float4 slices of its board's rows (the 8 lanes of one board read 128-B contiguous pieces of each 1 KiB row).
-//   * g2048_onehot_layer1 / g2048_onehot_dw1: the same gather for the update's kept layer-1 activations, and its
-//     transpose -- dW1 = X^T D1 of a one-hot X is a 16-row scatter-add of each sample's layer-1 delta: one wave owns
-//     a 64-unit slice of a [272][64] LDS accumulator (rows 17 c + e_c, conflict-free: one row per wave-wide add),
-//     a contiguous range of samples, and writes one fp32 partial slab; g2048_fold_partials sums the slabs in fp64.
-// Roofline: the dense layers are fp32-MFMA bound (157.3 TFLOP/s dense fp32 on MI355X); the one-hot gather moves
-// 16 rows x 4 H1 B per board through L1/L2 instead of 2 x 272 x H1 flops; dW1 is LDS-bound (16 adds of 256 B per
-// sample and slice).
+//     272-wide fp32 GEMM: x has exactly one 1 per cell, so each cell's slice of x is an exact bf16 operand, and W1 is
+//     packed as three exact bf16 planes (w = p0 + p1 + p2): per cell and 32-unit tile 3 v_mfma_f32_32x32x16_bf16
+//     (onehot_l0_tile / deep_forward), every product exact, act((hi + lo) + b1) -- the same bits in the rollout, the
+//     policy and (since round 6, no separate layer-0 kernel) inside the gradient kernel.
+//   * g2048_onehot_layer1 / g2048_onehot_dw1: the update's layer-1 activations for the hipBLASLt path (a gather of the
+//     16 W1 rows a board selects), and dW1 = X^T D1 of a one-hot X on the bf16 MFMA (A = the exact one-hot of two
+//     cells, B = the deltas split into three exact bf16 planes), one fp32 partial slab per workgroup, the slabs summed
+//     in fp64 by g2048_fold_partials.
+// Roofline: the dense layers are fp32-MFMA bound (157.3 TFLOP/s dense fp32 on MI355X); the one-hot layer 0 and dW1
+// run on the bf16 MFMA at 3 planes per product; the gather of g2048_onehot_layer1 is L2-bound (16 rows x 4 H1 B per
+// sample).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -90,7 +91,7 @@ __host__ __device__ inline int tile_row(int r, int h) { return (r & 3) + 8 * (r 
 //                     W1[17 c + 8 (l >> 5) + j][32 t + (l & 31)], j = 0..7 (split3_bf16: w = p0 + p1 + p2 exactly)
 struct DeepNet {
     int L;                            // hidden layers
-    int onehot;                       // first layer is the one-hot gather table
+    int onehot;                       // first layer is the one-hot bf16-plane table
     int nt[kMaxHidden];
     int64_t w[kMaxHidden + 1], b[kMaxHidden + 1];
     int64_t wpl;                      // one-hot: W1's bf16-plane A fragments (see the layout note above)
@@ -220,23 +221,43 @@ struct DeepSmem {
 // every fragment load is issued two k-tiles (~2,000 cycles) before its use -- L2 latency under the gradient kernel's
 // load exceeded the one k-tile of round 4's double buffer.  Past the end the window reloads the last k-tile
 // (harmless, an L1 hit).  (Without a barrier hipcc sank every fragment load next to its MFMA and waited for it there:
-// four L2 round trips per k-tile.)  Same MFMAs in the same order as a plain loop.
+// four L2 round trips per k-tile.)  The B operands run one segment (4 k-steps) ahead: the next segment's two
+// ds_read2 are issued before this segment's MFMAs, so no segment waits for LDS reads issued next to its own first
+// MFMA (round 6: runner-config update 1.215 -> 1.179 s, rollout 0.252 -> 0.240 s, `profiles/round6/r7h/`).  Same
+// MFMAs in the same order as a plain loop.
 template <int STRIDE = kActStride>
 __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, const float* in, int t0, int t1, int h,
                                                int col) {
     floatx16 c = {};
     if (t0 >= t1) return c;
     float4 fa[4], fb[4];
-    const auto seg = [&](float4& f, int t, int q, int tn) {
-        const float* ib = in + (32 * t + 4 * h) * STRIDE + col + 8 * q * STRIDE;   // k-step 4 q + u: row 8 q + u + 4 h
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, ib[0 * STRIDE], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, ib[1 * STRIDE], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, ib[2 * STRIDE], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, ib[3 * STRIDE], c, 0, 0, 0);
-        f = fo[tn * 256 + q * 64];
-        __builtin_amdgcn_sched_barrier(0);
-    };
     const int last = t1 - 1;
+    // the B operands (4 LDS values per segment) one segment ahead: the next segment's reads are issued before this
+    // segment's MFMAs, so a segment waits for reads issued ~4 MFMAs earlier instead of its own
+    const float* base = in + 4 * h * STRIDE + col;
+    const auto ld4 = [&](float (&v)[4], int t, int q) {
+        const float* ib = base + (32 * t + 8 * q) * STRIDE;   // k-step 4 q + u: row 8 q + u + 4 h
+        v[0] = ib[0 * STRIDE];
+        v[1] = ib[1 * STRIDE];
+        v[2] = ib[2 * STRIDE];
+        v[3] = ib[3 * STRIDE];
+    };
+    float bc[4], bn[4];
+    ld4(bc, t0, 0);
+    const auto seg = [&](float4& f, int t, int q, int tn) {
+        ld4(bn, q < 3 ? t : (t + 1 < t1 ? t + 1 : last), (q + 1) & 3);   // past the end: a harmless re-read
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, bc[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, bc[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, bc[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, bc[3], c, 0, 0, 0);
+        f = fo[tn * 256 + q * 64];
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next segment's 2 ds_read2 first,
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // then this segment's 4 MFMAs,
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // then the fragment reload
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; i++) bc[i] = bn[i];
+    };
 #pragma unroll
     for (int q = 0; q < 4; q++) fa[q] = fo[t0 * 256 + q * 64];
 #pragma unroll
@@ -934,7 +955,7 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
 //     the forward's MFMA chain on the backward fragments (W_l in A-fragment order, streamed from L2), written over
 //     a_{l-1} in LDS;
 //   * first layer: log2 / raw obs: dW_0 += x^T delta_0 on MFMA (x rebuilt from the boards); one-hot obs: delta_0 is
-//     written out ([n][H0p], row-major) for g2048_onehot_dw1's scatter;
+//     written out ([n][H0p], row-major) for g2048_onehot_dw1's bf16 MFMA;
 //   * biases: per-thread sums (unit = thread).
 // Every workgroup writes one fp32 partial slab (g2048_fold_partials sums them in fp64).
 // Three instantiations by the net's dense dW tile count (deep_grad_variant), every one at two waves per SIMD so that
@@ -1396,9 +1417,31 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     const float* ap = A + (32 * ti + col) * kActStride + h;
                     const float* dp = D + (32 * tj + col) * kActStride + h;
                     floatx16 c = acc[k];
+                    // the operands of k-steps 8..15 read while the MFMAs of 0..7 run (the same MFMAs, same order)
+                    float av[2][8], dv[2][8];
 #pragma unroll
-                    for (int s2 = 0; s2 < 16; s2++)
-                        c = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[2 * s2], dp[2 * s2], c, 0, 0, 0);
+                    for (int i = 0; i < 8; i++) {
+                        av[0][i] = ap[2 * i];
+                        dv[0][i] = dp[2 * i];
+                    }
+#pragma unroll
+                    for (int hh = 0; hh < 2; hh++) {
+                        if (hh == 0) {
+#pragma unroll
+                            for (int i = 0; i < 8; i++) {
+                                av[1][i] = ap[2 * (8 + i)];
+                                dv[1][i] = dp[2 * (8 + i)];
+                            }
+                        }
+#pragma unroll
+                        for (int i = 0; i < 8; i++)
+                            c = __builtin_amdgcn_mfma_f32_32x32x2f32(av[hh][i], dv[hh][i], c, 0, 0, 0);
+                        if (hh == 0) {
+                            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // the second half's reads first
+                            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // then the first half's MFMAs
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    }
                     acc[k] = c;
                 }
             }
@@ -1438,7 +1481,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         {
             DEEP_LANE_IDS;
             if constexpr (OBS == G2048_OBS_ONEHOT) {
-                // delta_0 out for the one-hot scatter (g2048_onehot_dw1): row j, unit tid (coalesced rows) -- by the last
+                // delta_0 out for the one-hot dW1 (g2048_onehot_dw1): row j, unit tid (coalesced rows) -- by the last
                 // launch of a multi-launch net only (each launch recomputes the same rows)
                 const int H0 = 32 * net.nt[0];
                 if (tid < H0 && a.last_pass) {
@@ -2129,9 +2172,6 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
     }
     int64_t grid = (n_order + 31) / 32;
     if (grid > 2 * (int64_t)cus) grid = 2 * (int64_t)cus;   // persistent; the slots refill from the queue
-    if (obs == G2048_OBS_ONEHOT)
-        return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_ONEHOT, 0, 32>(a, (int)grid, s)
-                                            : launch_deep_roll<G2048_OBS_ONEHOT, 1, 32>(a, (int)grid, s);
     if (obs == G2048_OBS_LOG2)
         return activation == G2048_ACT_RELU ? launch_deep_roll<G2048_OBS_LOG2, 0, 32>(a, (int)grid, s)
                                             : launch_deep_roll<G2048_OBS_LOG2, 1, 32>(a, (int)grid, s);
