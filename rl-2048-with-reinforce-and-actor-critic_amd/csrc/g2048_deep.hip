@@ -982,7 +982,8 @@ constexpr int kDeepGradMaxBlock = 512;
 // One unit tile t of a one-hot layer 0 for 32 boards (lane col: board b) by the exact bf16-plane MFMAs: per cell one
 // exact one-hot B operand, hi plane into `hi`, mid and lo planes into `lo` (deep_forward's arithmetic, the same
 // bits), W1's plane fragments streamed from the packed net one cell ahead, the bias loaded after the chain; writes
-// act((hi + lo) + b1) to out[unit * stride + col].  The gradient kernel's layer 0.
+// act((hi + lo) + b1) to out[unit * stride + col].  The gradient kernel's layer 0.  (Two cells ahead -- with one
+// accumulator to fit the registers -- measured the same: 1.175-1.180 s against 1.179-1.180 s, profiles/round6/r7k/.)
 template <int ACT>
 __device__ __forceinline__ void onehot_l0_tile(const float* __restrict__ P, const DeepNet& net, int t, uint64_t b,
                                                float* out, int stride) {
@@ -1074,7 +1075,8 @@ struct DeepGradArgs {
 // __syncthreads() adds a workgroup release fence, i.e. vmcnt(0): every barrier would wait for the wave's global
 // stores (the V(s) / delta_0 rows) and for the weight-fragment loads a chain's window left in flight, none of which
 // another wave reads (loaded values are waited for at their use, as always).  The group's first barrier keeps
-// __syncthreads(): it retires the layer-0 LDS-DMA.  (__syncthreads() everywhere measured the same, round 5.)
+// __syncthreads() (the loads of the group's inputs).  (__syncthreads() everywhere measured the same, round 5; the
+// group's first barrier and the 64-slot rollout's barriers as LDS-only ones measured the same too, round 6 r7l/.)
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
