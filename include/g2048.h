@@ -377,20 +377,20 @@ int g2048_deep_rollout(const float* packed, int n_hidden, const int32_t* hidden,
                        const uint64_t* pol_inc, uint64_t* pol_buf, uint32_t* queue, const int32_t* order,
                        int64_t n_order, int resume, const g2048_suspend* sus, int64_t n, int64_t cap,
                        const g2048_traj* traj, void* stream);
-/* The activations of hidden layer `layer` as g2048_deep_grad computes them (in its 8-wave instantiations -- nets of
- * 41..64 dense tiles -- a layer with fewer than 8 output tiles and at least 2 k-tiles sums two half-k chains; the
- * 4-wave one and g2048_deep_policy / g2048_deep_rollout keep one chain):
+/* The activations of hidden layer `layer` as g2048_deep_grad computes them (in its 32-sample instantiations -- log2 /
+ * raw nets, one-hot nets of 41..64 dense tiles -- a layer with fewer than 8 output tiles and at least 2 k-tiles sums
+ * two half-k chains; the 64-sample one and g2048_deep_policy / g2048_deep_rollout keep one chain):
  * out[j * ld + u], u < its padded width (tests and diagnostics: the gradient kernel's own activation pattern). */
 int g2048_deep_hidden(const float* packed, int n_hidden, const int32_t* hidden, int activation, int obs_mode,
                       float obs_scale, const uint64_t* boards, int64_t n, int layer, float* out, int64_t ld,
                       void* stream);
 /* update_batch's actor or critic gradient (src/reinforce_agent.py:403-555, _backpropagation :639-678) fused for a
- * packed deep net (forward + loss gradient + backward in one kernel, 32 samples per workgroup step), covered when
+ * packed deep net (forward + loss gradient + backward in one kernel, 32 or 64 samples per workgroup step), covered when
  * g2048_deep_grad_slab() >= 0 (1..4 hidden layers of 1..256 units).  Nets of at most 64 dense 32x32 weight-gradient
  * tiles on one-hot obs (48 on log2 / raw: [256, 256], [256, 128, 64] and smaller) take one launch; larger ones one
- * launch per range of tiles, each redoing the forward and delta chains (g2048_deep_grad_passes()).  ABI 14: nets of
- * at most 40 tiles run two 4-wave workgroups per CU -- pass nparts = g2048_deep_grad_parts() (any nparts >= 1 is
- * correct; that one fills the chip).
+ * launch per range of tiles, each redoing the forward and delta chains (g2048_deep_grad_passes()).  The workgroup
+ * count depends on the instantiation (ABI 14; one per CU since round 6) -- pass nparts = g2048_deep_grad_parts()
+ * (any nparts >= 1 is correct; that one fills the chip).
  * grad_packed: g2048_deep_grad_pack (the dense layers' weights in backward-fragment order; re-pack after every
  * update).  Actor: coef = advantage x step weight, actions; critic (critic = 1): coef = step weight, target =
  * r + gamma V(s') m, loss 0 MSE / 1 Huber, delta_out = target - V, value_out = V (NULL ok).  partials [nparts][slab]

@@ -960,18 +960,24 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
 // Every workgroup writes one fp32 partial slab (g2048_fold_partials sums them in fp64).
 // Three instantiations by the net's dense dW tile count (deep_grad_variant), every one at two waves per SIMD so that
 // one wave's MFMA chains run while the other's gathers, epilogues and barriers do:
-//   * NW = 4, TPW = 10 (<= 40 tiles, LDS <= 80 KiB): TWO 4-wave workgroups per CU, each on its own 32-sample
-//     groups -- the two overlap each other's barriers, gathers and VALU phases (round 5; the runner config's
-//     [256, 128, 64] has exactly 40 tiles).  Its dense layers run the plain k-ordered chain (every output tile on one
-//     wave, as deep_forward), so its activations are bit for bit the rollout / policy kernels'.
-//   * NW = 8, TPW = 6 (<= 48 tiles): one 8-wave workgroup per CU (round 4); dense layers with fewer than 8 output
-//     tiles split k in two halves (dense_fwd_split) to keep the idle waves busy.
+//   * NB = 64, NW = 8, TPW = 5 (one-hot nets of <= 40 tiles whose LDS fits 160 KiB at 64 samples: the runner config's
+//     [256, 128, 64] has exactly 40 tiles; round 6): one 8-wave workgroup per CU on 64-sample groups (two 32-sample
+//     column tiles, LDS rows of 65 floats) -- every weight fragment (W1 planes, forward and backward dense
+//     fragments) is read from L2 once per 64 samples instead of 32, the two column tiles of one output tile on
+//     neighbouring waves (the second read hits L1), and a group's barriers are paid once per 64 samples; each dW tile
+//     contracts over 64 samples (32 k-steps) in its 5-tile register budget.  Every output tile of a dense layer is the
+//     plain k-ordered chain (deep_forward's), so its activations are bit for bit the rollout / policy kernels'.
+//     Runner config, 1M episodes, interleaved on one box: update 1.1524-1.1553 s against 1.1784-1.1808 s for round
+//     5's two 4-wave workgroups per CU on 32-sample groups (NW = 4, TPW = 10; profiles/round6/r7n/), which it
+//     replaces (no net reaches that form's LDS bound without exceeding this one's).
+//   * NW = 8, TPW = 6 (<= 48 tiles): 32-sample groups on one 8-wave workgroup per CU (round 4); dense layers with
+//     fewer than 8 output tiles split k in two halves (dense_fwd_split) to keep the idle waves busy.
 //   * NW = 8, TPW = 8 (<= 64 tiles: one-hot / log2 [256, 256] and [256, 256, x] nets, round 5): as above with 128
 //     accumulator registers per wave.
 // (A 4-wave workgroup alone per CU with 12 tiles per wave took the whole register file, one wave per SIMD.)
 constexpr int kDeepGradMaxBlock = 512;
 // Tried, not kept (measured on the runner config; the A/B switches are gone from the source): the 4-wave
-// instantiation's 64-unit layer as a 4-way k split (no change); log2 / raw nets of 49..64 dense tiles on the 8 x 8
+// instantiation's 64-unit layer as a 4-way k split (no change, round 5); log2 / raw nets of 49..64 dense tiles on the 8 x 8
 // instantiation (spills ~300 VGPRs; the two-layer cooperative kernel runs them); the delta_0 rows by 16-byte stores
 // (a quarter of the store instructions): 1.2535-1.2542 s against 1.2499-1.2517 s (profiles/round6/r7b/d0b128_*).
 // The one-hot layer 0 is computed here (onehot_l0_tile) since round 6: with the per-phase lane ids below the kernel
@@ -1020,8 +1026,64 @@ __device__ __forceinline__ void onehot_l0_tile(const float* __restrict__ P, cons
     for (int i = 0; i < 16; i++) out[(32 * t + tile_row(i, h)) * stride + col] = activate<ACT>((hi[i] + lo[i]) + bv[i]);
 }
 
+// The same for CT column tiles of 32 boards (the 64-sample gradient groups): one fragment stream, CT B operands
+// (as deep_forward64).  (A separate function: the CT = 1 case written this way compiled to other registers and made
+// round 5's 4 x 10 gradient kernel spill 22 VGPRs.)  Two cells ahead spills 5 VGPRs and measured slower: 1.169-1.172 s
+// against 1.150-1.153 s (profiles/round6/r7p/).
+template <int ACT, int CT>
+__device__ __forceinline__ void onehot_l0_tile_cols(const float* __restrict__ P, const DeepNet& net, int t,
+                                               const uint64_t (&b)[CT], float* out, int stride) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    int tq = (int)threadIdx.x;
+    asm volatile("" : "+v"(tq));   // lane ids derived here, not hoisted out of the caller's group loop
+    const int lane = tq & 63, h = lane >> 5, col = lane & 31;
+    const u32x4* ft = reinterpret_cast<const u32x4*>(P + net.wpl) + lane + (int64_t)t * (kOneHotPlaneFloats / 4);
+    u32x4 f[2][3];
+#pragma unroll
+    for (int pl = 0; pl < 3; pl++) f[0][pl] = ft[pl * 64];
+    floatx16 hi[CT], lo[CT];
+#pragma unroll
+    for (int cc = 0; cc < CT; cc++) hi[cc] = lo[cc] = floatx16{};
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        if (c + 1 < 16) {
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++) f[(c + 1) & 1][pl] = ft[((c + 1) * 3 + pl) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 bvv[CT];
+#pragma unroll
+        for (int cc = 0; cc < CT; cc++) {
+            const uint32_t nib = (uint32_t)(b[cc] >> (4 * c)) & 15u;
+            u32x4 dv;
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++)
+                dv[jj] = (nib == (uint32_t)(8 * h + 2 * jj) ? 0x3F80u : 0u) | (nib == (uint32_t)(8 * h + 2 * jj + 1) ? 0x3F800000u : 0u);
+            bvv[cc] = __builtin_bit_cast(bf16x8, dv);
+        }
+#pragma unroll
+        for (int cc = 0; cc < CT; cc++)
+            hi[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][0]), bvv[cc], hi[cc], 0, 0, 0);
+#pragma unroll
+        for (int cc = 0; cc < CT; cc++)
+            lo[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][1]), bvv[cc], lo[cc], 0, 0, 0);
+#pragma unroll
+        for (int cc = 0; cc < CT; cc++)
+            lo[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f[c & 1][2]), bvv[cc], lo[cc], 0, 0, 0);
+    }
+    float bv[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) bv[i] = P[net.b[0] + 32 * t + tile_row(i, h)];
+#pragma unroll
+    for (int cc = 0; cc < CT; cc++)
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            out[(32 * t + tile_row(i, h)) * stride + 32 * cc + col] = activate<ACT>((hi[cc][i] + lo[cc][i]) + bv[i]);
+}
+
 struct DeepGradVariant {
     int nw, tpw, ksplit, per_cu, passes;   // passes > 1: the dense dW tiles in ranges of nw x tpw, one launch each
+    int nb = 32;                           // samples per group
 };
 
 struct DeepGradArgs {
@@ -1102,9 +1164,12 @@ __device__ __forceinline__ int fresh_tid() {
     (void)h;                                                                             \
     (void)col
 
-template <int OBS, int ACT, int NW, int TPW, int KSPLIT>
+template <int OBS, int ACT, int NW, int TPW, int KSPLIT, int NB = 32>
 __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs a) {
+    static_assert(NB == 32 || (NB == 64 && NW == 8 && KSPLIT == 0 && OBS == G2048_OBS_ONEHOT), "64-sample groups");
     constexpr int kBlock = 64 * NW;
+    constexpr int SS = NB + 1;    // LDS row stride in floats: [unit][NB samples + 1]
+    constexpr int CT = NB / 32;   // 32-sample column tiles per group
     extern __shared__ float dyn[];
     const DeepNet& net = a.net;
     const int L = net.L;
@@ -1116,18 +1181,18 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     // partials, g, the boards and each thread's bias-gradient sums
     const auto actl = [&](int l) { return dyn + a.aoff[l]; };
     float* lds_end = dyn + a.lds_tail;
-    float (*part)[32][4] = reinterpret_cast<float (*)[32][4]>(lds_end);          // [8][32][4]
-    float (*gs)[4] = reinterpret_cast<float (*)[4]>(lds_end + 8 * 32 * 4);       // [32][4]
-    uint64_t* bds = reinterpret_cast<uint64_t*>(lds_end + 8 * 32 * 4 + 32 * 4);  // [32]
-    float* dbs = lds_end + 8 * 32 * 4 + 32 * 4 + 64;                             // [kMaxHidden][256]: db_l of unit tid
+    float (*part)[NB][4] = reinterpret_cast<float (*)[NB][4]>(lds_end);          // [8][NB][4]
+    float (*gs)[4] = reinterpret_cast<float (*)[4]>(lds_end + 8 * NB * 4);       // [NB][4]
+    uint64_t* bds = reinterpret_cast<uint64_t*>(lds_end + 8 * NB * 4 + NB * 4);  // [NB]
+    float* dbs = lds_end + 8 * NB * 4 + NB * 4 + 2 * NB;                         // [kMaxHidden][256]: db_l of unit tid
     float* wol = dbs + kMaxHidden * 256;                                         // [HL][4] output weights, then [4] bias
     // the group's per-sample inputs (coef, action, target / TD row: [7][32]) and the db_out sums ([32][4]) in LDS
     // instead of registers across the forward and delta chains (round 5: 29 -> 16 spilled VGPRs)
     float* smp_in = wol + 256 * 4 + 4;
-    float* dbo_l = smp_in + 7 * 32;
+    float* dbo_l = smp_in + 7 * NB;
     if (tid < 256)
         for (int l = 0; l < kMaxHidden; l++) dbs[l * 256 + tid] = 0.0f;
-    if (tid < 128) dbo_l[tid] = 0.0f;
+    if (tid < 4 * NB) dbo_l[tid] = 0.0f;
     const float* P = a.packed;
     {   // the output layer's weights and bias in LDS for the whole launch (its phases read them every group)
         const int HLw = 32 * net.nt[L - 1] * 4;
@@ -1144,10 +1209,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     // g over the groups (the slots are added in order at the end)
     float dwo[4] = {0.f, 0.f, 0.f, 0.f}, dbl = 0.f;
     const int HL = 32 * net.nt[L - 1];
-    const int oq = kBlock / HL, oper = (32 + oq - 1) / oq;   // sample ranges of the output layer
+    const int oq = kBlock / HL, oper = (NB + oq - 1) / oq;   // sample ranges of the output layer
     const float4* wout = reinterpret_cast<const float4*>(wol);
     const float* bo = wol + 4 * HL;
-    const uint32_t groups = (a.n + 31u) >> 5;
+    const uint32_t groups = (a.n + (uint32_t)(NB - 1)) / (uint32_t)NB;
 #if G2048_DEEP_DIAG
     uint64_t dph[kDiagSlots] = {};
     uint64_t dlast = __builtin_amdgcn_s_memtime();
@@ -1156,18 +1221,18 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         float td_v = 0.0f;   // V(s') of the critic's TD row (loaded after layer 0, used at the logits)
         {
             DEEP_LANE_IDS;
-            const uint32_t j = gi * 32u + (uint32_t)(tid & 31);
+            const uint32_t j = gi * (uint32_t)NB + (uint32_t)(tid & (NB - 1));
             const bool valid = j < a.n;
             const uint32_t jc = valid ? j : a.n - 1u;
-            if (tid < 32) bds[tid] = valid ? a.boards[j] : 0ull;
+            if (tid < NB) bds[tid] = valid ? a.boards[j] : 0ull;
             // the sample's coefficient / action / target, loaded now so that the forward covers their latency
-            const float cf = (tid < 32 && valid) ? a.coef[jc] : 0.0f;
-            const uint32_t act_j = (tid < 32 && !a.critic) ? a.actions[jc] : 0u;
+            const float cf = (tid < NB && valid) ? a.coef[jc] : 0.0f;
+            const uint32_t act_j = (tid < NB && !a.critic) ? a.actions[jc] : 0u;
             // the critic's target, or (TD rows) its reward / has-next / lane now and V(s') once layer 0 is done (the
             // lane index has arrived by then: no dependent load in front of the first barrier)
             float tg = 0.0f, td_r = 0.0f, td_h = 0.0f;
             int64_t td_l = 0;
-            if (tid < 32 && a.critic) {
+            if (tid < NB && a.critic) {
                 if (a.has_td) {
                     td_l = a.td.lane[jc];
                     td_r = a.td.reward[jc];
@@ -1177,14 +1242,14 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 }
             }
             __syncthreads();   // (a fence: vmcnt(0) -- the loads above have arrived)
-            if (tid < 32) {   // read back at the logits: their registers are free until then
+            if (tid < NB) {   // read back at the logits: their registers are free until then
                 smp_in[tid] = cf;
-                smp_in[32 + tid] = __uint_as_float(act_j);
-                smp_in[64 + tid] = tg;
-                smp_in[96 + tid] = td_r;
-                smp_in[128 + tid] = td_h;
-                smp_in[160 + tid] = __uint_as_float((uint32_t)td_l);
-                smp_in[192 + tid] = __uint_as_float((uint32_t)((uint64_t)td_l >> 32));
+                smp_in[NB + tid] = __uint_as_float(act_j);
+                smp_in[2 * NB + tid] = tg;
+                smp_in[3 * NB + tid] = td_r;
+                smp_in[4 * NB + tid] = td_h;
+                smp_in[5 * NB + tid] = __uint_as_float((uint32_t)td_l);
+                smp_in[6 * NB + tid] = __uint_as_float((uint32_t)((uint64_t)td_l >> 32));
             }
         }
         DEEP_STAMP(0);
@@ -1194,7 +1259,14 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             float* out = actl(0);
             const int nt0 = net.nt[0];
             if constexpr (OBS == G2048_OBS_ONEHOT) {
-                for (int t = w; t < nt0; t += NW) onehot_l0_tile<ACT>(P, net, t, bds[col], out, kActStride);
+                if constexpr (CT == 1) {
+                    for (int t = w; t < nt0; t += NW) onehot_l0_tile<ACT>(P, net, t, bds[col], out, SS);
+                } else {
+                    uint64_t bc[CT];
+#pragma unroll
+                    for (int cc = 0; cc < CT; cc++) bc[cc] = bds[32 * cc + col];
+                    for (int t = w; t < nt0; t += NW) onehot_l0_tile_cols<ACT, CT>(P, net, t, bc, out, SS);
+                }
             } else {
                 const uint64_t b = bds[col];
                 float x[8];
@@ -1210,7 +1282,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
 #pragma unroll
                     for (int r = 0; r < 16; r++) {
                         const int u = tile_row(r, h);
-                        out[(32 * t + u) * kActStride + col] = activate<ACT>(c[r] + bb[u]);
+                        out[(32 * t + u) * SS + col] = activate<ACT>(c[r] + bb[u]);
                     }
                 }
             }
@@ -1219,9 +1291,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         DEEP_STAMP(1);
         {
             DEEP_LANE_IDS;
-            if (tid < 32 && a.critic && a.has_td) {
-                const int64_t tl = (int64_t)((uint64_t)__float_as_uint(smp_in[160 + tid]) |
-                                             ((uint64_t)__float_as_uint(smp_in[192 + tid]) << 32));
+            if (tid < NB && a.critic && a.has_td) {
+                const int64_t tl = (int64_t)((uint64_t)__float_as_uint(smp_in[5 * NB + tid]) |
+                                             ((uint64_t)__float_as_uint(smp_in[6 * NB + tid]) << 32));
                 td_v = a.td.v_next[tl];
             }
         }
@@ -1235,14 +1307,17 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             if constexpr (KSPLIT != 0) {
                 dense_fwd_split<ACT, NW, KSPLIT>(in, out, frag, P + net.b[l], ntin, ntout, w);
             } else {   // deep_forward's chain: the rollout / policy kernels' bits
-                for (int o = w; o < ntout; o += NW) {
-                    const floatx16 c = frag_chain(frag + (int64_t)o * ntin * 256, in, 0, ntin, h, col);
+                // item i = (output tile i / CT, column tile i % CT): the column tiles of one output tile on
+                // neighbouring waves, so the second read of each fragment hits L1 (as deep_forward64)
+                for (int i = w; i < CT * ntout; i += NW) {
+                    const int o = i >> (CT - 1), cc = i & (CT - 1);
+                    const floatx16 c = frag_chain<SS>(frag + (int64_t)o * ntin * 256, in + 32 * cc, 0, ntin, h, col);
                     const float* bb = P + net.b[l] + 32 * o;
                     float bv[16];
 #pragma unroll
                     for (int r = 0; r < 16; r++) bv[r] = bb[tile_row(r, h)];
 #pragma unroll
-                    for (int r = 0; r < 16; r++) out[(32 * o + tile_row(r, h)) * kActStride + col] = activate<ACT>(c[r] + bv[r]);
+                    for (int r = 0; r < 16; r++) out[(32 * o + tile_row(r, h)) * SS + 32 * cc + col] = activate<ACT>(c[r] + bv[r]);
                 }
             }
             lds_barrier();
@@ -1254,16 +1329,16 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         //      uses all four; profiles/round6/r7c/, r7d/)
         {
             DEEP_LANE_IDS;
-            if (tid < 256) {
+            if (tid < 8 * NB) {
                 const float* in = actl(L - 1);
-                const int pp = tid >> 5, bb = tid & 31, per = HL >> 3;
+                const int pp = tid >> (CT + 4), bb = tid & (NB - 1), per = HL >> 3;
                 float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
                 if (per == 8) {   // a 64-unit last layer: the slice's 8 reads in flight, then the same chain
                     float x[8];
                     float4 wv[8];
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
-                        x[i] = in[(8 * pp + i) * kActStride + bb];
+                        x[i] = in[(8 * pp + i) * SS + bb];
                         wv[i] = wout[8 * pp + i];
                     }
                     __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
@@ -1276,7 +1351,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     }
                 } else
                 for (int u = pp * per; u < (pp + 1) * per; u++) {
-                    const float x = in[u * kActStride + bb];
+                    const float x = in[u * SS + bb];
                     const float4 wv = wout[u];
                     s0 = fmaf(x, wv.x, s0);
                     s1 = fmaf(x, wv.y, s1);
@@ -1294,13 +1369,13 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         // ---- logits -> g (threads 0..31, one sample each)
         {
             DEEP_LANE_IDS;
-                const uint32_t j = gi * 32u + (uint32_t)(tid & 31);
-                const bool valid = j < a.n;
-            if (tid < 32) {
+            const uint32_t j = gi * (uint32_t)NB + (uint32_t)(tid & (NB - 1));
+            const bool valid = j < a.n;
+            if (tid < NB) {
                 const float cf_ = smp_in[tid];
-                const uint32_t act_j_ = __float_as_uint(smp_in[32 + tid]);
-                float tg_ = smp_in[64 + tid];
-                const float td_r_ = smp_in[96 + tid], td_h_ = smp_in[128 + tid];
+                const uint32_t act_j_ = __float_as_uint(smp_in[NB + tid]);
+                float tg_ = smp_in[2 * NB + tid];
+                const float td_r_ = smp_in[3 * NB + tid], td_h_ = smp_in[4 * NB + tid];
                 float lg[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
@@ -1351,8 +1426,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             // ---- output layer backward: dW_out, db_{L-1}, delta_{L-1} in place; thread (unit u, sample range q) of
             //      oq ranges, so every thread works (one thread per unit ran 32 serial steps on one or two waves)
             if (tid < oq * HL) {
-                const int u = tid % HL, q = tid / HL, n0 = q * oper, n1 = n0 + oper < 32 ? n0 + oper : 32;
-                float* arow = actl(L - 1) + u * kActStride;
+                const int u = tid % HL, q = tid / HL, n0 = q * oper, n1 = n0 + oper < NB ? n0 + oper : NB;
+                float* arow = actl(L - 1) + u * SS;
                 const float4 wv = wout[u];
                 float d0 = dwo[0], d1 = dwo[1], d2 = dwo[2], d3 = dwo[3], db = dbl;
                 const auto step = [&](int n2, float x, float4 g4) {
@@ -1416,10 +1491,12 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 const int f = a.tile0 + w + NW * k;
                 if (f >= f0 && f < f1) {                     // wave-uniform
                     const int ti = (f - f0) / ntout, tj = (f - f0) % ntout;
-                    const float* ap = A + (32 * ti + col) * kActStride + h;
-                    const float* dp = D + (32 * tj + col) * kActStride + h;
+                    const float* ap = A + (32 * ti + col) * SS + h;
+                    const float* dp = D + (32 * tj + col) * SS + h;
                     floatx16 c = acc[k];
-                    // the operands of k-steps 8..15 read while the MFMAs of 0..7 run (the same MFMAs, same order)
+                    // in chunks of 8 k-steps, the next chunk's operands read while this chunk's MFMAs run (the same
+                    // MFMAs, same order)
+                    constexpr int NCH = NB / 16;
                     float av[2][8], dv[2][8];
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
@@ -1427,20 +1504,20 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                         dv[0][i] = dp[2 * i];
                     }
 #pragma unroll
-                    for (int hh = 0; hh < 2; hh++) {
-                        if (hh == 0) {
+                    for (int hh = 0; hh < NCH; hh++) {
+                        if (hh + 1 < NCH) {
 #pragma unroll
                             for (int i = 0; i < 8; i++) {
-                                av[1][i] = ap[2 * (8 + i)];
-                                dv[1][i] = dp[2 * (8 + i)];
+                                av[(hh + 1) & 1][i] = ap[2 * (8 * (hh + 1) + i)];
+                                dv[(hh + 1) & 1][i] = dp[2 * (8 * (hh + 1) + i)];
                             }
                         }
 #pragma unroll
                         for (int i = 0; i < 8; i++)
-                            c = __builtin_amdgcn_mfma_f32_32x32x2f32(av[hh][i], dv[hh][i], c, 0, 0, 0);
-                        if (hh == 0) {
-                            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // the second half's reads first
-                            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // then the first half's MFMAs
+                            c = __builtin_amdgcn_mfma_f32_32x32x2f32(av[hh & 1][i], dv[hh & 1][i], c, 0, 0, 0);
+                        if (hh + 1 < NCH) {
+                            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // the next chunk's reads first
+                            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // then this chunk's MFMAs
                             __builtin_amdgcn_sched_barrier(0);
                         }
                     }
@@ -1452,22 +1529,23 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             // delta_{l-1} = (W_l delta_l) act'(a_{l-1}): output tiles = layer l-1's units, k = layer l's units
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(a.bpacked + a.boff[l]) + lane;
             float* Aw = actl(l - 1);
-            for (int o = w; o < ntin; o += NW) {
-                const floatx16 c = frag_chain(frag + (int64_t)o * ntout * 256, D, 0, ntout, h, col);
+            for (int i = w; i < CT * ntin; i += NW) {
+                const int o = i >> (CT - 1), cc = i & (CT - 1);
+                const floatx16 c = frag_chain<SS>(frag + (int64_t)o * ntout * 256, D + 32 * cc, 0, ntout, h, col);
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
-                    float* pa = Aw + (32 * o + tile_row(r, h)) * kActStride + col;
+                    float* pa = Aw + (32 * o + tile_row(r, h)) * SS + 32 * cc + col;
                     *pa = c[r] * act_deriv<ACT>(*pa);
                 }
             }
             lds_barrier();
             // db_{l-1} of unit tid
             if (tid < 32 * ntin) {
-                const float* drow = Aw + tid * kActStride;
+                const float* drow = Aw + tid * SS;
                 float db = dbs[(l - 1) * 256 + tid];
                 // 8 rows' reads in flight per wait (the same adds in the same order)
 #pragma unroll
-                for (int n0 = 0; n0 < 32; n0 += 8) {
+                for (int n0 = 0; n0 < NB; n0 += 8) {
                     float v[8];
 #pragma unroll
                     for (int i = 0; i < 8; i++) v[i] = drow[n0 + i];
@@ -1489,10 +1567,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 if (tid < H0 && a.last_pass) {
                     // through a buffer resource over the group's rows (base and row offsets in SGPRs, no 64-bit
                     // per-lane address to keep live; the rows past a ragged group's end fall outside num_records)
-                    const float* drow = actl(0) + tid * kActStride;
-                    const uint32_t left = a.n - gi * 32u < 32u ? a.n - gi * 32u : 32u;
+                    const float* drow = actl(0) + tid * SS;
+                    const uint32_t left = a.n - gi * (uint32_t)NB < (uint32_t)NB ? a.n - gi * (uint32_t)NB : (uint32_t)NB;
                     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-                        a.d0_out + (size_t)gi * 32u * (uint32_t)H0, 0, (int)(left * (uint32_t)H0 * 4u), 0x00020000);
+                        a.d0_out + (size_t)gi * (uint32_t)NB * (uint32_t)H0, 0, (int)(left * (uint32_t)H0 * 4u), 0x00020000);
                     // in batches of 8: the batch's LDS reads issued together, one wait, then its stores (hipcc otherwise
                     // alternated one ds_read2 / one wait / two stores, 16 LDS round trips in series); the row offset
                     // advances by one scalar add per store (as 32 distinct offsets hipcc hoisted them out of the group
@@ -1500,7 +1578,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     const int rowb = __builtin_amdgcn_readfirstlane(H0 * 4);
                     int so = 0;
 #pragma unroll
-                    for (int n0 = 0; n0 < 32; n0 += 8) {
+                    for (int n0 = 0; n0 < NB; n0 += 8) {
                         float v[8];
 #pragma unroll
                         for (int i = 0; i < 8; i++) v[i] = drow[n0 + i];
@@ -1522,7 +1600,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     const int t = w + NW * i;
                     if (t < net.nt[0]) {
                         floatx16 c = acc0[i];
-                        const float* dp = D0 + (32 * t + col) * kActStride + h;
+                        const float* dp = D0 + (32 * t + col) * SS + h;
 #pragma unroll
                         for (int s2 = 0; s2 < 16; s2++) {
                             const float xv = col < 16 ? obs_value<OBS>(bds[2 * s2 + h], col, a.obs_scale) : 0.0f;
@@ -1551,7 +1629,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     float dbo = 0.0f;
     {
         float* red = dyn;                                   // [oq][HL][5]
-        if (tid < 32) {
+        if (tid < NB) {
 #pragma unroll
             for (int k = 0; k < 4; k++) gs[tid][k] = dbo_l[tid * 4 + k];
         }
@@ -1571,7 +1649,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             dbs[(L - 1) * 256 + tid] = sum[4];
         }
         if (tid < 4)
-            for (int q = 0; q < 32; q++) dbo += gs[q][tid];
+            for (int q = 0; q < NB; q++) dbo += gs[q][tid];
         __syncthreads();
     }
     float* out = a.part + (size_t)blockIdx.x * a.pslab;
@@ -1676,17 +1754,18 @@ DeepGradLayout deep_grad_layout(const DeepNet& n) {
 
 // floats of the hidden layers' activations, at least the output layer's final reduction (deep_grad_kernel:
 // [oq][HL][5], oq HL <= the block size)
-int64_t deep_grad_act_floats(const DeepNet& n, int nw) {
+int64_t deep_grad_act_floats(const DeepNet& n, int nw, int nb = 32) {
     int64_t units = 0;
     for (int l = 0; l < n.L; l++) units += 32 * n.nt[l];
-    int64_t f = units * kActStride;
+    int64_t f = units * (nb + 1);
     const int64_t red = 5 * 64 * nw;
     if (red > f) f = red;
     return f;
 }
-int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, bias sums, output weights / bias
-    return (deep_grad_act_floats(n, nw) + 8 * 32 * 4 + 32 * 4 + 64 + kMaxHidden * 256 + 256 * 4 + 4 +
-            7 * 32 + 32 * 4) * 4;
+// + part, g, boards, bias sums, output weights / bias, the per-sample inputs, the db_out sums
+int64_t deep_grad_lds_bytes(const DeepNet& n, int nw, int nb = 32) {
+    return (deep_grad_act_floats(n, nw, nb) + 8 * nb * 4 + nb * 4 + 2 * nb + kMaxHidden * 256 + 256 * 4 + 4 +
+            7 * nb + nb * 4) * 4;
 }
 
 // the instantiation that covers the net (nw = 0: none; see deep_grad_kernel).  The 4-wave and the 64-tile ones are
@@ -1694,8 +1773,8 @@ int64_t deep_grad_lds_bytes(const DeepNet& n, int nw) {   // + part, g, boards, 
 // of 10 or 8 dense tiles per wave, hipcc spills whole accumulator tiles (~300-650 VGPRs).
 DeepGradVariant deep_grad_variant(const DeepNet& n) {
     const int tiles = deep_grad_layout(n).ntiles;
-    if (n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 4) <= 80 * 1024)
-        return {4, 10, 0, 2, 1};
+    if (n.onehot && tiles <= 40 && deep_grad_lds_bytes(n, 8, 64) <= 160 * 1024)
+        return {8, 5, 0, 1, 1, 64};
     if (tiles <= 48 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 6, 1, 1, 1};
     if (n.onehot && tiles <= 64 && deep_grad_lds_bytes(n, 8) <= 160 * 1024) return {8, 8, 1, 1, 1};
     // past one launch's accumulator budget (round 5; e.g. one-hot [256, 256, 256], log2 [256, 256]): the dense dW
@@ -2280,7 +2359,7 @@ int g2048_deep_grad_pack(const float* const* W, int obs_mode, int n_hidden, cons
 }  // extern "C"
 
 namespace {
-template <int OBS, int ACT, int NW, int TPW, int KSPLIT>
+template <int OBS, int ACT, int NW, int TPW, int KSPLIT, int NB = 32>
 int launch_deep_grad_v(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t s) {
     // the dynamic-LDS attribute is per kernel and device: one bit per device id, set on the first launch there
     // (two threads racing both set it, which is harmless)
@@ -2289,19 +2368,19 @@ int launch_deep_grad_v(const DeepGradArgs& a, int grid, int64_t lds, hipStream_t
     if (hipGetDevice(&dev) != hipSuccess) return dfail(G2048_EHIP, "deep gradient: hipGetDevice failed");
     const uint64_t bit = 1ull << (dev & 63);
     if (!(attr_set.load(std::memory_order_acquire) & bit)) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&deep_grad_kernel<OBS, ACT, NW, TPW, KSPLIT>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&deep_grad_kernel<OBS, ACT, NW, TPW, KSPLIT, NB>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return (void)hipGetLastError(), dfail(G2048_EHIP, "deep gradient: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
         attr_set.fetch_or(bit, std::memory_order_acq_rel);
     }
-    hipLaunchKernelGGL((deep_grad_kernel<OBS, ACT, NW, TPW, KSPLIT>), dim3(grid), dim3(64 * NW), (unsigned)lds, s, a);
+    hipLaunchKernelGGL((deep_grad_kernel<OBS, ACT, NW, TPW, KSPLIT, NB>), dim3(grid), dim3(64 * NW), (unsigned)lds, s, a);
     return check_hip();
 }
 
 template <int OBS, int ACT>
 int launch_deep_grad_pass(const DeepGradArgs& a, const DeepGradVariant& v, int grid, int64_t lds, hipStream_t s) {
     if constexpr (OBS == G2048_OBS_ONEHOT) {
-        if (v.nw == 4) return launch_deep_grad_v<OBS, ACT, 4, 10, 0>(a, grid, lds, s);
+        if (v.nb == 64) return launch_deep_grad_v<OBS, ACT, 8, 5, 0, 64>(a, grid, lds, s);
         if (v.tpw == 8) return launch_deep_grad_v<OBS, ACT, 8, 8, 1>(a, grid, lds, s);
     }
     return launch_deep_grad_v<OBS, ACT, 8, 6, 1>(a, grid, lds, s);
@@ -2351,15 +2430,15 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
     a.net = net;
     a.packed = packed;
     a.bpacked = grad_packed;
+    const DeepGradVariant v = deep_grad_variant(net);
     int off = 0;
     for (int l = 0; l < net.L; l++) {
         a.boff[l] = g.boff[l];
         a.tile_begin[l] = g.tile_begin[l];
         a.aoff[l] = off;
-        off += 32 * net.nt[l] * kActStride;
+        off += 32 * net.nt[l] * (v.nb + 1);
     }
-    const DeepGradVariant v = deep_grad_variant(net);
-    a.lds_tail = (int)deep_grad_act_floats(net, v.nw);   // >= off: room for the output layer's reduction
+    a.lds_tail = (int)deep_grad_act_floats(net, v.nw, v.nb);   // >= off: room for the output layer's reduction
     for (int l = 0; l <= net.L; l++) {
         a.pw[l] = g.pw[l];
         a.pb[l] = g.pb[l];
@@ -2385,7 +2464,7 @@ int g2048_deep_grad(const float* packed, const float* grad_packed, int n_hidden,
 #if G2048_DEEP_DIAG
     a.diag = g_deep_diag;
 #endif
-    const int64_t lds = deep_grad_lds_bytes(net, v.nw);
+    const int64_t lds = deep_grad_lds_bytes(net, v.nw, v.nb);
     hipStream_t s = (hipStream_t)stream;
     const int grid = (int)nparts;   // every workgroup writes its slab (zeros when it gets no group)
     if (obs_mode == G2048_OBS_ONEHOT)

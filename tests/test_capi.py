@@ -198,10 +198,10 @@ def test_deep_sizes_and_validation_without_gpu(L):
         assert lib.g2048_deep_grad_slab(obs, len(hs), arr(hs)) == -1, (obs, hs)
         assert lib.g2048_deep_grad_parts(obs, len(hs), arr(hs)) == -1, (obs, hs)
         assert lib.g2048_deep_grad_passes(obs, len(hs), arr(hs)) == -1, (obs, hs)
-    # workgroups that fill the chip: two 4-wave workgroups per CU for one-hot nets of <= 40 tiles, else one
+    # workgroups that fill the chip: one per CU (64-sample groups for one-hot nets of <= 40 tiles, round 6)
     cus = lib.g2048_deep_grad_parts(L.OBS_LOG2, 3, arr([64, 48, 32]))
     assert cus > 0
-    assert lib.g2048_deep_grad_parts(L.OBS_ONEHOT, 3, arr([256, 128, 64])) == 2 * cus
+    assert lib.g2048_deep_grad_parts(L.OBS_ONEHOT, 3, arr([256, 128, 64])) == cus
     assert lib.g2048_deep_grad_parts(L.OBS_ONEHOT, 2, arr([256, 256])) == cus
     assert lib.g2048_onehot_dw1_slab(256) == 273 * 256 and lib.g2048_onehot_dw1_slab(0) == -1
     assert lib.g2048_onehot_dw1_slab(257) == -1

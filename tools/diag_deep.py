@@ -19,6 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--episodes", type=int, default=262144)
 ap.add_argument("--lib", default="tools/libg2048_deepdiag.so")
 ap.add_argument("--label", default="")
+ap.add_argument("--nb", type=int, default=64, help="samples per gradient group of the net's instantiation")
 ap.add_argument("--rollout", action="store_true", help="stamp the rollout (deep_rollout_kernel) instead of the update")
 ap.add_argument("--rollout-waves", type=int, default=8, help="waves per rollout workgroup (8: 64 slots, 4: 32 slots)")
 args = ap.parse_args()
@@ -84,8 +85,9 @@ for rep in range(0 if args.rollout else 2):
     print(json.dumps({"label": args.label, "rep": rep, "episodes": E, "samples": int(batch.lengths.sum()),
                       "waves": int(d.shape[0]), "groups_per_wave": float(d[:, 9].mean()),
                       "cycles_per_group": round(tot),
-                      # the busiest wave's MFMAs (4-wave variant: 512 x 64 cycles), its SIMD shared with the other
-                      # workgroup's wave: 2 x that per group at 100 % MFMA
-                      "mfma_floor_cycles_per_group": 2 * 512 * 64,
+                      # the busiest SIMD's MFMA cycles per group of --nb samples (dense fp32 chains and dW tiles,
+                      # 1920 v_mfma_f32_32x32x2f32 of 64 cycles per 32 samples over 4 SIMDs, plus the layer-0 bf16
+                      # MFMAs: 65.5 k cycles per 64 samples)
+                      "mfma_floor_cycles_per_group": 65536 * args.nb // 64,
                       "phases_cycles": {p: round(v) for p, v in zip(PHASES, mean)},
                       "phases_share": {p: round(v / tot, 3) for p, v in zip(PHASES, mean)}}), flush=True)

@@ -1,11 +1,13 @@
 """TOOL: where the GPU sits idle inside a window of a rocprofv3 kernel trace (host-bound gaps between launches).
 
     rocprofv3 --kernel-trace --output-format csv -d D -o run -- python3 tools/bench_refconfig.py --episodes 1048576
-    python tools/gap_profile.py D [--after KERNEL_SUBSTR] [--last-window]
+    python tools/gap_profile.py D [--after KERNEL_SUBSTR] [--before KERNEL_SUBSTR] [--durations KERNEL_SUBSTR]
 
 The window: from the LAST dispatch whose name contains --after (default: the last update's first gradient kernel,
 'onehot_l0_mfma_kernel') to the end of the trace.  Prints the window's span, the summed dispatch time (union of
 intervals), the idle time, and the idle gaps grouped by the kernel that ends them (the host work in front of it).
+--durations: also the launches of that kernel in the window by duration bucket (count, summed time) -- how much of
+its time is in launches too short to fill the chip.
 """
 import collections
 import csv
@@ -65,6 +67,20 @@ def main():
     print("idle gaps by the kernel that ends them:")
     for n, t in gaps.most_common(15):
         print(f"  {t / 1e6:9.2f} ms in {ngaps[n]:6d} gaps  before {n}")
+    if "--durations" in sys.argv:
+        k = sys.argv[sys.argv.index("--durations") + 1]
+        edges = [0, 20, 50, 100, 200, 500, 1000, 2000, 5000, float("inf")]
+        cnt, tot = collections.Counter(), collections.Counter()
+        for s, e, n in win:
+            if k in n:
+                us = (e - s) / 1e3
+                b = next(i for i in range(len(edges) - 1) if us < edges[i + 1])
+                cnt[b] += 1
+                tot[b] += us
+        print(f"launches of {k} by duration:")
+        for b in range(len(edges) - 1):
+            if cnt[b]:
+                print(f"  {edges[b]:6.0f} - {edges[b + 1]:6.0f} us: {cnt[b]:6d} launches, {tot[b] / 1e3:9.2f} ms")
 
 
 if __name__ == "__main__":
