@@ -1029,10 +1029,13 @@ __device__ __forceinline__ void onehot_l0_tile(const float* __restrict__ P, cons
 // The same for CT column tiles of 32 boards (the 64-sample gradient groups): one fragment stream, CT B operands
 // (as deep_forward64).  (A separate function: the CT = 1 case written this way compiled to other registers and made
 // round 5's 4 x 10 gradient kernel spill 22 VGPRs.)  Two cells ahead spills 5 VGPRs and measured slower: 1.169-1.172 s
-// against 1.150-1.153 s (profiles/round6/r7p/).
+// against 1.150-1.153 s (profiles/round6/r7p/).  With `oh` (the gradient kernel's 64-sample form) the B operands come
+// from the LDS table of onehot_entry instead of the compares and selects (~20 VALU per cell and column tile): update
+// 1.133-1.138 -> 1.121-1.124 s on one box (profiles/round6/s2/).
 template <int ACT, int CT>
 __device__ __forceinline__ void onehot_l0_tile_cols(const float* __restrict__ P, const DeepNet& net, int t,
-                                               const uint64_t (&b)[CT], float* out, int stride) {
+                                               const uint64_t (&b)[CT], float* out, int stride,
+                                               const uint4* oh = nullptr) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     int tq = (int)threadIdx.x;
     asm volatile("" : "+v"(tq));   // lane ids derived here, not hoisted out of the caller's group loop
@@ -1055,6 +1058,10 @@ __device__ __forceinline__ void onehot_l0_tile_cols(const float* __restrict__ P,
 #pragma unroll
         for (int cc = 0; cc < CT; cc++) {
             const uint32_t nib = (uint32_t)(b[cc] >> (4 * c)) & 15u;
+            if (oh) {   // the table (same operand as the compares)
+                bvv[cc] = __builtin_bit_cast(bf16x8, oh[(nib << 1) | (uint32_t)h]);
+                continue;
+            }
             u32x4 dv;
 #pragma unroll
             for (int jj = 0; jj < 4; jj++)
@@ -1190,6 +1197,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     // instead of registers across the forward and delta chains (round 5: 29 -> 16 spilled VGPRs)
     float* smp_in = wol + 256 * 4 + 4;
     float* dbo_l = smp_in + 7 * NB;
+    // (64-sample form) the one-hot B-operand table (onehot_entry), as the 64-slot rollout's layer 0
+    const uint4* ohl = reinterpret_cast<const uint4*>(dbo_l + 4 * NB);
     if (tid < 256)
         for (int l = 0; l < kMaxHidden; l++) dbs[l * 256 + tid] = 0.0f;
     if (tid < 4 * NB) dbo_l[tid] = 0.0f;
@@ -1213,13 +1222,73 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
     const float4* wout = reinterpret_cast<const float4*>(wol);
     const float* bo = wol + 4 * HL;
     const uint32_t groups = (a.n + (uint32_t)(NB - 1)) / (uint32_t)NB;
+    // A group's per-sample inputs (threads 0..NB-1): board, coefficient, action, critic target or TD row.  The
+    // 64-sample form loads group g + gridDim.x's at the end of group g, ahead of g's delta_0 stores, and puts them in
+    // LDS behind those stores: the loads are older than the stores in the in-order vmcnt, so neither the next
+    // group's top nor this group's end drains the stores or waits a full load latency (the 32-sample forms load at
+    // the group's top behind a fence).  Round 6: the group top's 2.7 k cycles (of 104 k) -> 0.3 k; runner-config 1M
+    // update 1.168-1.172 -> 1.133-1.138 s on one box (profiles/round6/s2/).
+    struct GroupIn {
+        uint64_t board;
+        float cf, tg, td_r, td_h;
+        uint32_t act;
+        int64_t td_l;
+        bool valid;
+    };
+    const auto load_in = [&](uint32_t g) {
+        GroupIn v{0ull, 0.0f, 0.0f, 0.0f, 0.0f, 0u, 0, false};
+        const int t = fresh_tid();
+        if (t < NB && a.n > 0) {
+            const uint32_t j = g * (uint32_t)NB + (uint32_t)t;
+            const bool valid = j < a.n;
+            const uint32_t jc = valid ? j : a.n - 1u;
+            // every field loaded from valid memory whatever the launch's mode, then selected: no branch per mode,
+            // so the loads issue together (merged per-mode paths made the wait-count pass drain the board and
+            // coefficient loads before the action load was issued)
+            const uint8_t* pact = a.critic ? reinterpret_cast<const uint8_t*>(a.boards) : a.actions;
+            const float* ptg = a.critic && !a.has_td ? a.target : a.coef;
+            const int64_t* ptl = a.has_td ? a.td.lane : reinterpret_cast<const int64_t*>(a.boards);
+            const float* ptr = a.has_td ? a.td.reward : a.coef;
+            const float* pth = a.has_td ? a.td.has_next : a.coef;
+            // raw values here, the selects at put_in: a select next to its load would wait for the load there
+            v.board = a.boards[jc];
+            v.cf = a.coef[jc];
+            v.tg = ptg[jc];
+            v.td_r = ptr[jc];
+            v.td_h = pth[jc];
+            v.act = pact[jc];
+            v.td_l = ptl[jc];
+            v.valid = valid;
+        }
+        return v;
+    };
+    const auto put_in = [&](const GroupIn& v) {
+        const int t = fresh_tid();
+        if (t < NB) {
+            const bool use_tg = a.critic && !a.has_td;
+            const int64_t tl = a.has_td ? v.td_l : 0;
+            bds[t] = v.valid ? v.board : 0ull;
+            smp_in[t] = v.valid ? v.cf : 0.0f;
+            smp_in[NB + t] = __uint_as_float(a.critic ? 0u : v.act);
+            smp_in[2 * NB + t] = use_tg ? v.tg : 0.0f;
+            smp_in[3 * NB + t] = a.has_td ? v.td_r : 0.0f;
+            smp_in[4 * NB + t] = a.has_td ? v.td_h : 0.0f;
+            smp_in[5 * NB + t] = __uint_as_float((uint32_t)tl);
+            smp_in[6 * NB + t] = __uint_as_float((uint32_t)((uint64_t)tl >> 32));
+        }
+    };
+    if constexpr (NB == 64) {
+        if (tid < 32) const_cast<uint4*>(ohl)[tid] = onehot_entry((uint32_t)tid);
+        put_in(load_in(blockIdx.x));
+        __syncthreads();   // (also orders the LDS initialisation above)
+    }
 #if G2048_DEEP_DIAG
     uint64_t dph[kDiagSlots] = {};
     uint64_t dlast = __builtin_amdgcn_s_memtime();
 #endif
     for (uint32_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
         float td_v = 0.0f;   // V(s') of the critic's TD row (loaded after layer 0, used at the logits)
-        {
+        if constexpr (NB != 64) {
             DEEP_LANE_IDS;
             const uint32_t j = gi * (uint32_t)NB + (uint32_t)(tid & (NB - 1));
             const bool valid = j < a.n;
@@ -1265,7 +1334,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     uint64_t bc[CT];
 #pragma unroll
                     for (int cc = 0; cc < CT; cc++) bc[cc] = bds[32 * cc + col];
-                    for (int t = w; t < nt0; t += NW) onehot_l0_tile_cols<ACT, CT>(P, net, t, bc, out, SS);
+                    for (int t = w; t < nt0; t += NW) onehot_l0_tile_cols<ACT, CT>(P, net, t, bc, out, SS, ohl);
                 }
             } else {
                 const uint64_t b = bds[col];
@@ -1560,7 +1629,37 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
         // ---- first layer's weight gradient
         {
             DEEP_LANE_IDS;
-            if constexpr (OBS == G2048_OBS_ONEHOT) {
+            if constexpr (NB == 64) {
+                // (one launch: last_pass) the next group's inputs first (see load_in), then delta_0 out for the
+                // one-hot dW1 over all 8 waves: thread (unit u, half hf) stores rows 32 hf .. 32 hf + 31 of unit u.
+                // Through a buffer resource over the group's rows: rows past a ragged group's end, and threads past
+                // 2 H0, fall outside num_records (the row offset runs in the VGPR offset, one add per store).
+                const GroupIn nx = load_in(gi + gridDim.x);
+                const int H0 = 32 * net.nt[0];
+                const int hf = tid >= H0 ? 1 : 0, u = tid - hf * H0;
+                const bool live = tid < 2 * H0;
+                const float* drow = actl(0) + (live ? u : 0) * SS + 32 * hf;
+                const uint32_t left = a.n - gi * (uint32_t)NB < (uint32_t)NB ? a.n - gi * (uint32_t)NB : (uint32_t)NB;
+                const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                    a.d0_out + (size_t)gi * (uint32_t)NB * (uint32_t)H0, 0, (int)(left * (uint32_t)H0 * 4u), 0x00020000);
+                const int rowb = __builtin_amdgcn_readfirstlane(H0 * 4);
+                int vo = live ? (u + 32 * hf * H0) * 4 : 0x40000000;
+#pragma unroll
+                for (int n0 = 0; n0 < 32; n0 += 8) {
+                    float v[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) v[i] = drow[n0 + i];
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);   // the 4 ds_read2 first
+                    __builtin_amdgcn_sched_group_barrier(0x040, 8, 0);   // then the 8 stores
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), rd, vo, 0, 0);
+                        vo += rowb;
+                        asm volatile("" : "+v"(vo));   // one running offset, not 32 hoisted constants
+                    }
+                }
+                put_in(nx);
+            } else if constexpr (OBS == G2048_OBS_ONEHOT) {
                 // delta_0 out for the one-hot dW1 (g2048_onehot_dw1): row j, unit tid (coalesced rows) -- by the last
                 // launch of a multi-launch net only (each launch recomputes the same rows)
                 const int H0 = 32 * net.nt[0];
@@ -1765,7 +1864,7 @@ int64_t deep_grad_act_floats(const DeepNet& n, int nw, int nb = 32) {
 // + part, g, boards, bias sums, output weights / bias, the per-sample inputs, the db_out sums
 int64_t deep_grad_lds_bytes(const DeepNet& n, int nw, int nb = 32) {
     return (deep_grad_act_floats(n, nw, nb) + 8 * nb * 4 + nb * 4 + 2 * nb + kMaxHidden * 256 + 256 * 4 + 4 +
-            7 * nb + nb * 4) * 4;
+            7 * nb + nb * 4 + (nb == 64 ? 32 * 4 : 0)) * 4;
 }
 
 // the instantiation that covers the net (nw = 0: none; see deep_grad_kernel).  The 4-wave and the 64-tile ones are
