@@ -224,7 +224,10 @@ struct DeepSmem {
 // four L2 round trips per k-tile.)  The B operands run one segment (4 k-steps) ahead: the next segment's two
 // ds_read2 are issued before this segment's MFMAs, so no segment waits for LDS reads issued next to its own first
 // MFMA (round 6: runner-config update 1.215 -> 1.179 s, rollout 0.252 -> 0.240 s, `profiles/round6/r7h/`).  Same
-// MFMAs in the same order as a plain loop.
+// MFMAs in the same order as a plain loop.  (Also round 6, in the 64-sample gradient kernel: k-tile 0's fragments of
+// each wave's first item loaded before the barrier that opens the phase -- 92 spilled SGPRs, update 1.259-1.264 s
+// against 1.119-1.123 s; the hidden biases staged in LDS for the epilogues -- 1.119-1.120 s, even; neither kept,
+// `profiles/round6/s3/`.)
 template <int STRIDE = kActStride>
 __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, const float* in, int t0, int t1, int h,
                                                int col) {
