@@ -798,7 +798,13 @@ __device__ __forceinline__ void store_stream(uint64_t* rs, uint64_t* buf, uint32
 constexpr uint32_t kNoEpisode = 0xFFFFFFFFu;
 
 // NB = 32: 4-wave workgroups, two per CU, deep_forward; NB = 64 (one-hot nets): one 8-wave workgroup per CU,
-// deep_forward64 (above).  Slot owners: lanes 0 .. NB - 1 of wave 0.
+// deep_forward64 (above).  Slot owners: lanes 0 .. NB - 1 of wave 0.  Their phase is ~6.9 k of a step's ~47 k
+// cycles at 64 slots (the other waves wait for it at the step's first barrier; round 6 stamps, profiles/round6/s5/:
+// logits + choice 2.2 k, env step 2.5 k, trajectory row 0.5 k, claim 1.3 k).  Tried in round 6 and not kept
+// (runner config, 1M episodes, interleaved on one box, profiles/round6/s6/, s7/): all four actions' row-table reads
+// issued before the choice (32 scattered loads per lane: logits + choice 2.2 k -> 6.5 k cycles, rollout 0.241 ->
+// 0.263 s); the move by line_move_alu instead of the tables (env step 2.5 k -> 3.0 k, 0.241 -> 0.243 s); the output
+// bias from LDS and the fp64 division of k = 3 skipped (0.241 -> 0.242 s).
 template <int OBS, int ACT, int NB>
 __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(DeepRollArgs a) {
     static_assert(NB == 32 || (NB == 64 && OBS == G2048_OBS_ONEHOT), "64 slots: one-hot nets");
@@ -901,7 +907,12 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
             const double u = a.greedy ? 0.0 : pcg_random(gp);
             float p[4];
             const uint32_t act = softmax_select(lg, mw, a.use_mask != 0, a.greedy != 0, u, p);
+            FWD_STAMP(dc, 6);
             const StepValues ov = env_step_pcg(b, act, sc, mt, ge, a.rc, a.max_steps, lut, code);
+#if G2048_DEEP_DIAG
+            asm volatile("" ::"v"(ov.board), "v"(ov.reward), "v"(ov.flags));
+#endif
+            FWD_STAMP(dc, 7);
             const size_t row = (size_t)t * a.n + ep;
             a.tr.boards[row] = b;
             a.tr.actions[row] = (uint8_t)act;
@@ -928,6 +939,7 @@ __global__ void __launch_bounds__(NB * 8, NB == 64 ? 1 : 2) deep_rollout_kernel(
                 a.sus.list[atomicAdd(a.sus.count, 1u)] = (int32_t)ep;
                 ep = kNoEpisode;
             }
+            FWD_STAMP(dc, 8);
         }
         FWD_STAMP(dc, 4);
         if (tid < 64) claim();

@@ -48,7 +48,8 @@ lib.g2048_diag_deep_stamps.argtypes = [ctypes.c_void_p]
 slots = 4096 * 10
 buf = torch.zeros(slots, dtype=torch.int64, device=dev)
 E = args.episodes
-RPHASES = ["top+boards", "layer0", "dense", "out_partials", "owners", "claim"]
+RPHASES = ["top+boards", "layer0", "dense", "out_partials", "owners_rest", "claim", "owner_logits_choice",
+           "owner_env_step", "owner_row_stores"]
 for rep in range(2 if args.rollout else 0):
     # deep_rollout_kernel: per step of a workgroup, wave 0 (whose lanes own the episode slots: logits, choice, env
     # step, trajectory row) and the other waves (which wait for it at the next step's first barrier)
@@ -65,7 +66,7 @@ for rep in range(2 if args.rollout else 0):
     out = {"label": args.label, "rep": rep, "episodes": E, "steps": int(batch.lengths.sum()), "workgroups": int(d.shape[0]),
            "steps_per_workgroup": float(d[:, 0, 9].mean())}
     for name, ws in (("wave0", [0]), ("waves1_%d" % (W - 1), list(range(1, W)))):
-        per = (d[:, ws, :6] / d[:, ws, 9:10]).reshape(-1, 6).mean(axis=0)
+        per = (d[:, ws, :9] / d[:, ws, 9:10]).reshape(-1, 9).mean(axis=0)
         out[name] = {"cycles_per_step": round(per.sum()), "phases_cycles": {p: round(v) for p, v in zip(RPHASES, per)}}
     print(json.dumps(out), flush=True)
 for rep in range(0 if args.rollout else 2):
