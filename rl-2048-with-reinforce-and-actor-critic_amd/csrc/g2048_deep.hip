@@ -1615,6 +1615,22 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
             float* Aw = actl(l - 1);
             for (int i = w; i < CT * ntin; i += NW) {
                 const int o = i >> (CT - 1), cc = i & (CT - 1);
+                if constexpr (ACT == 0 && NB == 64) {
+                    // ReLU: act'(a) read as a 16-bit mask BEFORE the chain (its LDS reads under the chain's first
+                    // fragment loads, not after its last MFMA), then only the stores after it -- the same products
+                    // c * 1 or c * 0 (round 6: update 1.120-1.124 -> 1.115-1.118 s on one box, profiles/round6/s8/;
+                    // the 64-unit layer's forward as two half-k chains on all 8 waves measured slower there:
+                    // 1.126-1.132 s)
+                    uint32_t pos = 0;
+#pragma unroll
+                    for (int r = 0; r < 16; r++)
+                        pos |= (Aw[(32 * o + tile_row(r, h)) * SS + 32 * cc + col] > 0.0f ? 1u : 0u) << r;
+                    const floatx16 c = frag_chain<SS>(frag + (int64_t)o * ntout * 256, D + 32 * cc, 0, ntout, h, col);
+#pragma unroll
+                    for (int r = 0; r < 16; r++)
+                        Aw[(32 * o + tile_row(r, h)) * SS + 32 * cc + col] = c[r] * (((pos >> r) & 1u) ? 1.0f : 0.0f);
+                    continue;
+                }
                 const floatx16 c = frag_chain<SS>(frag + (int64_t)o * ntout * 256, D + 32 * cc, 0, ntout, h, col);
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
