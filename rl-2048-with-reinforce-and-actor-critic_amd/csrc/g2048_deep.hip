@@ -362,7 +362,7 @@ __device__ __forceinline__ uint4 onehot_entry(uint32_t idx) {
 
 // Tools-only phase clock (-DG2048_DEEP_DIAG=1 builds; see deep_grad_kernel's DEEP_STAMP): deep_forward stamps its
 // layer phases into it when the caller passes one (the rollout kernel), an empty type in the product.
-constexpr int kDiagSlots = 10;
+constexpr int kDiagSlots = 15;
 #if G2048_DEEP_DIAG
 struct DiagClock {
     uint64_t ph[kDiagSlots];
@@ -1405,8 +1405,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 }
             }
             lds_barrier();
+            DEEP_STAMP(l == 1 ? 2 : 9);
         }
-        DEEP_STAMP(2);
         // ---- output layer partials (as deep_forward; threads 0..255).  (Round 6: the same sums from the last dense
         //      layer's epilogue registers, the chain handed across the lane halves -- same bits, no pass and barrier
         //      here -- measured 0.4 % slower: the epilogue lengthens the 2-tile layer's waves while the pass here
@@ -1609,7 +1609,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 }
             }
             lds_barrier();                               // every read of a_{l-1} by the dW tiles is done
-            DEEP_STAMP(6);
+            DEEP_STAMP(l == L - 1 ? 6 : 10);
             // delta_{l-1} = (W_l delta_l) act'(a_{l-1}): output tiles = layer l-1's units, k = layer l's units
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(a.bpacked + a.boff[l]) + lane;
             float* Aw = actl(l - 1);
@@ -1639,6 +1639,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 }
             }
             lds_barrier();
+            DEEP_STAMP(l == L - 1 ? 11 : 12);
             // db_{l-1} of unit tid
             if (tid < 32 * ntin) {
                 const float* drow = Aw + tid * SS;
@@ -1655,7 +1656,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                 }
                 dbs[(l - 1) * 256 + tid] = db;
             }
-            DEEP_STAMP(7);
+            DEEP_STAMP(l == L - 1 ? 7 : 13);
         }
         // ---- first layer's weight gradient
         {

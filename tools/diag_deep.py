@@ -40,12 +40,16 @@ MLP = dict(hidden_sizes=[256, 128, 64], activation="ReLU", init_distribution="He
 AGENT = dict(gamma=0.99, learning_rate=0.01, baseline_mode="batch", model_seed=0, reward_rank_weights=None,
              optimizer="adam", adam_beta1=0.9, adam_beta2=0.999, augmentation=False, use_critic=True,
              critic_learning_rate=0.0005, critic_loss_type="mse", huber_delta=1.0)
-PHASES = ["boards", "layer0", "dense_fwd", "out_partials", "logits_g", "out_bwd", "dW", "delta+db", "first_layer_out"]
+NS = 15   # kDiagSlots (g2048_deep.hip): the last slot counts groups / steps
+# gradient kernel slots: the top dense layer's dW / delta / db and the lower layers' apart, the first dense layer's
+# forward and the deeper ones' apart
+PHASES = ["boards", "layer0", "dense_fwd_l1", "out_partials", "logits_g", "out_bwd", "dW_top", "db_top",
+          "first_layer_out", "dense_fwd_l2+", "dW_lower", "delta_top", "delta_lower", "db_lower"]
 dev = torch.device("cuda", 0)
 agent = ReinforceAgent(Game2048EnvConfig(**ENV), MLPConfig(**MLP), ReinforceAgentConfig(**AGENT), device=dev)
 lib = L.lib()
 lib.g2048_diag_deep_stamps.argtypes = [ctypes.c_void_p]
-slots = 4096 * 10
+slots = 4096 * NS
 buf = torch.zeros(slots, dtype=torch.int64, device=dev)
 E = args.episodes
 RPHASES = ["top+boards", "layer0", "dense", "out_partials", "owners_rest", "claim", "owner_logits_choice",
@@ -61,12 +65,12 @@ for rep in range(2 if args.rollout else 0):
     torch.cuda.synchronize()
     lib.g2048_diag_deep_stamps(None)
     W = args.rollout_waves
-    d = buf.view(-1, W, 10).cpu().numpy().astype(np.float64)
-    d = d[d[:, 0, 9] > 0]
+    d = buf.view(-1, W, NS).cpu().numpy().astype(np.float64)
+    d = d[d[:, 0, NS - 1] > 0]
     out = {"label": args.label, "rep": rep, "episodes": E, "steps": int(batch.lengths.sum()), "workgroups": int(d.shape[0]),
-           "steps_per_workgroup": float(d[:, 0, 9].mean())}
+           "steps_per_workgroup": float(d[:, 0, NS - 1].mean())}
     for name, ws in (("wave0", [0]), ("waves1_%d" % (W - 1), list(range(1, W)))):
-        per = (d[:, ws, :9] / d[:, ws, 9:10]).reshape(-1, 9).mean(axis=0)
+        per = (d[:, ws, :9] / d[:, ws, NS - 1:NS]).reshape(-1, 9).mean(axis=0)
         out[name] = {"cycles_per_step": round(per.sum()), "phases_cycles": {p: round(v) for p, v in zip(RPHASES, per)}}
     print(json.dumps(out), flush=True)
 for rep in range(0 if args.rollout else 2):
@@ -78,13 +82,13 @@ for rep in range(0 if args.rollout else 2):
     agent.update_from_batch(batch)
     torch.cuda.synchronize()
     lib.g2048_diag_deep_stamps(None)
-    d = buf.view(-1, 10).cpu().numpy().astype(np.float64)
-    d = d[d[:, 9] > 0]
-    per = d[:, :9] / d[:, 9:10]                      # cycles per group, per wave
+    d = buf.view(-1, NS).cpu().numpy().astype(np.float64)
+    d = d[d[:, NS - 1] > 0]
+    per = d[:, :NS - 1] / d[:, NS - 1:NS]                      # cycles per group, per wave
     mean = per.mean(axis=0)
     tot = mean.sum()
     print(json.dumps({"label": args.label, "rep": rep, "episodes": E, "samples": int(batch.lengths.sum()),
-                      "waves": int(d.shape[0]), "groups_per_wave": float(d[:, 9].mean()),
+                      "waves": int(d.shape[0]), "groups_per_wave": float(d[:, NS - 1].mean()),
                       "cycles_per_group": round(tot),
                       # the busiest SIMD's MFMA cycles per group of --nb samples (dense fp32 chains and dW tiles,
                       # 1920 v_mfma_f32_32x32x2f32 of 64 cycles per 32 samples over 4 SIMDs, plus the layer-0 bf16
