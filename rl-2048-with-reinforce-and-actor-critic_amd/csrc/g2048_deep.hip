@@ -281,6 +281,59 @@ __device__ __forceinline__ floatx16 frag_chain(const float4* __restrict__ fo, co
     return c;
 }
 
+// frag_chain over k-tiles [0, nt) with k-tile 0's fragments carried across a wave's items: fa holds k-tile 0 of `fo`
+// on entry, and its window reload past the end fetches k-tile 0 of `fo_next` (the wave's next item; NULL: the last
+// k-tile again) -- so the next item's first MFMAs do not wait an L2 round trip behind this item's epilogue.  The
+// same MFMAs in the same order as frag_chain(fo, in, 0, nt, h, col).
+template <int STRIDE = kActStride>
+__device__ __forceinline__ floatx16 frag_chain_carry(const float4* __restrict__ fo, const float* in, int nt, int h,
+                                                     int col, float4 (&fa)[4], const float4* __restrict__ fo_next) {
+    floatx16 c = {};
+    float4 fb[4];
+    const int last = nt - 1;
+    const float* base = in + 4 * h * STRIDE + col;
+    const auto ld4 = [&](float (&v)[4], int t, int q) {
+        const float* ib = base + (32 * t + 8 * q) * STRIDE;
+        v[0] = ib[0 * STRIDE];
+        v[1] = ib[1 * STRIDE];
+        v[2] = ib[2 * STRIDE];
+        v[3] = ib[3 * STRIDE];
+    };
+    float bc[4], bn[4];
+    ld4(bc, 0, 0);
+    const auto seg = [&](float4& f, int t, int q, const float4* nf) {
+        ld4(bn, q < 3 ? t : (t + 1 < nt ? t + 1 : last), (q + 1) & 3);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, bc[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, bc[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, bc[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, bc[3], c, 0, 0, 0);
+        f = nf[q * 64];
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; i++) bc[i] = bn[i];
+    };
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; q++) fb[q] = fo[(nt > 1 ? 256 : 0) + q * 64];   // k-tile 1 (needed 16 MFMAs later)
+    int t = 0;
+    for (; t + 1 < nt; t += 2) {
+        const float4* na = t + 2 < nt ? fo + (t + 2) * 256 : (fo_next ? fo_next : fo + last * 256);
+        const float4* nb = t + 3 < nt ? fo + (t + 3) * 256 : fo + last * 256;
+#pragma unroll
+        for (int q = 0; q < 4; q++) seg(fa[q], t, q, na);
+#pragma unroll
+        for (int q = 0; q < 4; q++) seg(fb[q], t + 1, q, nb);
+    }
+    if (t < nt) {   // odd nt: the last k-tile from fa, which then takes the next item's k-tile 0
+#pragma unroll
+        for (int q = 0; q < 4; q++) seg(fa[q], t, q, fo_next ? fo_next : fo + last * 256);
+    }
+    return c;
+}
+
 // One dense hidden layer (in -> out, [unit][board] stride kActStride) whose k range is split in two halves when it
 // has fewer output tiles than 8 (the gradient kernel's waves) and at least 2 k-tiles: output tile o is
 // act(fl(c0 + c1) + b) with c0 / c1 the k-ordered MFMA chains over k-tiles [0, ntin/2) and [ntin/2, ntin) -- the
@@ -1608,29 +1661,48 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) deep_grad_kernel(DeepGradArgs
                     acc[k] = c;
                 }
             }
-            lds_barrier();                               // every read of a_{l-1} by the dW tiles is done
-            DEEP_STAMP(l == L - 1 ? 6 : 10);
             // delta_{l-1} = (W_l delta_l) act'(a_{l-1}): output tiles = layer l-1's units, k = layer l's units
             const float4* __restrict__ frag = reinterpret_cast<const float4*>(a.bpacked + a.boff[l]) + lane;
             float* Aw = actl(l - 1);
-            for (int i = w; i < CT * ntin; i += NW) {
-                const int o = i >> (CT - 1), cc = i & (CT - 1);
-                if constexpr (ACT == 0 && NB == 64) {
-                    // ReLU: act'(a) read as a 16-bit mask BEFORE the chain (its LDS reads under the chain's first
-                    // fragment loads, not after its last MFMA), then only the stores after it -- the same products
-                    // c * 1 or c * 0 (round 6: update 1.120-1.124 -> 1.115-1.118 s on one box, profiles/round6/s8/;
-                    // the 64-unit layer's forward as two half-k chains on all 8 waves measured slower there:
-                    // 1.126-1.132 s)
+            // (64-sample form, ReLU) k-tile 0's fragments of the wave's first item, loaded before the barrier below
+            // (in flight across it: update 1.121-1.123 -> 1.116-1.118 s on one box, profiles/round6/s12/; the same
+            // for the dense forward's first chains -- after layer 0 / before each layer's barrier -- measured much
+            // slower, 1.177 against 1.115-1.117 s, s13/, as in s3/)
+            float4 fa[4];
+            const auto load_fa = [&]() {
+                if (w < CT * ntin) {
+                    const float4* f0 = frag + (int64_t)(w >> (CT - 1)) * ntout * 256;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) fa[q] = f0[q * 64];
+                }
+            };
+            if constexpr (ACT == 0 && NB == 64) load_fa();
+            lds_barrier();                               // every read of a_{l-1} by the dW tiles is done
+            DEEP_STAMP(l == L - 1 ? 6 : 10);
+            if constexpr (ACT == 0 && NB == 64) {
+                // ReLU, 64-sample form (round 6): per item act'(a) read as a 16-bit mask BEFORE the chain (its LDS
+                // reads under the chain's first fragment loads, not after its last MFMA), then only the stores after
+                // it -- the same products c * 1 or c * 0 (update 1.120-1.124 -> 1.115-1.118 s on one box,
+                // profiles/round6/s8/); and k-tile 0's fragments carried from one item of the wave to the next
+                // (frag_chain_carry: 1.112-1.113 -> 1.105-1.107 s, s11/).  (The 64-unit layer's forward as two
+                // half-k chains on all 8 waves measured slower, 1.126-1.132 s, s8/.)
+                for (int i = w; i < CT * ntin; i += NW) {
+                    const int o = i >> (CT - 1), cc = i & (CT - 1);
                     uint32_t pos = 0;
 #pragma unroll
                     for (int r = 0; r < 16; r++)
                         pos |= (Aw[(32 * o + tile_row(r, h)) * SS + 32 * cc + col] > 0.0f ? 1u : 0u) << r;
-                    const floatx16 c = frag_chain<SS>(frag + (int64_t)o * ntout * 256, D + 32 * cc, 0, ntout, h, col);
+                    const int inext = i + NW;
+                    const float4* fnext = inext < CT * ntin ? frag + (int64_t)(inext >> (CT - 1)) * ntout * 256 : nullptr;
+                    const floatx16 c = frag_chain_carry<SS>(frag + (int64_t)o * ntout * 256, D + 32 * cc, ntout, h, col,
+                                                            fa, fnext);
 #pragma unroll
                     for (int r = 0; r < 16; r++)
                         Aw[(32 * o + tile_row(r, h)) * SS + 32 * cc + col] = c[r] * (((pos >> r) & 1u) ? 1.0f : 0.0f);
-                    continue;
                 }
+            } else
+            for (int i = w; i < CT * ntin; i += NW) {
+                const int o = i >> (CT - 1), cc = i & (CT - 1);
                 const floatx16 c = frag_chain<SS>(frag + (int64_t)o * ntout * 256, D + 32 * cc, 0, ntout, h, col);
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
